@@ -1,0 +1,358 @@
+"""ctypes binding of libcaldera_hip.so (include/caldera_hip.h) + thin torch-tensor wrappers.
+
+PyTorch is plumbing here: it owns device memory (caching allocator workspaces), the HIP
+stream (`torch.cuda.current_stream().cuda_stream`) and RNG.  Every arithmetic step of the
+hot path goes through one of the C-ABI entry points below; there is no torch or CPU
+fallback — a missing library or a non-HIP tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcaldera_hip.so")
+
+CQ_F32, CQ_F16 = 0, 1
+EPI_LINEAR, EPI_RESID, EPI_WERR = 0, 1, 2
+CQ_EINVAL, CQ_EHIP, CQ_EWORKSPACE = -1, -2, -3
+
+c_i64, c_int, c_float, c_double, c_size, c_vp = (ctypes.c_int64, ctypes.c_int, ctypes.c_float,
+                                                 ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64), ("batch", c_i64),
+        ("trans_a", c_int), ("trans_b", c_int),
+        ("A", c_vp), ("lda", c_i64), ("stride_a", c_i64),
+        ("B", c_vp), ("ldb", c_i64), ("stride_b", c_i64),
+        ("C", c_vp), ("ldc", c_i64), ("stride_c", c_i64),
+        ("D", c_vp), ("ldd", c_i64), ("stride_d", c_i64), ("d_f16", c_int),
+        ("alpha", c_float), ("beta", c_float), ("gamma", c_float),
+        ("alpha_v", c_vp), ("beta_v", c_vp), ("gamma_v", c_vp),
+        ("epi", c_int),
+        ("absmax_bits", c_vp),
+        ("w", c_vp), ("stride_w", c_i64),
+        ("err_out", c_vp),
+    ]
+
+
+_SIGS = {
+    "cq_abi_version": (c_int, []),
+    "cq_last_error": (ctypes.c_char_p, []),
+    "cq_rms_scale_workspace": (c_size, [c_i64, c_i64]),
+    "cq_rms_scale": (c_int, [c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_quantize_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_quantize_uniform": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+    "cq_quantize_uniform_known_max": (c_int, [c_vp, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp,
+                                              c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+    "cq_unpack_codes": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "cq_dequant_uniform": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "cq_build_residual": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp,
+                                  c_vp, c_vp]),
+    "cq_gemm_workspace": (c_size, [ctypes.POINTER(GemmArgs)]),
+    "cq_gemm_f32": (c_int, [ctypes.POINTER(GemmArgs), c_vp, c_size, c_vp]),
+    "cq_gram_f64_workspace": (c_size, [c_i64, c_i64, c_i64, c_i64]),
+    "cq_gram_f64": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_int, c_i64, c_i64, c_vp, c_int, c_i64,
+                            c_i64, c_vp, c_vp, c_size, c_vp]),
+    "cq_spd_whiten": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
+    "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_size, c_vp]),
+    "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
+                                 c_vp]),
+    "cq_weighted_sqsum": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+    "cq_scale_rc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
+                            c_i64, c_vp, c_i64, c_vp]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libcaldera_hip.so and declare every export (no device calls)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.cq_abi_version() != 1:
+        raise RuntimeError("libcaldera_hip.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+class CalderaHipError(RuntimeError):
+    pass
+
+
+def _check(st: int, what: str):
+    if st != 0:
+        msg = load().cq_last_error().decode(errors="replace")
+        if st == CQ_EINVAL:
+            if "Bit-width not supported" in msg:
+                raise AssertionError("Bit-width not supported!")
+            raise ValueError(f"{what}: {msg}")
+        raise CalderaHipError(f"{what}: status {st}: {msg}")
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _require_hip(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("caldera-mi355x kernels need HIP device tensors (no CPU fallback)")
+
+
+def workspace(nbytes: int, dev) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+
+
+# ---------------------------------------------------------------------------- wrappers
+def rms_scale(W: torch.Tensor, do_scale: bool):
+    """W (B, m, n) fp16/fp32 -> (gs (B,) fp32, Ws same dtype).  alg.py:38-42."""
+    _require_hip(W)
+    W = W.contiguous()
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[W.dtype]
+    B = W.shape[0]
+    numel = W[0].numel()
+    gs = torch.empty(B, dtype=torch.float32, device=W.device)
+    Ws = torch.empty_like(W)
+    lib = load()
+    ws = workspace(lib.cq_rms_scale_workspace(B, numel), W.device)
+    _check(lib.cq_rms_scale(dt, _p(W), B, numel, int(bool(do_scale)), _p(gs), _p(Ws), _p(ws), ws.numel(),
+                            _stream(W.device)), "cq_rms_scale")
+    return gs, Ws
+
+
+def weighted_sqsum(x: torch.Tensor, w: torch.Tensor | None, ncols: int) -> torch.Tensor:
+    _require_hip(x, w)
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[x.dtype]
+    B = x.shape[0]
+    numel = x[0].numel()
+    out = torch.empty(B, dtype=torch.float64, device=x.device)
+    lib = load()
+    ws = workspace(lib.cq_rms_scale_workspace(B, numel), x.device)
+    _check(lib.cq_weighted_sqsum(dt, _p(x), B, numel, _p(w), ncols, _p(out), _p(ws), ws.numel(),
+                                 _stream(x.device)), "cq_weighted_sqsum")
+    return out
+
+
+def code_dtype(bits: int):
+    return torch.int8 if bits <= 8 else torch.int16
+
+
+def quantize_uniform(x: torch.Tensor, block_size: int, bits: int, eps: float = 1e-8, *,
+                     codes=True, packed=False, deq=True, err_w=None, err_ncols=1, want_err=False):
+    """x (B, numel) fp32 contiguous.  quantization.py:244-269 / :290-307 (uniform)."""
+    _require_hip(x, err_w)
+    assert x.dtype == torch.float32 and x.is_contiguous()
+    B, numel = x.shape
+    dev = x.device
+    out = {}
+    out["codes"] = torch.empty((B, numel), dtype=code_dtype(bits), device=dev) if codes else None
+    out["packed"] = (torch.empty((B, numel * bits // 8), dtype=torch.uint8, device=dev)
+                     if packed and bits <= 4 else None)
+    out["deq"] = torch.empty((B, numel), dtype=torch.float32, device=dev) if deq else None
+    out["scale"] = torch.empty((B, numel // block_size), dtype=torch.float32, device=dev)
+    out["err"] = torch.empty(B, dtype=torch.float64, device=dev) if (want_err or err_w is not None) else None
+    lib = load()
+    ws = workspace(lib.cq_quantize_workspace(B, numel, block_size), dev)
+    _check(lib.cq_quantize_uniform(_p(x), B, numel, block_size, bits, eps, _p(out["codes"]),
+                                   _p(out["packed"]), _p(out["deq"]), _p(out["scale"]), _p(err_w),
+                                   err_ncols, _p(out["err"]), _p(ws), ws.numel(), _stream(dev)),
+           "cq_quantize_uniform")
+    return out
+
+
+def quantize_known_max(x, absmax_bits, bits, eps=1e-8, *, codes=None, packed=None, deq=None,
+                       scale=None, err_w=None, err_ncols=1, err_out=None):
+    _require_hip(x)
+    B = x.shape[0]
+    numel = x[0].numel()
+    lib = load()
+    ws = workspace(lib.cq_quantize_workspace(B, numel, numel), x.device)
+    _check(lib.cq_quantize_uniform_known_max(_p(x), B, numel, bits, eps, _p(absmax_bits), _p(codes),
+                                             _p(packed), _p(deq), _p(scale), _p(err_w), err_ncols,
+                                             _p(err_out), _p(ws), ws.numel(), _stream(x.device)),
+           "cq_quantize_uniform_known_max")
+
+
+def dequantize_uniform(codes: torch.Tensor, scale: torch.Tensor, bits: int, packed: bool = False,
+                       numel: int | None = None) -> torch.Tensor:
+    """(float(c)/k) * scale per block; codes (..., ) int8/int16 or packed uint8; scale (nblocks,)."""
+    _require_hip(codes, scale)
+    total = numel if numel is not None else codes.numel()
+    nb = scale.numel()
+    out = torch.empty(total, dtype=torch.float32, device=codes.device)
+    _check(load().cq_dequant_uniform(_p(codes), int(packed), _p(scale), total, total // nb, bits, _p(out),
+                                     _stream(codes.device)), "cq_dequant_uniform")
+    return out
+
+
+def unpack_codes(packed: torch.Tensor, numel: int, bits: int) -> torch.Tensor:
+    _require_hip(packed)
+    B = packed.shape[0]
+    codes = torch.empty((B, numel), dtype=torch.int8, device=packed.device)
+    _check(load().cq_unpack_codes(_p(packed), B, numel, bits, _p(codes), _stream(packed.device)),
+           "cq_unpack_codes")
+    return codes
+
+
+def build_residual(Ws, qcodes, qscale, bits, ycol, Y=None, res=None):
+    """Y = (Ws - deq(Q)) * ycol[col];  res = Ws - deq(Q).  alg.py:124 + :211 (diagonal H)."""
+    _require_hip(Ws, qcodes, qscale, ycol, Y, res)
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[Ws.dtype]
+    B, m, n = Ws.shape
+    _check(load().cq_build_residual(dt, _p(Ws), _p(qcodes), _p(qscale), bits, _p(ycol), B, m, n,
+                                    _p(Y), _p(res), _stream(Ws.device)), "cq_build_residual")
+
+
+def _mat(t: torch.Tensor):
+    """(tensor (B, r, c) or (r, c) with unit column stride) -> (ptr, ld, batch_stride)."""
+    if t.dim() == 2:
+        assert t.stride(1) == 1
+        return t, t.stride(0), 0
+    assert t.dim() == 3 and t.stride(2) == 1, "matrices must have unit column stride"
+    return t, t.stride(1), (t.stride(0) if t.shape[0] > 1 else 0)
+
+
+def gemm(A, B, *, ta=False, tb=False, C=None, alpha=1.0, beta=0.0, D=None, gamma=0.0,
+         epi=EPI_LINEAR, absmax=None, w=None, err_out=None, alpha_v=None, beta_v=None,
+         gamma_v=None, batch=None):
+    """Batched C = alpha op(A) op(B) + beta C + gamma D (or RESID / WERR epilogues)."""
+    _require_hip(A, B, C, D, w)
+    A_, lda, sa = _mat(A)
+    B_, ldb, sb = _mat(B)
+    M = A.shape[-1] if ta else A.shape[-2]
+    K = A.shape[-2] if ta else A.shape[-1]
+    N = B.shape[-2] if tb else B.shape[-1]
+    Kb = B.shape[-1] if tb else B.shape[-2]
+    assert K == Kb, f"gemm: inner dims {K} vs {Kb}"
+    if batch is None:
+        batch = max(t.shape[0] if t is not None and t.dim() == 3 else 1 for t in (A, B, C, D))
+    g = GemmArgs()
+    g.M, g.N, g.K, g.batch = M, N, K, batch
+    g.trans_a, g.trans_b = int(ta), int(tb)
+    g.A, g.lda, g.stride_a = A_.data_ptr(), lda, sa
+    g.B, g.ldb, g.stride_b = B_.data_ptr(), ldb, sb
+    if C is not None:
+        C_, ldc, sc = _mat(C)
+        assert C.shape[-2] == M and C.shape[-1] == N
+        g.C, g.ldc, g.stride_c = C_.data_ptr(), ldc, sc
+    if D is not None:
+        D_, ldd, sd = _mat(D)
+        assert D.shape[-2] == M and D.shape[-1] == N, f"D shape {tuple(D.shape)} vs {(M, N)}"
+        g.D, g.ldd, g.stride_d, g.d_f16 = D_.data_ptr(), ldd, sd, int(D.dtype == torch.float16)
+        if D.dtype not in (torch.float16, torch.float32):
+            raise TypeError("D must be fp16/fp32")
+    g.alpha, g.beta, g.gamma = alpha, beta, gamma
+    g.alpha_v = alpha_v.data_ptr() if alpha_v is not None else None
+    g.beta_v = beta_v.data_ptr() if beta_v is not None else None
+    g.gamma_v = gamma_v.data_ptr() if gamma_v is not None else None
+    g.epi = epi
+    g.absmax_bits = absmax.data_ptr() if absmax is not None else None
+    if w is not None:
+        g.w = w.data_ptr()
+        g.stride_w = w.shape[-1] if (w.dim() == 2 and w.shape[0] > 1) else 0
+    g.err_out = err_out.data_ptr() if err_out is not None else None
+    lib = load()
+    dev = A.device
+    nws = lib.cq_gemm_workspace(ctypes.byref(g))
+    ws = workspace(nws, dev) if nws else None
+    _check(lib.cq_gemm_f32(ctypes.byref(g), _p(ws), 0 if ws is None else ws.numel(), _stream(dev)),
+           "cq_gemm_f32")
+    return C
+
+
+def gram_f64(A, B, *, ta=False, tb=False, out=None):
+    """C = op(A)^T op(B) style Gram: A is K x M (or M x K if ta), B is K x N (or N x K if tb)."""
+    _require_hip(A, B)
+    A_, lda, sa = _mat(A)
+    B_, ldb, sb = _mat(B)
+    K = A.shape[-1] if ta else A.shape[-2]
+    M = A.shape[-2] if ta else A.shape[-1]
+    N = B.shape[-2] if tb else B.shape[-1]
+    batch = max(t.shape[0] if t.dim() == 3 else 1 for t in (A, B))
+    if out is None:
+        out = torch.empty((batch, M, N), dtype=torch.float64, device=A.device)
+    lib = load()
+    ws = workspace(lib.cq_gram_f64_workspace(M, N, K, batch), A.device)
+    _check(lib.cq_gram_f64(M, N, K, batch, _p(A_), int(ta), lda, sa, _p(B_), int(tb), ldb, sb, _p(out),
+                           _p(ws), ws.numel(), _stream(A.device)), "cq_gram_f64")
+    return out
+
+
+def spd_whiten(S: torch.Tensor):
+    """S (B, p, p) fp64 SPD (overwritten) -> (Wt32, Wt64, info) with Wt^T S Wt = I."""
+    _require_hip(S)
+    B, p, _ = S.shape
+    Wt32 = torch.empty((B, p, p), dtype=torch.float32, device=S.device)
+    Wt64 = torch.empty((B, p, p), dtype=torch.float64, device=S.device)
+    info = torch.empty(B, dtype=torch.int32, device=S.device)
+    _check(load().cq_spd_whiten(_p(S), p, B, _p(Wt32), _p(Wt64), _p(info), _stream(S.device)),
+           "cq_spd_whiten")
+    return Wt32, Wt64, info
+
+
+def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-14, want64=False):
+    """A (B, p, p) fp64 symmetric (overwritten) -> (evals desc (B,p) fp64, V32, V64, sweeps)."""
+    _require_hip(A)
+    B, p, _ = A.shape
+    ev = torch.empty((B, p), dtype=torch.float64, device=A.device)
+    V32 = torch.empty((B, p, p), dtype=torch.float32, device=A.device)
+    V64 = torch.empty((B, p, p), dtype=torch.float64, device=A.device) if want64 else None
+    sw = torch.empty(B, dtype=torch.int32, device=A.device)
+    lib = load()
+    ws = workspace(lib.cq_jacobi_workspace(p, B), A.device)
+    _check(lib.cq_jacobi_eigh(_p(A), p, B, max_sweeps, tol, _p(ev), _p(V32), _p(V64), _p(sw), _p(ws),
+                              ws.numel(), _stream(A.device)), "cq_jacobi_eigh")
+    return ev, V32, V64, sw
+
+
+def ritz_residual(X, Z, theta, r):
+    _require_hip(X, Z, theta)
+    B, k, p = X.shape
+    out = torch.empty(B, dtype=torch.float32, device=X.device)
+    lib = load()
+    ws = workspace(lib.cq_ritz_workspace(k, r, B), X.device)
+    _check(lib.cq_ritz_residual(_p(X), _p(Z), _p(theta), k, p, r, B, _p(out), _p(ws), ws.numel(),
+                                _stream(X.device)), "cq_ritz_residual")
+    return out
+
+
+def scale_rc(X, *, trans=False, rowscale=None, colscale=None, out=None):
+    """out[b] = op(X[b]) * rowscale[b][:,None] * colscale[b][None,:] (scales (B,len) or (len,))."""
+    _require_hip(X, rowscale, colscale)
+    X_, ldx, sx = _mat(X)
+    B = X.shape[0] if X.dim() == 3 else 1
+    rows, cols = (X.shape[-1], X.shape[-2]) if trans else (X.shape[-2], X.shape[-1])
+    if out is None:
+        out = torch.empty((B, rows, cols), dtype=torch.float32, device=X.device)
+    Y_, ldy, sy = _mat(out)
+    rss = rowscale.shape[-1] if rowscale is not None and rowscale.dim() == 2 and rowscale.shape[0] > 1 else 0
+    css = colscale.shape[-1] if colscale is not None and colscale.dim() == 2 and colscale.shape[0] > 1 else 0
+    if X.dim() == 3 and X.shape[0] > 1:
+        sx = X.stride(0)
+    if out.dim() == 3 and out.shape[0] > 1:
+        sy = out.stride(0)
+    _check(load().cq_scale_rc(_p(X_), ldx, sx, int(trans), _p(Y_), ldy, sy, rows, cols, B, _p(rowscale),
+                              rss, _p(colscale), css, _stream(X.device)), "cq_scale_rc")
+    return out

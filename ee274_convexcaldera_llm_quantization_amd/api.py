@@ -1,0 +1,86 @@
+"""Batched entry point behind the drop-in `caldera()` (src/caldera/decomposition/alg.py).
+
+`caldera_batch` decomposes several same-shape weight matrices in lockstep on one HIP
+device (the throughput path used by bench.py and the multi-GPU sharder) and returns one
+CalderaDecomposition per matrix with the reference's field layout
+(RCR/src/caldera/utils/dataclasses.py:87-106, populated as alg.py:71-112 does).
+"""
+from __future__ import annotations
+
+import torch
+
+from .engine import CalderaEngine, EngineParams
+
+
+def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
+    """Return diag(H) if H is diagonal, else raise (dense H is not on the MI355X path yet)."""
+    if H.dim() == 1:
+        if H.shape[0] != n:
+            raise ValueError(f"H diagonal has length {H.shape[0]}, expected {n}")
+        return H
+    if H.dim() != 2 or H.shape[0] != n or H.shape[1] != n:
+        raise ValueError(f"H must be ({n}, {n}), got {tuple(H.shape)}")
+    d = torch.diagonal(H)
+    off = torch.count_nonzero(H) - torch.count_nonzero(d)
+    if int(off.item()) != 0:
+        raise NotImplementedError("caldera-mi355x: only diagonal H (None, identity or diag_embed(h), "
+                                  "as every reference caller passes) is supported on MI355X")
+    return d.contiguous()
+
+
+def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, scale_W=True,
+                  decomposition_cls=None, engine_kwargs=None, return_engine=False):
+    """Ws: list of (m, n) tensors or a (B, m, n) tensor.  H: None, (n,) diagonal, or (n, n)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("caldera-mi355x: no HIP device available (this engine has no CPU path)")
+    if decomposition_cls is None:
+        from .src.caldera.utils.dataclasses import CalderaDecomposition as decomposition_cls
+    dev_req = torch.device(device) if not isinstance(device, torch.device) else device
+    comp = dev_req if dev_req.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+    if comp.index is None:
+        comp = torch.device("cuda", torch.cuda.current_device())
+    if isinstance(Ws, torch.Tensor) and Ws.dim() == 3:
+        items = list(Ws.unbind(0))
+        W = Ws
+    else:
+        items = list(Ws)
+        W = None
+    for w in items:
+        if w.dim() != 2:
+            raise ValueError("W must be a 2-D weight matrix")
+    w_dev = items[0].device
+    w_dtype = items[0].dtype
+    if W is None:
+        W = torch.stack([w.to(comp) for w in items])
+    W = W.to(comp)
+    if W.dtype not in (torch.float16, torch.float32):
+        W = W.float()
+    B, m, n = W.shape
+    h = None if H is None else _diag_of(H.to(comp).float(), n)
+    params = EngineParams.from_caldera_params(quant_params)
+    eng = CalderaEngine(params, **(engine_kwargs or {}))
+    res = eng.run(W, h, scale_W=scale_W, use_tqdm=use_tqdm)
+    out = []
+    lr_dev = dev_req if dev_req.type == "cpu" else comp
+    for d in res:
+        dec = decomposition_cls(
+            Q=d["Q"].to(w_dev),
+            L=d["L"].to(lr_dev),
+            R=d["R"].to(lr_dev),
+        )
+        dec.scaleWH = None
+        dec.SU = torch.ones(n, dtype=w_dtype, device=w_dev)
+        dec.SV = torch.ones(m, dtype=w_dtype, device=w_dev)
+        dec.W = d["W"].cpu()
+        for f in ("Q_idxs", "L_idxs", "R_idxs"):
+            v = d[f]
+            setattr(dec, f, v.to(lr_dev if f != "Q_idxs" else w_dev) if v is not None else None)
+        for f in ("Q_scale", "L_scale", "R_scale"):
+            v = d[f]
+            setattr(dec, f, v.to(lr_dev if f != "Q_scale" else w_dev) if torch.is_tensor(v) else v)
+        dec.errors = d["errors"]
+        dec.global_scale = d["global_scale"]
+        out.append(dec)
+    if return_engine:
+        return out, eng
+    return out

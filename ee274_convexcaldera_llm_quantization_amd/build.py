@@ -1,0 +1,48 @@
+"""Build libcaldera_hip.so in-tree with hipcc for gfx950 (no JIT cache, no pip install: the
+.so travels with the repo snapshot to the GPU box)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libcaldera_hip.so")
+SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip"]
+FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
+         # bit-exact quantiser: no FMA contraction, IEEE-correct fp32 division/sqrt
+         "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + ["cq_common.h"]]
+    deps.append(os.path.join(HERE, "..", "include", "caldera_hip.h"))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,190 @@
+/*
+ * caldera_hip.h — C-ABI of libcaldera_hip.so, the MI355X (gfx950) engine behind the
+ * drop-in `caldera()` / `LowMemoryQuantizer` API.
+ *
+ * The reference (genglongling/EE274_ConvexCaldera_LLM_quantization) is pure Python on
+ * PyTorch: it has no native boundary.  Each entry point below replaces the tensor ops of
+ * one step of the reference hot path; the replaced reference lines are cited per entry
+ * (RCR/ = rank-constrained-regression-main/).  The Python caller is
+ * ee274_convexcaldera_llm_quantization_amd/_lib.py (ctypes).
+ *
+ * Conventions (every export):
+ *   - returns int status: 0 = ok, < 0 = error (CQ_E*); cq_last_error() gives a
+ *     thread-local message.  No C++ exception crosses the ABI.
+ *   - never allocates device memory: the caller passes workspace (size queried with the
+ *     matching *_workspace function).  Launches are stream-ordered on `stream`
+ *     (a hipStream_t; NULL = default stream) and never synchronise the host.
+ *   - all matrices are row-major; "batch" = number of independent matrices of one shape,
+ *     laid out at a fixed element stride (stride 0 = broadcast one operand).
+ *   - pointers are device pointers unless the name ends in _host.
+ */
+#ifndef CALDERA_HIP_H
+#define CALDERA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CQ_ABI_VERSION 1
+
+#define CQ_OK 0
+#define CQ_EINVAL (-1)   /* bad argument (shape, bits, null pointer) */
+#define CQ_EHIP (-2)     /* HIP runtime error (launch failed)        */
+#define CQ_EWORKSPACE (-3) /* workspace too small                    */
+
+/* dtype tags */
+#define CQ_F32 0
+#define CQ_F16 1
+
+int cq_abi_version(void);
+const char* cq_last_error(void);
+
+/* ---------------------------------------------------------------------------------
+ * Global RMS scaling.  Replaces RCR/src/caldera/decomposition/alg.py:38-42:
+ *   gs = W.square().mean().sqrt().item();  W = W / gs      (evaluated in W's dtype)
+ * W: batch x numel of dtype (CQ_F16 | CQ_F32).  gs_out[b] (float) receives the scale as
+ * the reference rounds it (fp16 for fp16 W).  Ws_out gets W/gs in W's dtype
+ * (half(float(w)/gs) for fp16).  If do_scale == 0, gs = 1 and Ws = W.
+ */
+size_t cq_rms_scale_workspace(int64_t batch, int64_t numel);
+int cq_rms_scale(int dtype, const void* W, int64_t batch, int64_t numel, int do_scale,
+                 float* gs_out, void* Ws_out, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Uniform absmax quantiser.  Replaces RCR/src/caldera/utils/quantization.py:244-269
+ * (quantize_block, method "uniform"), :93-101 (_quantize_uniform) and :290-295/:103-105
+ * (dequantize_block).  x: batch x numel fp32, blocks of block_size consecutive elements
+ * (block_size == numel is the whole-matrix case forced by alg.py:247).
+ *   scale[b*nblk + j] = max(max|x_blk|, eps)                 (fp32)
+ *   code = rint((x / scale) * k),  k = 2^(bits-1) - 1           (int8 for bits<=8, else int16)
+ *   deq  = (float(code) / k) * scale
+ * Outputs are optional (pass NULL to skip): codes (int8/int16, reference layout),
+ * packed (bits 2/4 only: offset-binary c+k, MSB-first, 4 resp. 2 codes per byte),
+ * deq (fp32).  If err_w != NULL and err_out != NULL, also accumulates
+ *   err_out[b] = sum_ij err_w[j % err_ncols] * (deq_ij - x_ij)^2   (fp64, deterministic)
+ * i.e. the numerator of alg.py:286-302 after a Q update with diagonal H.
+ */
+size_t cq_quantize_workspace(int64_t batch, int64_t numel, int64_t block_size);
+int cq_quantize_uniform(const float* x, int64_t batch, int64_t numel, int64_t block_size,
+                        int bits, float eps, void* codes, uint8_t* packed, float* deq,
+                        float* scale, const float* err_w, int64_t err_ncols, double* err_out,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* Same quantiser when the whole-matrix absmax is already known (bits of |x|max as
+ * uint32 in absmax_bits[b], e.g. produced by cq_gemm_f32 EPI_RESID).  Replaces
+ * alg.py:262-283 (maybe_update_Q / update_Q_non_data_aware) after the fused residual. */
+int cq_quantize_uniform_known_max(const float* x, int64_t batch, int64_t numel, int bits,
+                                  float eps, const uint32_t* absmax_bits, void* codes,
+                                  uint8_t* packed, float* deq, float* scale,
+                                  const float* err_w, int64_t err_ncols, double* err_out,
+                                  void* ws, size_t ws_bytes, void* stream);
+
+/* Dequantise (quantization.py:103-105, :292-295): out[e] = (float(c_e)/k) * scale[e / block_size].
+ * codes: int8 (bits <= 8) / int16 (bits 16), or offset-binary packed if `packed` (bits 2/4).
+ * total = elements over the whole batch (scales indexed globally). */
+int cq_dequant_uniform(const void* codes, int packed, const float* scale, int64_t total,
+                       int64_t block_size, int bits, float* out, void* stream);
+
+/* Unpack offset-binary packed codes (layout above) to int8 reference codes. */
+int cq_unpack_codes(const uint8_t* packed, int64_t batch, int64_t numel, int bits,
+                    int8_t* codes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Residual builder for the LR update.  Replaces alg.py:124 (residual = W - Q) and the
+ * diagonal-H form of alg.py:211 (Y = residual @ H_sqrt @ eigvecs; for diagonal H this is
+ * a column scaling by sqrt(h) up to a permutation that LR_init undoes):
+ *   res_ij = float(Ws_ij) - (float(c_ij)/k)*scale_b    (Q from packed codes; packed==NULL: Q=0)
+ *   Y_ij   = res_ij * ycol[j]                           (ycol == NULL: 1)
+ * Ws: fp16 or fp32 (dtype).  Y and/or res_out may be NULL.
+ */
+int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const float* scale,
+                      int bits, const float* ycol, int64_t batch, int64_t m, int64_t n,
+                      float* Y, float* res_out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Batched FP32 GEMM on gfx950 MFMA (v_mfma_f32_32x32x2_f32; exact f32 products).
+ * Carries every dense product of the hot path: Gram Y Y^T, the filtered subspace
+ * iteration G X, Ritz rotations X V, R = U^T Y, and the LPLR normal-equation products of
+ * alg.py:162-182.  op(A) is M x K, op(B) is K x N.
+ *   epi = CQ_EPI_LINEAR:  C = alpha*op(A)op(B) + beta*C + gamma*D
+ *   epi = CQ_EPI_RESID :  C = D - op(A)op(B) (D fp32, or fp16 if d_f16);
+ *                          atomicMax(absmax_bits[b], |C|)     (alg.py:262 fused with :262 of quantization.py)
+ *   epi = CQ_EPI_WERR  :  no C; err_out[b] += sum_ij w[j]*(D_ij - op(A)op(B)_ij)^2 (fp64,
+ *                          deterministic two-stage) — alg.py:182 and :286-302 for diagonal H
+ * Strides are in elements between consecutive batch entries (0 = shared).
+ */
+#define CQ_EPI_LINEAR 0
+#define CQ_EPI_RESID 1
+#define CQ_EPI_WERR 2
+
+typedef struct cq_gemm_args {
+    int64_t M, N, K, batch;
+    int trans_a, trans_b;
+    const float* A; int64_t lda, stride_a;
+    const float* B; int64_t ldb, stride_b;
+    float* C; int64_t ldc, stride_c;
+    const void* D; int64_t ldd, stride_d; int d_f16;
+    float alpha, beta, gamma;
+    const float* alpha_v; const float* beta_v; const float* gamma_v; /* optional per-batch
+                                       coefficients (device, [batch]); override the scalars */
+    int epi;
+    uint32_t* absmax_bits;           /* EPI_RESID: [batch], pre-zeroed by caller */
+    const float* w; int64_t stride_w; /* EPI_WERR: column weights (may be NULL) */
+    double* err_out;                 /* EPI_WERR: [batch] */
+} cq_gemm_args;
+
+size_t cq_gemm_workspace(const cq_gemm_args* a);
+int cq_gemm_f32(const cq_gemm_args* a, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Small dense kernels of the rank-r solver (replace torch.linalg.svd at alg.py:217,
+ * torch.linalg.lstsq at alg.py:163,175 and torch.linalg.eigh at alg.py:23).
+ */
+/* C[b] (M x N, fp64) = op(A[b])^T-style Gram:  C = A^T B with A K x M, B K x N
+ * (trans_a/trans_b: A stored M x K / B stored N x K).  fp32 inputs, fp64 accumulation. */
+size_t cq_gram_f64_workspace(int64_t M, int64_t N, int64_t K, int64_t batch);
+int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, int trans_a,
+                int64_t lda, int64_t stride_a, const float* B, int trans_b, int64_t ldb,
+                int64_t stride_b, double* C, void* ws, size_t ws_bytes, void* stream);
+
+/* SPD whitening by symmetric Gaussian elimination (Cholesky-equivalent):
+ * for each b, finds upper-triangular Wt (p x p) with Wt^T S Wt = I, written as fp32
+ * (Wt32) and/or fp64 (Wt64).  S is overwritten.  info[b] = 0 ok, j+1 if pivot j <= 0. */
+int cq_spd_whiten(double* S, int64_t p, int64_t batch, float* Wt32, double* Wt64,
+                  int* info, void* stream);
+
+/* Symmetric eigendecomposition by parallel cyclic Jacobi (fp64), eigenpairs sorted by
+ * DESCENDING eigenvalue.  A (p x p) is overwritten; evals[b*p..]; V32/V64 (p x p, columns
+ * = eigenvectors), either may be NULL.  sweeps_out[b] = sweeps used (may be NULL). */
+size_t cq_jacobi_workspace(int64_t p, int64_t batch);
+int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol,
+                   double* evals, float* V32, double* V64, int* sweeps_out, void* ws,
+                   size_t ws_bytes, void* stream);
+
+/* Ritz residuals: out[b] = max_{i<r} ||Z[:,i] - theta_i X[:,i]||_2 / |theta_0|
+ * (X, Z: k x p row-major with ld p).  theta fp64 [b*p..]. */
+size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch);
+int cq_ritz_residual(const float* X, const float* Z, const double* theta, int64_t k,
+                     int64_t p, int64_t r, int64_t batch, float* out, void* ws,
+                     size_t ws_bytes, void* stream);
+
+/* Chebyshev 3-term recurrence support and elementwise helpers. */
+/* out[b] = sum(x[b]^2 * w[j % ncols]) fp64 (w may be NULL) — denominators of alg.py:298 */
+int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel,
+                      const float* w, int64_t ncols, double* out, void* ws, size_t ws_bytes,
+                      void* stream);
+/* Y[b][i][j] = op(X[b])[i][j] * rowscale[b*rss + i] * colscale[b*css + j]
+ * (op(X)[i][j] = X[i*ldx + j], or X[j*ldx + i] if trans_x; a NULL scale is 1;
+ *  a stride of 0 shares the scale vector across the batch). rows x cols is op(X)'s shape. */
+int cq_scale_rc(const float* X, int64_t ldx, int64_t stride_x, int trans_x, float* Y,
+                int64_t ldy, int64_t stride_y, int64_t rows, int64_t cols, int64_t batch,
+                const float* rowscale, int64_t rowscale_stride, const float* colscale,
+                int64_t colscale_stride, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CALDERA_HIP_H */
