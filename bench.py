@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Benchmark: CALDERA decompositions of synthetic 4096x4096 fp16 weight matrices
+(BASELINE.json configs[1]: rank 128, Q 2-bit, L/R 16-bit, iters 5, update_order [Q, LR],
+H = I) on MI355X.  One "step" = one batched pass of the hot path (caldera() of
+alg.py:24-112) over B matrices resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank decomposes
+its own batch (matrices are independent: weak scaling, no data-path collective); the
+timed region is bracketed by barrier + synchronize and the max over ranks is reported.
+
+Prints ONE JSON line (rank 0) with value = matrices/s over all ranks, the roofline of the
+dominant kernel (fp32 MFMA GEMM of the subspace filter, timed with HIP events on its
+stream inside the timed region), the relative Frobenius error of Q+LR against the CPU
+reference path on the same matrix, and the CPU baseline (the numpy/LAPACK oracle,
+oracle/caldera_oracle.py, timed on this host on one full decomposition).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "ee274_convexcaldera_llm_quantization_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+M = N = 4096
+RANK = 128
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+PEAK_HBM_GBS = 8000.0
+
+
+def make_params():
+    from src.caldera.utils.dataclasses import CalderaParams
+    return CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=RANK, iters=5, lplr_iters=5,
+                         update_order=["Q", "LR"], sigma_reg=1e-8)
+
+
+def synth_batch(B, seed0, dev):
+    ws = []
+    for i in range(B):
+        torch.manual_seed(seed0 + i)
+        ws.append((torch.randn(M, N) * 0.02).to(torch.float16))
+    return torch.stack(ws).to(dev)
+
+
+def frob_vs_reference(dec_gpu, W_cpu, do_oracle):
+    """Relative Frobenius error of Q+LR (a) against the golden sketch of the reference run
+    (tests/golden/sum_large.npz, seed-0 matrix), (b) against the CPU oracle on the same W."""
+    out = {}
+    QLR = (dec_gpu.Q.double() + dec_gpu.L.double() @ dec_gpu.R.double()).cpu().numpy()
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sum_large.npz"), allow_pickle=False)
+    om = np.random.default_rng(1234).standard_normal((N, 16))
+    sk = QLR @ om
+    ref = g["cfg2_sketch_QLR"]
+    out["frob_err_vs_ref_sketch"] = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
+    cpu = None
+    if do_oracle:
+        from oracle import caldera_oracle as O  # CPU baseline leg only
+        nthreads = len(os.sched_getaffinity(0))
+        t0 = time.perf_counter()
+        d = O.caldera(O.Params(Q_bits=2, L_bits=16, R_bits=16, rank=RANK, iters=5,
+                               update_order=["Q", "LR"], sigma_reg=1e-8), W_cpu.numpy())
+        el = time.perf_counter() - t0
+        exp = d.Q.astype(np.float64) + d.L.astype(np.float64) @ d.R.astype(np.float64)
+        out["frob_err_vs_ref"] = float(np.linalg.norm(QLR - exp) / np.linalg.norm(exp))
+        cpu = {"value": 1.0 / el, "unit": "matrices/s", "cores": nthreads, "kind": "port",
+               "sample": f"1 full cfg2 decomposition (seed-0 4096x4096, iters 5) by the numpy/"
+                         f"LAPACK oracle, {el:.1f} s on {nthreads} host threads"}
+    return out, cpu
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from ee274_convexcaldera_llm_quantization_amd import api, solver
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    K.load()
+    qp = make_params()
+    B = args.batch
+    Wb = synth_batch(B, 1000 * rank, dev)
+
+    def step():
+        return api.caldera_batch(qp, Wb, None, device=dev, return_engine=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # time the dominant kernel (the G X filter GEMMs) with HIP events on its stream
+    solver.EVENT_PROBE.enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        decs, eng = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    solver.EVENT_PROBE.enable(False)
+    probe = solver.EVENT_PROBE.summary()
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total = args.steps * B * world
+    value = total / el
+    result = {
+        "metric": "weight matrices/sec (4096x4096, rank-128, Q=2-bit) + Frob err vs ref",
+        "value": value, "unit": "matrices/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32 (fp16 W in, fp32 MFMA, int2 codes)",
+        "data": "synthetic: W = randn(4096,4096)*0.02 -> fp16, seed per matrix",
+        "config": {"workload": "BASELINE configs[1]: 4096x4096 fp16, rank 128, Q_bits 2, L/R_bits 16, "
+                               "iters 5, update_order [Q, LR], H = I",
+                   "batch_per_gpu": B, "matrices_per_step": B * world, "parallelism": f"dp{world} (matrix-sharded)"},
+    }
+    if probe["count"]:
+        flops = probe["flops_per_launch"]
+        ach = flops / (probe["avg_ms"] * 1e-3) / 1e12
+        result["roofline"] = {"kernel": "gemm_f32_kernel (G X subspace filter)", "bound": "mfma",
+                              "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                              "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                              "launches_timed": probe["count"], "avg_launch_ms": probe["avg_ms"],
+                              "flops_per_launch": flops}
+    st = eng.solver.stats.as_dict() if eng.solver is not None else {}
+    result["solver"] = {"matvecs_per_batch": st.get("matvecs", 0), "outer_iters": st.get("outer", 0)}
+    if rank == 0 and world == 1 and not args.no_parity:
+        W0 = synth_batch(1, 0, "cpu")[0]
+        d0 = api.caldera_batch(qp, [W0.to(dev)], None, device=dev)[0]
+        par, cpu = frob_vs_reference(d0, W0, not args.no_cpu_baseline)
+        result.update(par)
+        if cpu is not None:
+            result["cpu_baseline"] = cpu
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -290,7 +290,7 @@ size_t cq_gemm_workspace(const cq_gemm_args* a) {
 int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(g, "cq_gemm_f32: null args");
     CQ_REQUIRE(g->M > 0 && g->N > 0 && g->K >= 0 && g->batch > 0, "cq_gemm_f32: bad shape");
-    CQ_REQUIRE(g->A && g->B, "cq_gemm_f32: null A/B");
+    CQ_REQUIRE((g->A && g->B) || g->K == 0, "cq_gemm_f32: null A/B");
     CQ_REQUIRE(g->epi >= CQ_EPI_LINEAR && g->epi <= CQ_EPI_WERR, "cq_gemm_f32: bad epi");
     CQ_REQUIRE(g->batch <= 65535 && ceil_div(g->M, BM) <= 65535, "cq_gemm_f32: grid too large");
     if (g->epi == CQ_EPI_LINEAR) {

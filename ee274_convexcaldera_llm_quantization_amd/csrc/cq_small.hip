@@ -100,49 +100,83 @@ static int gram_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
 }
 
 // ------------------------------------------------------------------ SPD whitening
+// Symmetric Gaussian elimination S = L D L^T on the upper triangle (the trailing block stays
+// symmetric), E = L^{-1} built alongside; Wt = E^T D^{-1/2}.  One workgroup per matrix,
+// operands L2-resident; every thread batches UNR independent element updates so the
+// loads of a step are in flight together (the step is latency-bound, not FLOP-bound).
 constexpr int kSmallThreads = 1024;
+constexpr int UNR = 8;
 
 __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __restrict__ S_all,
                                                                     int64_t p, double* __restrict__ E_all,
                                                                     float* __restrict__ W32,
                                                                     int* __restrict__ info) {
-    extern __shared__ double fac[];  // p factors + p pivots
+    extern __shared__ double fac[];  // row factors of the current step + pivots
     double* piv = fac + p;
+    __shared__ int bad;
+    __shared__ double dmax_s;
     const int64_t b = blockIdx.x;
     double* S = S_all + b * p * p;
     double* E = E_all + b * p * p;
     const int tid = threadIdx.x;
     for (int64_t e = tid; e < p * p; e += kSmallThreads) E[e] = (e / p == e % p) ? 1.0 : 0.0;
-    __shared__ int bad;
-    if (tid == 0) bad = 0;
+    if (tid == 0) {
+        bad = 0;
+        double dm = 0.0;
+        for (int64_t j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
+        dmax_s = dm;
+    }
     __syncthreads();
-    double dmax = 0.0;
-    for (int64_t j = 0; j < p; ++j) dmax = fmax(dmax, fabs(S[j * p + j]));
+    const double dmax = dmax_s;
     for (int64_t j = 0; j < p; ++j) {
         const double d = S[j * p + j];
         if (!(d > 1e-300 && d > dmax * 1e-30)) {  // not positive definite (or NaN)
-            if (tid == 0) { bad = (int)(j + 1); }
+            if (tid == 0) bad = (int)(j + 1);
             __syncthreads();
             break;
         }
-        for (int64_t i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = S[i * p + j] / d;
+        for (int64_t i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = S[j * p + i] / d;  // upper row j
         if (tid == 0) piv[j] = d;
         __syncthreads();
-        // rows i > j:  S_i[c] -= f_i S_j[c] (c >= j);  E_i[c] -= f_i E_j[c] (c <= j)
-        const int64_t rows = p - j - 1;
-        const int64_t wS = p - j, wE = j + 1;
-        const int64_t work = rows * (wS + wE);
-        for (int64_t e = tid; e < work; e += kSmallThreads) {
-            const int64_t r = e / (wS + wE), c = e % (wS + wE);
-            const int64_t i = j + 1 + r;
-            const double f = fac[i];
-            if (c < wS) {
-                const int64_t col = j + c;
-                S[i * p + col] -= f * S[j * p + col];
-            } else {
-                const int64_t col = c - wS;
-                E[i * p + col] -= f * E[j * p + col];
+        // upper trailing: S[i][c] -= f_i S[j][c] for j < i <= c ;  E[i][c] -= f_i E[j][c], c <= j, i > j
+        const int64_t t = p - j - 1;               // trailing size
+        const int64_t nS = t * (t + 1) / 2;        // upper-triangular trailing elements
+        const int64_t nE = t * (j + 1);
+        const int64_t work = nS + nE;
+        for (int64_t e0 = tid; e0 < work; e0 += (int64_t)kSmallThreads * UNR) {
+            double* dst[UNR];
+            double val[UNR];
+            double src[UNR];
+            double f[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int64_t e = e0 + (int64_t)u * kSmallThreads;
+                dst[u] = nullptr;
+                if (e < nS) {
+                    // e -> (ri, ci) in the upper triangle of the t x t trailing block, row-major
+                    // rows of decreasing length: invert with a float sqrt then fix up
+                    const double tt = (double)t;
+                    int64_t ri = (int64_t)((2.0 * tt + 1.0 - sqrt((2.0 * tt + 1.0) * (2.0 * tt + 1.0) - 8.0 * (double)e)) * 0.5);
+                    if (ri < 0) ri = 0;
+                    while (ri > 0 && ri * t - ri * (ri - 1) / 2 > e) --ri;
+                    while ((ri + 1) * t - (ri + 1) * ri / 2 <= e) ++ri;
+                    const int64_t ci = ri + (e - (ri * t - ri * (ri - 1) / 2));
+                    const int64_t i = j + 1 + ri, c = j + 1 + ci;
+                    dst[u] = S + i * p + c;
+                    src[u] = S[j * p + c];
+                    f[u] = fac[i];
+                } else if (e < work) {
+                    const int64_t q = e - nS;
+                    const int64_t i = j + 1 + q / (j + 1), c = q % (j + 1);
+                    dst[u] = E + i * p + c;
+                    src[u] = E[j * p + c];
+                    f[u] = fac[i];
+                }
+                val[u] = dst[u] ? *dst[u] : 0.0;
             }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+                if (dst[u]) *dst[u] = val[u] - f[u] * src[u];
         }
         __syncthreads();
     }
@@ -151,16 +185,20 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __res
         return;
     }
     if (tid == 0) info[b] = 0;
-    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular)
+    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular); staged in S (fp64)
     for (int64_t e = tid; e < p * p; e += kSmallThreads) {
         const int64_t a = e / p, c = e % p;
         const double v = (c >= a) ? E[c * p + a] / sqrt(piv[c]) : 0.0;
         if (W32) W32[b * p * p + e] = (float)v;
-        S[e] = v;  // stage fp64 result in S (caller may read Wt64 from here)
+        S[e] = v;
     }
 }
 
 // ------------------------------------------------------------------ Jacobi eigensolver
+// Parallel cyclic Jacobi: round-robin pairing, p/2 disjoint rotations per round.  A is updated
+// on 2x2 blocks (pair a, pair b), upper blocks only, mirrored; eigenvectors are accumulated
+// TRANSPOSED (Vt rows = eigenvector components) so a rotation of columns i, j of V is a
+// coalesced update of rows i, j of Vt.  Loads are batched UNR-deep per thread.
 __device__ __forceinline__ void rr_pair(int64_t P, int64_t rd, int64_t q, int64_t& i, int64_t& j) {
     const int64_t n1 = P - 1;
     if (q == 0) { i = n1; j = rd % n1; }
@@ -170,7 +208,7 @@ __device__ __forceinline__ void rr_pair(int64_t P, int64_t rd, int64_t q, int64_
 
 __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restrict__ A_all,
                                                                 int64_t p, int max_sweeps, double tol,
-                                                                double* __restrict__ V_all,
+                                                                double* __restrict__ Vt_all,
                                                                 double* __restrict__ evals,
                                                                 float* __restrict__ V32,
                                                                 double* __restrict__ V64,
@@ -183,12 +221,12 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
     int* pi = reinterpret_cast<int*>(sm + 2 * H);  // H
     int* pj = pi + H;                               // H
     __shared__ double red[16];
-    __shared__ int stop;
+    __shared__ int stop, nact;
     const int64_t b = blockIdx.x;
     double* A = A_all + b * p * p;
-    double* V = V_all + b * p * p;
+    double* Vt = Vt_all + b * p * p;
     const int tid = threadIdx.x;
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) V[e] = (e / p == e % p) ? 1.0 : 0.0;
+    for (int64_t e = tid; e < p * p; e += kSmallThreads) Vt[e] = (e / p == e % p) ? 1.0 : 0.0;
     // symmetrise in place (Rayleigh-Ritz matrices X^T G X carry rounding asymmetry)
     for (int64_t e = tid; e < p * p; e += kSmallThreads) {
         const int64_t i = e / p, j = e % p;
@@ -199,9 +237,9 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
         }
     }
     __syncthreads();
+    const int64_t nup = H * (H + 1) / 2;
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
-        // convergence: off(A)^2 <= tol^2 * sum diag^2
         double off = 0.0, dg = 0.0;
         for (int64_t e = tid; e < p * p; e += kSmallThreads) {
             const double v = A[e];
@@ -213,6 +251,8 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
         __syncthreads();
         if (stop) break;
         for (int64_t rd = 0; rd < P - 1; ++rd) {
+            if (tid == 0) nact = 0;
+            __syncthreads();
             for (int64_t q = tid; q < H; q += kSmallThreads) {
                 int64_t i, j;
                 rr_pair(P, rd, q, i, j);
@@ -220,62 +260,104 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
                 if (j < p) {
                     const double aij = A[i * p + j];
                     const double aii = A[i * p + i], ajj = A[j * p + j];
-                    if (fabs(aij) > 1e-300 && fabs(aij) > 1e-18 * sqrt(fabs(aii * ajj))) {
+                    if (fabs(aij) > 1e-300 && fabs(aij) > 1e-17 * sqrt(fabs(aii * ajj))) {
                         const double th = (ajj - aii) / (2.0 * aij);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
                         c = 1.0 / sqrt(1.0 + t * t);
                         s = t * c;
+                        atomicAdd(&nact, 1);
                     }
                 }
                 cs[q] = c; sn[q] = s; pi[q] = (int)i; pj[q] = (int)j;
             }
             __syncthreads();
-            // A <- J^T A J on 2x2 blocks (qa <= qb), mirrored for symmetry
-            const int64_t nblk = H * H;
-            for (int64_t e = tid; e < nblk; e += kSmallThreads) {
-                const int64_t qa = e / H, qb = e % H;
-                if (qa > qb) continue;
-                const double ca = cs[qa], sa_ = sn[qa], cb = cs[qb], sb_ = sn[qb];
-                if (sa_ == 0.0 && sb_ == 0.0) continue;
-                const int64_t ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
-                const bool va = ja < p, vb = jb < p;
-                const double x00 = A[ia * p + ib];
-                const double x01 = vb ? A[ia * p + jb] : 0.0;
-                const double x10 = va ? A[ja * p + ib] : 0.0;
-                const double x11 = (va && vb) ? A[ja * p + jb] : 0.0;
-                // columns (pair b)
-                const double y00 = cb * x00 - sb_ * x01, y01 = sb_ * x00 + cb * x01;
-                const double y10 = cb * x10 - sb_ * x11, y11 = sb_ * x10 + cb * x11;
-                // rows (pair a)
-                double z00 = ca * y00 - sa_ * y10, z10 = sa_ * y00 + ca * y10;
-                double z01 = ca * y01 - sa_ * y11, z11 = sa_ * y01 + ca * y11;
-                if (qa == qb) { z01 = 0.0; z10 = 0.0; }
-                A[ia * p + ib] = z00;
-                if (vb) A[ia * p + jb] = z01;
-                if (va) A[ja * p + ib] = z10;
-                if (va && vb) A[ja * p + jb] = z11;
-                if (qa != qb) {
-                    A[ib * p + ia] = z00;
-                    if (vb) A[jb * p + ia] = z01;
-                    if (va) A[ib * p + ja] = z10;
-                    if (va && vb) A[jb * p + ja] = z11;
+            if (nact == 0) continue;
+            // ---- A <- J^T A J on upper 2x2 pair blocks (qa <= qb), mirrored
+            for (int64_t e0 = tid; e0 < nup; e0 += (int64_t)kSmallThreads * 4) {
+                double x[4][4];
+                int64_t off4[4][4];
+                double ca[4], sa4[4], cb[4], sb4[4];
+                bool live[4], diag[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t e = e0 + (int64_t)u * kSmallThreads;
+                    live[u] = false;
+                    diag[u] = false;
+                    if (e < nup) {
+                        int64_t qb = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+                        while (qb * (qb + 1) / 2 > e) --qb;
+                        while ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
+                        const int64_t qa = e - qb * (qb + 1) / 2;
+                        ca[u] = cs[qa]; sa4[u] = sn[qa]; cb[u] = cs[qb]; sb4[u] = sn[qb];
+                        if (sa4[u] != 0.0 || sb4[u] != 0.0) {
+                            live[u] = true;
+                            diag[u] = (qa == qb);
+                            const int64_t ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
+                            const bool va = ja < p, vb = jb < p;
+                            off4[u][0] = ia * p + ib;
+                            off4[u][1] = vb ? ia * p + jb : -1;
+                            off4[u][2] = va ? ja * p + ib : -1;
+                            off4[u][3] = (va && vb) ? ja * p + jb : -1;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w) x[u][w] = off4[u][w] >= 0 ? A[off4[u][w]] : 0.0;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (!live[u]) continue;
+                    const double y00 = cb[u] * x[u][0] - sb4[u] * x[u][1], y01 = sb4[u] * x[u][0] + cb[u] * x[u][1];
+                    const double y10 = cb[u] * x[u][2] - sb4[u] * x[u][3], y11 = sb4[u] * x[u][2] + cb[u] * x[u][3];
+                    double z00 = ca[u] * y00 - sa4[u] * y10, z10 = sa4[u] * y00 + ca[u] * y10;
+                    double z01 = ca[u] * y01 - sa4[u] * y11, z11 = sa4[u] * y01 + ca[u] * y11;
+                    if (diag[u]) { z01 = 0.0; z10 = 0.0; }
+                    const double z[4] = {z00, z01, z10, z11};
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const int64_t o = off4[u][w];
+                        if (o < 0) continue;
+                        A[o] = z[w];
+                        if (!diag[u]) {  // mirror: (r, c) -> (c, r)
+                            const int64_t rr = o / p, cc = o % p;
+                            A[cc * p + rr] = z[w];
+                        }
+                    }
                 }
             }
-            // V <- V J
-            for (int64_t e = tid; e < p * H; e += kSmallThreads) {
-                const int64_t x = e / H, q = e % H;
-                const double c = cs[q], s = sn[q];
-                if (s == 0.0) continue;
-                const int64_t i = pi[q], j = pj[q];
-                const double vi = V[x * p + i], vj = V[x * p + j];
-                V[x * p + i] = c * vi - s * vj;
-                V[x * p + j] = s * vi + c * vj;
+            // ---- Vt rows i, j <- rotation (coalesced along the row)
+            const int64_t nv = H * p;
+            for (int64_t e0 = tid; e0 < nv; e0 += (int64_t)kSmallThreads * UNR) {
+                double vi[UNR], vj[UNR];
+                int64_t oi[UNR], oj[UNR];
+                double c[UNR], s[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const int64_t e = e0 + (int64_t)u * kSmallThreads;
+                    oi[u] = -1;
+                    if (e < nv) {
+                        const int64_t q = e / p, xcol = e % p;
+                        s[u] = sn[q];
+                        if (s[u] != 0.0) {
+                            c[u] = cs[q];
+                            oi[u] = (int64_t)pi[q] * p + xcol;
+                            oj[u] = (int64_t)pj[q] * p + xcol;
+                            vi[u] = Vt[oi[u]];
+                            vj[u] = Vt[oj[u]];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    if (oi[u] < 0) continue;
+                    Vt[oi[u]] = c[u] * vi[u] - s[u] * vj[u];
+                    Vt[oj[u]] = s[u] * vi[u] + c[u] * vj[u];
+                }
             }
             __syncthreads();
         }
     }
     if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
-    // sort descending by rank counting (ties broken by index)
+    // sort descending by rank counting (ties broken by index); eigenvector i = row i of Vt
     for (int64_t i = tid; i < p; i += kSmallThreads) {
         const double di = A[i * p + i];
         int64_t rank = 0;
@@ -284,11 +366,15 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
             rank += (dj > di) || (dj == di && j < i);
         }
         evals[b * p + rank] = di;
-        for (int64_t x = 0; x < p; ++x) {
-            const double v = V[x * p + i];
-            if (V32) V32[b * p * p + x * p + rank] = (float)v;
-            if (V64) V64[b * p * p + x * p + rank] = v;
-        }
+        pi[i] = (int)rank;
+    }
+    __syncthreads();
+    for (int64_t e = tid; e < p * p; e += kSmallThreads) {
+        const int64_t i = e / p, x = e % p;  // component x of eigenvector i
+        const double v = Vt[e];
+        const int64_t rk = pi[i];
+        if (V32) V32[b * p * p + x * p + rk] = (float)v;
+        if (V64) V64[b * p * p + x * p + rk] = v;
     }
 }
 
@@ -386,7 +472,7 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     if (!ws || ws_bytes < cq_jacobi_workspace(p, batch))
         return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
     const int64_t H = (p + (p & 1)) / 2;
-    const size_t lds = 2 * H * sizeof(double) + 2 * H * sizeof(int);
+    const size_t lds = 2 * H * sizeof(double) + 2 * (2 * H) * sizeof(int);
     jacobi_kernel<<<(unsigned)batch, kSmallThreads, lds, as_stream(stream)>>>(
         A, p, max_sweeps, tol, reinterpret_cast<double*>(ws), evals, V32, V64, sweeps_out);
     return check_launch("cq_jacobi_eigh");

@@ -27,6 +27,45 @@ import torch
 from . import _lib as K
 
 
+class _EventProbe:
+    """HIP-event timing of the dominant kernel (the G X filter GEMM) on the stream it is
+    launched on; used by bench.py inside its timed region (roofline.achieved)."""
+
+    def __init__(self):
+        self.on = False
+        self.pairs = []
+        self.flops = 0
+
+    def enable(self, on: bool):
+        self.on = on
+        if on:
+            self.pairs = []
+
+    def start(self, flops):
+        if not self.on:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.flops = flops
+        return (e0, e1)
+
+    def stop(self, ev):
+        if ev is not None:
+            ev[1].record()
+            self.pairs.append(ev)
+
+    def summary(self):
+        if not self.pairs:
+            return {"count": 0}
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self.pairs]
+        return {"count": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": self.flops}
+
+
+EVENT_PROBE = _EventProbe()
+
+
 class SolverStats:
     def __init__(self):
         self.outer = 0
@@ -110,15 +149,20 @@ class RankRSolver:
         t0 = torch.where(ok, (ref - ctr) / e, torch.full_like(c, 2.0))
         s = 1.0 / t0
         Y1 = self._free(X)
+        fl = 2.0 * self.k * self.k * self.p * self.B
         # Y1 = (s/e) G X - (s ctr/e) X
+        ev = EVENT_PROBE.start(fl)
         K.gemm(G, X, C=Y1, D=X, alpha_v=(s / e).float(), gamma_v=(-s * ctr / e).float())
+        EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = X, Y1
         for _ in range(1, deg):
             sn = 1.0 / (2.0 * t0 - s)
+            a_v, b_v, g_v = (2 * sn / e).float(), (-sn * s).float(), (-2 * sn * ctr / e).float()
             # prev <- (2 sn/e) G cur + (-sn s) prev + (-2 sn ctr/e) cur
-            K.gemm(G, cur, C=prev, D=cur, alpha_v=(2 * sn / e).float(), beta_v=(-sn * s).float(),
-                   gamma_v=(-2 * sn * ctr / e).float())
+            ev = EVENT_PROBE.start(fl)
+            K.gemm(G, cur, C=prev, D=cur, alpha_v=a_v, beta_v=b_v, gamma_v=g_v)
+            EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur, s = cur, prev, sn
         return cur
