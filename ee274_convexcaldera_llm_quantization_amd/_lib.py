@@ -312,7 +312,7 @@ def spd_whiten(S: torch.Tensor):
     return Wt32, Wt64, info
 
 
-def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-14, want64=False):
+def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want64=False):
     """A (B, p, p) fp64 symmetric (overwritten) -> (evals desc (B,p) fp64, V32, V64, sweeps)."""
     _require_hip(A)
     B, p, _ = A.shape

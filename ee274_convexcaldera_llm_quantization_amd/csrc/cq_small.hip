@@ -102,13 +102,13 @@ static int gram_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
 // ------------------------------------------------------------------ SPD whitening
 // Symmetric Gaussian elimination S = L D L^T on the upper triangle (the trailing block stays
 // symmetric), E = L^{-1} built alongside; Wt = E^T D^{-1/2}.  One workgroup per matrix,
-// operands L2-resident; every thread batches UNR independent element updates so the
-// loads of a step are in flight together (the step is latency-bound, not FLOP-bound).
+// operands L2-resident.  2-D wave/lane loops (no integer division in the hot loops), every
+// lane keeps several independent row elements in flight.
 constexpr int kSmallThreads = 1024;
-constexpr int UNR = 8;
+constexpr int kSmallWaves = kSmallThreads / 64;
 
 __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __restrict__ S_all,
-                                                                    int64_t p, double* __restrict__ E_all,
+                                                                    int p, double* __restrict__ E_all,
                                                                     float* __restrict__ W32,
                                                                     int* __restrict__ info) {
     extern __shared__ double fac[];  // row factors of the current step + pivots
@@ -116,67 +116,40 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __res
     __shared__ int bad;
     __shared__ double dmax_s;
     const int64_t b = blockIdx.x;
-    double* S = S_all + b * p * p;
-    double* E = E_all + b * p * p;
-    const int tid = threadIdx.x;
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) E[e] = (e / p == e % p) ? 1.0 : 0.0;
+    double* S = S_all + b * (int64_t)p * p;
+    double* E = E_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = wid; i < p; i += kSmallWaves)
+        for (int c = lane; c < p; c += 64) E[i * p + c] = (i == c) ? 1.0 : 0.0;
     if (tid == 0) {
         bad = 0;
         double dm = 0.0;
-        for (int64_t j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
+        for (int j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
         dmax_s = dm;
     }
     __syncthreads();
     const double dmax = dmax_s;
-    for (int64_t j = 0; j < p; ++j) {
+    for (int j = 0; j < p; ++j) {
         const double d = S[j * p + j];
         if (!(d > 1e-300 && d > dmax * 1e-30)) {  // not positive definite (or NaN)
-            if (tid == 0) bad = (int)(j + 1);
+            if (tid == 0) bad = j + 1;
             __syncthreads();
             break;
         }
-        for (int64_t i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = S[j * p + i] / d;  // upper row j
+        for (int i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = S[j * p + i] / d;  // upper row j
         if (tid == 0) piv[j] = d;
         __syncthreads();
-        // upper trailing: S[i][c] -= f_i S[j][c] for j < i <= c ;  E[i][c] -= f_i E[j][c], c <= j, i > j
-        const int64_t t = p - j - 1;               // trailing size
-        const int64_t nS = t * (t + 1) / 2;        // upper-triangular trailing elements
-        const int64_t nE = t * (j + 1);
-        const int64_t work = nS + nE;
-        for (int64_t e0 = tid; e0 < work; e0 += (int64_t)kSmallThreads * UNR) {
-            double* dst[UNR];
-            double val[UNR];
-            double src[UNR];
-            double f[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const int64_t e = e0 + (int64_t)u * kSmallThreads;
-                dst[u] = nullptr;
-                if (e < nS) {
-                    // e -> (ri, ci) in the upper triangle of the t x t trailing block, row-major
-                    // rows of decreasing length: invert with a float sqrt then fix up
-                    const double tt = (double)t;
-                    int64_t ri = (int64_t)((2.0 * tt + 1.0 - sqrt((2.0 * tt + 1.0) * (2.0 * tt + 1.0) - 8.0 * (double)e)) * 0.5);
-                    if (ri < 0) ri = 0;
-                    while (ri > 0 && ri * t - ri * (ri - 1) / 2 > e) --ri;
-                    while ((ri + 1) * t - (ri + 1) * ri / 2 <= e) ++ri;
-                    const int64_t ci = ri + (e - (ri * t - ri * (ri - 1) / 2));
-                    const int64_t i = j + 1 + ri, c = j + 1 + ci;
-                    dst[u] = S + i * p + c;
-                    src[u] = S[j * p + c];
-                    f[u] = fac[i];
-                } else if (e < work) {
-                    const int64_t q = e - nS;
-                    const int64_t i = j + 1 + q / (j + 1), c = q % (j + 1);
-                    dst[u] = E + i * p + c;
-                    src[u] = E[j * p + c];
-                    f[u] = fac[i];
-                }
-                val[u] = dst[u] ? *dst[u] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < UNR; ++u)
-                if (dst[u]) *dst[u] = val[u] - f[u] * src[u];
+        // S[i][c] -= f_i S[j][c] for j < i <= c  (upper trailing);  E[i][c] -= f_i E[j][c], c <= j
+        for (int i = j + 1 + wid; i < p; i += kSmallWaves) {
+            const double f = fac[i];
+            double* Si = S + i * p;
+            const double* Sj = S + j * p;
+#pragma unroll 4
+            for (int c = i + lane; c < p; c += 64) Si[c] -= f * Sj[c];
+            double* Ei = E + i * p;
+            const double* Ej = E + j * p;
+#pragma unroll 4
+            for (int c = lane; c <= j; c += 64) Ei[c] -= f * Ej[c];
         }
         __syncthreads();
     }
@@ -186,75 +159,78 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __res
     }
     if (tid == 0) info[b] = 0;
     // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular); staged in S (fp64)
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) {
-        const int64_t a = e / p, c = e % p;
-        const double v = (c >= a) ? E[c * p + a] / sqrt(piv[c]) : 0.0;
-        if (W32) W32[b * p * p + e] = (float)v;
-        S[e] = v;
-    }
+    for (int a = wid; a < p; a += kSmallWaves)
+        for (int c = lane; c < p; c += 64) {
+            const double v = (c >= a) ? E[c * p + a] / sqrt(piv[c]) : 0.0;
+            if (W32) W32[b * (int64_t)p * p + a * p + c] = (float)v;
+            S[a * p + c] = v;
+        }
 }
 
 // ------------------------------------------------------------------ Jacobi eigensolver
 // Parallel cyclic Jacobi: round-robin pairing, p/2 disjoint rotations per round.  A is updated
-// on 2x2 blocks (pair a, pair b), upper blocks only, mirrored; eigenvectors are accumulated
-// TRANSPOSED (Vt rows = eigenvector components) so a rotation of columns i, j of V is a
-// coalesced update of rows i, j of Vt.  Loads are batched UNR-deep per thread.
-__device__ __forceinline__ void rr_pair(int64_t P, int64_t rd, int64_t q, int64_t& i, int64_t& j) {
-    const int64_t n1 = P - 1;
-    if (q == 0) { i = n1; j = rd % n1; }
-    else { i = (rd + q) % n1; j = (rd - q + n1) % n1; }
-    if (i > j) { const int64_t t = i; i = j; j = t; }
+// on 2x2 blocks (pair a <= pair b), mirrored; one wave per pair-b row strip, lanes over
+// pair a.  Eigenvectors are accumulated TRANSPOSED (row i of Vt = eigenvector i), so a
+// rotation of columns i, j of V is a coalesced update of rows i, j of Vt (one wave per pair,
+// lanes along the row).  All index math is 32-bit and division-free.
+__device__ __forceinline__ void rr_pair(int P, int rd, int q, int& i, int& j) {
+    const int n1 = P - 1;
+    if (q == 0) { i = n1; j = rd; }
+    else {
+        i = rd + q; if (i >= n1) i -= n1;
+        j = rd - q; if (j < 0) j += n1;
+    }
+    if (i > j) { const int t = i; i = j; j = t; }
 }
 
 __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restrict__ A_all,
-                                                                int64_t p, int max_sweeps, double tol,
+                                                                int p, int max_sweeps, double tol,
                                                                 double* __restrict__ Vt_all,
                                                                 double* __restrict__ evals,
                                                                 float* __restrict__ V32,
                                                                 double* __restrict__ V64,
                                                                 int* __restrict__ sweeps_out) {
     extern __shared__ double sm[];
-    const int64_t P = p + (p & 1);
-    const int64_t H = P / 2;
+    const int P = p + (p & 1);
+    const int H = P / 2;
     double* cs = sm;          // H
     double* sn = sm + H;      // H
-    int* pi = reinterpret_cast<int*>(sm + 2 * H);  // H
-    int* pj = pi + H;                               // H
+    int* pi = reinterpret_cast<int*>(sm + 2 * H);  // P ints (pi | pj during rounds)
+    int* pj = pi + H;
     __shared__ double red[16];
     __shared__ int stop, nact;
     const int64_t b = blockIdx.x;
-    double* A = A_all + b * p * p;
-    double* Vt = Vt_all + b * p * p;
-    const int tid = threadIdx.x;
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) Vt[e] = (e / p == e % p) ? 1.0 : 0.0;
-    // symmetrise in place (Rayleigh-Ritz matrices X^T G X carry rounding asymmetry)
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) {
-        const int64_t i = e / p, j = e % p;
-        if (i < j) {
-            const double s = 0.5 * (A[i * p + j] + A[j * p + i]);
-            A[i * p + j] = s;
-            A[j * p + i] = s;
+    double* A = A_all + b * (int64_t)p * p;
+    double* Vt = Vt_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = wid; i < p; i += kSmallWaves)
+        for (int c = lane; c < p; c += 64) {
+            Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
+            if (i < c) {  // symmetrise (Rayleigh-Ritz matrices carry rounding asymmetry)
+                const double s = 0.5 * (A[i * p + c] + A[c * p + i]);
+                A[i * p + c] = s;
+                A[c * p + i] = s;
+            }
         }
-    }
     __syncthreads();
-    const int64_t nup = H * (H + 1) / 2;
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
-        for (int64_t e = tid; e < p * p; e += kSmallThreads) {
-            const double v = A[e];
-            if (e / p == e % p) dg += v * v; else off += v * v;
-        }
+        for (int i = wid; i < p; i += kSmallWaves)
+            for (int c = lane; c < p; c += 64) {
+                const double v = A[i * p + c];
+                if (i == c) dg += v * v; else off += v * v;
+            }
         const double offs = block_sum_f64(off, red);
         const double dgs = block_sum_f64(dg, red);
         if (tid == 0) stop = (offs <= tol * tol * dgs) ? 1 : 0;
         __syncthreads();
         if (stop) break;
-        for (int64_t rd = 0; rd < P - 1; ++rd) {
+        for (int rd = 0; rd < P - 1; ++rd) {
             if (tid == 0) nact = 0;
             __syncthreads();
-            for (int64_t q = tid; q < H; q += kSmallThreads) {
-                int64_t i, j;
+            for (int q = tid; q < H; q += kSmallThreads) {
+                int i, j;
                 rr_pair(P, rd, q, i, j);
                 double c = 1.0, s = 0.0;
                 if (j < p) {
@@ -268,89 +244,56 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
                         atomicAdd(&nact, 1);
                     }
                 }
-                cs[q] = c; sn[q] = s; pi[q] = (int)i; pj[q] = (int)j;
+                cs[q] = c; sn[q] = s; pi[q] = i; pj[q] = j;
             }
             __syncthreads();
             if (nact == 0) continue;
-            // ---- A <- J^T A J on upper 2x2 pair blocks (qa <= qb), mirrored
-            for (int64_t e0 = tid; e0 < nup; e0 += (int64_t)kSmallThreads * 4) {
-                double x[4][4];
-                int64_t off4[4][4];
-                double ca[4], sa4[4], cb[4], sb4[4];
-                bool live[4], diag[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t e = e0 + (int64_t)u * kSmallThreads;
-                    live[u] = false;
-                    diag[u] = false;
-                    if (e < nup) {
-                        int64_t qb = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
-                        while (qb * (qb + 1) / 2 > e) --qb;
-                        while ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
-                        const int64_t qa = e - qb * (qb + 1) / 2;
-                        ca[u] = cs[qa]; sa4[u] = sn[qa]; cb[u] = cs[qb]; sb4[u] = sn[qb];
-                        if (sa4[u] != 0.0 || sb4[u] != 0.0) {
-                            live[u] = true;
-                            diag[u] = (qa == qb);
-                            const int64_t ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
-                            const bool va = ja < p, vb = jb < p;
-                            off4[u][0] = ia * p + ib;
-                            off4[u][1] = vb ? ia * p + jb : -1;
-                            off4[u][2] = va ? ja * p + ib : -1;
-                            off4[u][3] = (va && vb) ? ja * p + jb : -1;
-#pragma unroll
-                            for (int w = 0; w < 4; ++w) x[u][w] = off4[u][w] >= 0 ? A[off4[u][w]] : 0.0;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (!live[u]) continue;
-                    const double y00 = cb[u] * x[u][0] - sb4[u] * x[u][1], y01 = sb4[u] * x[u][0] + cb[u] * x[u][1];
-                    const double y10 = cb[u] * x[u][2] - sb4[u] * x[u][3], y11 = sb4[u] * x[u][2] + cb[u] * x[u][3];
-                    double z00 = ca[u] * y00 - sa4[u] * y10, z10 = sa4[u] * y00 + ca[u] * y10;
-                    double z01 = ca[u] * y01 - sa4[u] * y11, z11 = sa4[u] * y01 + ca[u] * y11;
-                    if (diag[u]) { z01 = 0.0; z10 = 0.0; }
-                    const double z[4] = {z00, z01, z10, z11};
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        const int64_t o = off4[u][w];
-                        if (o < 0) continue;
-                        A[o] = z[w];
-                        if (!diag[u]) {  // mirror: (r, c) -> (c, r)
-                            const int64_t rr = o / p, cc = o % p;
-                            A[cc * p + rr] = z[w];
-                        }
+            // ---- A <- J^T A J on 2x2 pair blocks (qa <= qb); wave strips over qb, balanced
+            for (int w = wid; w < H; w += kSmallWaves) {
+                // pair strips qb = w and qb = H-1-w alternate so every wave gets ~H/2 blocks
+                const int qb = (w & 1) ? (H - 1 - (w >> 1)) : (w >> 1);
+                const double cb = cs[qb], sb = sn[qb];
+                const int ib = pi[qb], jb = pj[qb];
+                const bool vb = jb < p;
+                for (int qa = lane; qa <= qb; qa += 64) {
+                    const double ca = cs[qa], sa = sn[qa];
+                    if (sa == 0.0 && sb == 0.0) continue;
+                    const int ia = pi[qa], ja = pj[qa];
+                    const bool va = ja < p;
+                    const double x00 = A[ia * p + ib];
+                    const double x01 = vb ? A[ia * p + jb] : 0.0;
+                    const double x10 = va ? A[ja * p + ib] : 0.0;
+                    const double x11 = (va && vb) ? A[ja * p + jb] : 0.0;
+                    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                    double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
+                    double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
+                    if (qa == qb) {
+                        z01 = 0.0; z10 = 0.0;
+                        A[ia * p + ib] = z00;
+                        if (va && vb) A[ja * p + jb] = z11;
+                        if (vb) A[ia * p + jb] = 0.0;
+                        if (va) A[ja * p + ib] = 0.0;
+                    } else {
+                        A[ia * p + ib] = z00; A[ib * p + ia] = z00;
+                        if (vb) { A[ia * p + jb] = z01; A[jb * p + ia] = z01; }
+                        if (va) { A[ja * p + ib] = z10; A[ib * p + ja] = z10; }
+                        if (va && vb) { A[ja * p + jb] = z11; A[jb * p + ja] = z11; }
                     }
                 }
             }
-            // ---- Vt rows i, j <- rotation (coalesced along the row)
-            const int64_t nv = H * p;
-            for (int64_t e0 = tid; e0 < nv; e0 += (int64_t)kSmallThreads * UNR) {
-                double vi[UNR], vj[UNR];
-                int64_t oi[UNR], oj[UNR];
-                double c[UNR], s[UNR];
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const int64_t e = e0 + (int64_t)u * kSmallThreads;
-                    oi[u] = -1;
-                    if (e < nv) {
-                        const int64_t q = e / p, xcol = e % p;
-                        s[u] = sn[q];
-                        if (s[u] != 0.0) {
-                            c[u] = cs[q];
-                            oi[u] = (int64_t)pi[q] * p + xcol;
-                            oj[u] = (int64_t)pj[q] * p + xcol;
-                            vi[u] = Vt[oi[u]];
-                            vj[u] = Vt[oj[u]];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    if (oi[u] < 0) continue;
-                    Vt[oi[u]] = c[u] * vi[u] - s[u] * vj[u];
-                    Vt[oj[u]] = s[u] * vi[u] + c[u] * vj[u];
+            // ---- Vt rows i, j of each active pair (coalesced along the row)
+            for (int q = wid; q < H; q += kSmallWaves) {
+                const double s = sn[q];
+                if (s == 0.0) continue;
+                const double c = cs[q];
+                double* ri = Vt + pi[q] * p;
+                double* rj = Vt + pj[q] * p;
+#pragma unroll 4
+                for (int x = lane; x < p; x += 64) {
+                    const double vi = ri[x], vj = rj[x];
+                    ri[x] = c * vi - s * vj;
+                    rj[x] = s * vi + c * vj;
                 }
             }
             __syncthreads();
@@ -358,24 +301,279 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
     }
     if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
     // sort descending by rank counting (ties broken by index); eigenvector i = row i of Vt
-    for (int64_t i = tid; i < p; i += kSmallThreads) {
+    for (int i = tid; i < p; i += kSmallThreads) {
         const double di = A[i * p + i];
-        int64_t rank = 0;
-        for (int64_t j = 0; j < p; ++j) {
+        int rank = 0;
+        for (int j = 0; j < p; ++j) {
             const double dj = A[j * p + j];
             rank += (dj > di) || (dj == di && j < i);
         }
         evals[b * p + rank] = di;
-        pi[i] = (int)rank;
+        pi[i] = rank;
     }
     __syncthreads();
-    for (int64_t e = tid; e < p * p; e += kSmallThreads) {
-        const int64_t i = e / p, x = e % p;  // component x of eigenvector i
-        const double v = Vt[e];
-        const int64_t rk = pi[i];
-        if (V32) V32[b * p * p + x * p + rk] = (float)v;
-        if (V64) V64[b * p * p + x * p + rk] = v;
+    for (int i = wid; i < p; i += kSmallWaves) {
+        const int rk = pi[i];
+        for (int x = lane; x < p; x += 64) {  // component x of eigenvector i -> V[x][rk]
+            const double v = Vt[i * p + x];
+            if (V32) V32[b * (int64_t)p * p + x * p + rk] = (float)v;
+            if (V64) V64[b * (int64_t)p * p + x * p + rk] = v;
+        }
     }
+}
+
+// ------------------------------------------------------------------ Jacobi, LDS-resident A
+// Same cyclic round-robin Jacobi as jacobi_kernel, with A packed (upper triangle) in LDS:
+// fp64 for p <= 180, fp32 for p <= 256 (fp32 rotations: near-degenerate Ritz pairs mix at
+// ~eps32*||T||/gap, far below the 1e-4 product tolerance).  The eigenvector
+// rows (Vt) stay in global memory, updated coalesced along rows for active pairs only.
+template <typename T>
+__global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double* __restrict__ A_all,
+                                                                    int p, int max_sweeps, double tol,
+                                                                    double* __restrict__ Vt_all,
+                                                                    double* __restrict__ evals,
+                                                                    float* __restrict__ V32,
+                                                                    double* __restrict__ V64,
+                                                                    int* __restrict__ sweeps_out) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int P = p + (p & 1);
+    const int H = P / 2;
+    const int npk = p * (p + 1) / 2;
+    double* cs = reinterpret_cast<double*>(smem_raw);       // H
+    double* sn = cs + H;                                    // H
+    int* pi = reinterpret_cast<int*>(sn + H);               // P ints (pi | pj)
+    int* pj = pi + H;
+    int* rowoff = pi + P;                                   // p
+    T* a = reinterpret_cast<T*>(rowoff + p + ((p & 1) ? 1 : 0) + 2);  // packed upper
+    __shared__ double red[16];
+    __shared__ int stop, nact;
+    const int64_t b = blockIdx.x;
+    const double* Ag = A_all + b * (int64_t)p * p;
+    double* Vt = Vt_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < p; i += kSmallThreads) rowoff[i] = i * p - i * (i - 1) / 2;
+    __syncthreads();
+    for (int i = wid; i < p; i += kSmallWaves)
+        for (int c = lane; c < p; c += 64) {
+            Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
+            if (c >= i) a[rowoff[i] + c - i] = (T)(0.5 * (Ag[i * p + c] + Ag[c * p + i]));
+        }
+    __syncthreads();
+    auto A = [&](int i, int j) -> T& { return i <= j ? a[rowoff[i] + j - i] : a[rowoff[j] + i - j]; };
+    const double skip_rel = sizeof(T) == 4 ? 1e-9 : 1e-17;
+    int sweep = 0;
+    for (; sweep < max_sweeps; ++sweep) {
+        double off = 0.0, dg = 0.0;
+        for (int i = wid; i < p; i += kSmallWaves)
+            for (int c = i + lane; c < p; c += 64) {
+                const double v = (double)a[rowoff[i] + c - i];
+                if (c == i) dg += v * v; else off += 2.0 * v * v;
+            }
+        const double offs = block_sum_f64(off, red);
+        const double dgs = block_sum_f64(dg, red);
+        if (tid == 0) stop = (offs <= tol * tol * dgs) ? 1 : 0;
+        __syncthreads();
+        if (stop) break;
+        for (int rd = 0; rd < P - 1; ++rd) {
+            if (tid == 0) nact = 0;
+            __syncthreads();
+            for (int q = tid; q < H; q += kSmallThreads) {
+                int i, j;
+                rr_pair(P, rd, q, i, j);
+                double c = 1.0, s = 0.0;
+                if (j < p) {
+                    const double aij = (double)A(i, j);
+                    const double aii = (double)A(i, i), ajj = (double)A(j, j);
+                    if (fabs(aij) > 1e-300 && fabs(aij) > skip_rel * sqrt(fabs(aii * ajj))) {
+                        const double th = (ajj - aii) / (2.0 * aij);
+                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        s = t * c;
+                        atomicAdd(&nact, 1);
+                    }
+                }
+                cs[q] = c; sn[q] = s; pi[q] = i; pj[q] = j;
+            }
+            __syncthreads();
+            if (nact == 0) continue;
+            for (int w = wid; w < H; w += kSmallWaves) {
+                const int qb = (w & 1) ? (H - 1 - (w >> 1)) : (w >> 1);
+                const double cb = cs[qb], sb = sn[qb];
+                const int ib = pi[qb], jb = pj[qb];
+                const bool vb = jb < p;
+                for (int qa = lane; qa <= qb; qa += 64) {
+                    const double ca = cs[qa], sa = sn[qa];
+                    if (sa == 0.0 && sb == 0.0) continue;
+                    const int ia = pi[qa], ja = pj[qa];
+                    const bool va = ja < p;
+                    if (qa == qb) {
+                        if (!va) continue;
+                        const double x00 = A(ia, ia), x01 = A(ia, ja), x11 = A(ja, ja);
+                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                        const double y10 = cb * x01 - sb * x11, y11 = sb * x01 + cb * x11;
+                        A(ia, ia) = (T)(ca * y00 - sa * y10);
+                        A(ja, ja) = (T)(sa * y01 + ca * y11);
+                        A(ia, ja) = (T)0;
+                        continue;
+                    }
+                    const double x00 = A(ia, ib);
+                    const double x01 = vb ? (double)A(ia, jb) : 0.0;
+                    const double x10 = va ? (double)A(ja, ib) : 0.0;
+                    const double x11 = (va && vb) ? (double)A(ja, jb) : 0.0;
+                    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                    A(ia, ib) = (T)(ca * y00 - sa * y10);
+                    if (vb) A(ia, jb) = (T)(ca * y01 - sa * y11);
+                    if (va) A(ja, ib) = (T)(sa * y00 + ca * y10);
+                    if (va && vb) A(ja, jb) = (T)(sa * y01 + ca * y11);
+                }
+            }
+            for (int q = wid; q < H; q += kSmallWaves) {
+                const double s = sn[q];
+                if (s == 0.0) continue;
+                const double c = cs[q];
+                double* ri = Vt + pi[q] * p;
+                double* rj = Vt + pj[q] * p;
+#pragma unroll 4
+                for (int x = lane; x < p; x += 64) {
+                    const double vi = ri[x], vj = rj[x];
+                    ri[x] = c * vi - s * vj;
+                    rj[x] = s * vi + c * vj;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
+    int* rk = pi;  // P >= p ints
+    for (int i = tid; i < p; i += kSmallThreads) {
+        const double di = (double)a[rowoff[i]];
+        int rank = 0;
+        for (int j = 0; j < p; ++j) {
+            const double dj = (double)a[rowoff[j]];
+            rank += (dj > di) || (dj == di && j < i);
+        }
+        evals[b * p + rank] = di;
+        rk[i] = rank;
+    }
+    __syncthreads();
+    for (int i = wid; i < p; i += kSmallWaves) {
+        const int r = rk[i];
+        for (int x = lane; x < p; x += 64) {
+            const double v = Vt[i * p + x];
+            if (V32) V32[b * (int64_t)p * p + x * p + r] = (float)v;
+            if (V64) V64[b * (int64_t)p * p + x * p + r] = v;
+        }
+    }
+}
+
+static size_t jacobi_lds_bytes(int p, int esize) {
+    const int P = p + (p & 1), H = P / 2;
+    return (size_t)2 * H * sizeof(double) + (size_t)(P + p + (p & 1) + 2) * sizeof(int) +
+           (size_t)p * (p + 1) / 2 * esize + 16;
+}
+
+// ------------------------------------------------------------------ blocked SPD whitening
+// Panel-blocked symmetric elimination (nb = 32): each panel of 32 pivots is reduced in LDS,
+// then the trailing upper triangle receives one rank-32 Schur update
+//   S[i][c] -= sum_k U[k][i] U[k][c] / d_k ,   E[i][:] = -sum_k (U[k][i]/d_k) E[k][:]
+// (U = panel rows after in-panel elimination), E = L^{-1}; finally Wt = E^T D^{-1/2}.
+constexpr int WNB = 32;
+
+__global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
+    double* __restrict__ S_all, int p, double* __restrict__ E_all, float* __restrict__ W32,
+    int* __restrict__ info) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    double* U = reinterpret_cast<double*>(smem_raw);      // WNB x p   (panel rows of S, cols >= J)
+    double* Ep = U + WNB * p;                             // WNB x p   (panel rows of E)
+    double* piv = Ep + WNB * p;                           // p
+    double* fk = piv + p;                                 // WNB
+    __shared__ int bad;
+    __shared__ double dmax_s;
+    const int64_t b = blockIdx.x;
+    double* S = S_all + b * (int64_t)p * p;
+    double* E = E_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = wid; i < p; i += kSmallWaves)
+        for (int c = lane; c < p; c += 64) E[i * p + c] = (i == c) ? 1.0 : 0.0;
+    if (tid == 0) {
+        bad = 0;
+        double dm = 0.0;
+        for (int j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
+        dmax_s = dm;
+    }
+    __syncthreads();
+    const double dmax = dmax_s;
+    for (int J = 0; J < p && !bad; J += WNB) {
+        const int nb = min(WNB, p - J);
+        // load panel rows of S (columns >= J, upper part) and E (columns < J + nb)
+        for (int k = wid; k < nb; k += kSmallWaves)
+            for (int c = lane; c < p; c += 64) {
+                U[k * p + c] = (c >= J) ? S[(J + k) * p + c] : 0.0;
+                Ep[k * p + c] = (c < J + nb) ? E[(J + k) * p + c] : 0.0;
+            }
+        __syncthreads();
+        // in-panel elimination of pivots J..J+nb-1
+        for (int k = 0; k < nb; ++k) {
+            const double d = U[k * p + J + k];
+            if (!(d > 1e-300 && d > dmax * 1e-30)) {
+                if (tid == 0) bad = J + k + 1;
+                break;
+            }
+            if (tid < nb) fk[tid] = (tid > k) ? U[k * p + J + tid] / d : 0.0;
+            if (tid == 0) piv[J + k] = d;
+            __syncthreads();
+            // rows k2 > k of the panel: U[k2][c] -= f_k2 U[k][c] (c >= J+k2); Ep[k2] -= f_k2 Ep[k]
+            for (int k2 = k + 1 + wid; k2 < nb; k2 += kSmallWaves) {
+                const double f = fk[k2];
+                for (int c = J + k2 + lane; c < p; c += 64) U[k2 * p + c] -= f * U[k * p + c];
+                for (int c = lane; c <= J + k; c += 64) Ep[k2 * p + c] -= f * Ep[k * p + c];
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+        if (bad) break;
+        // write panel E rows back
+        for (int k = wid; k < nb; k += kSmallWaves)
+            for (int c = lane; c < J + nb; c += 64) E[(J + k) * p + c] = Ep[k * p + c];
+        // trailing rank-nb update, rows i >= J + nb
+        const int t0 = J + nb;
+        for (int i = t0 + wid; i < p; i += kSmallWaves) {
+            double g[WNB];
+#pragma unroll
+            for (int k = 0; k < WNB; ++k) g[k] = (k < nb) ? U[k * p + i] / piv[J + k] : 0.0;
+            for (int c = i + lane; c < p; c += 64) {
+                double acc = S[i * p + c];
+#pragma unroll
+                for (int k = 0; k < WNB; ++k)
+                    if (k < nb) acc -= g[k] * U[k * p + c];
+                S[i * p + c] = acc;
+            }
+            for (int c = lane; c < t0; c += 64) {
+                double acc = E[i * p + c];
+#pragma unroll
+                for (int k = 0; k < WNB; ++k)
+                    if (k < nb) acc -= g[k] * Ep[k * p + c];
+                E[i * p + c] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (tid == 0) info[b] = bad;
+        return;
+    }
+    if (tid == 0) info[b] = 0;
+    for (int a2 = wid; a2 < p; a2 += kSmallWaves)
+        for (int c = lane; c < p; c += 64) {
+            const double v = (c >= a2) ? E[c * p + a2] / sqrt(piv[c]) : 0.0;
+            if (W32) W32[b * (int64_t)p * p + a2 * p + c] = (float)v;
+            S[a2 * p + c] = v;
+        }
+}
+
+static size_t whiten_lds_bytes(int p) {
+    return (size_t)(2 * WNB * p + p + WNB) * sizeof(double) + 16;
 }
 
 // ------------------------------------------------------------------ Ritz residuals
@@ -454,7 +652,11 @@ int cq_spd_whiten(double* S, int64_t p, int64_t batch, float* Wt32, double* Wt64
     CQ_REQUIRE(S && p > 0 && batch > 0 && info && Wt64, "cq_spd_whiten: bad args (Wt64 is required scratch)");
     hipStream_t s = as_stream(stream);
     // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
-    spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, p, Wt64, Wt32, info);
+    const size_t wl = whiten_lds_bytes((int)p);
+    if (wl <= 160 * 1024)
+        spd_whiten_blocked_kernel<<<(unsigned)batch, kSmallThreads, wl, s>>>(S, (int)p, Wt64, Wt32, info);
+    else
+        spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, (int)p, Wt64, Wt32, info);
     if (hipMemcpyAsync(Wt64, S, (size_t)batch * p * p * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
         return set_error(CQ_EHIP, "cq_spd_whiten: copy failed");
     return check_launch("cq_spd_whiten");
@@ -472,9 +674,20 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     if (!ws || ws_bytes < cq_jacobi_workspace(p, batch))
         return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
     const int64_t H = (p + (p & 1)) / 2;
-    const size_t lds = 2 * H * sizeof(double) + 2 * (2 * H) * sizeof(int);
-    jacobi_kernel<<<(unsigned)batch, kSmallThreads, lds, as_stream(stream)>>>(
-        A, p, max_sweeps, tol, reinterpret_cast<double*>(ws), evals, V32, V64, sweeps_out);
+    hipStream_t s = as_stream(stream);
+    double* Vt = reinterpret_cast<double*>(ws);
+    const size_t l64 = jacobi_lds_bytes((int)p, 8), l32 = jacobi_lds_bytes((int)p, 4);
+    if (l64 <= 160 * 1024) {
+        jacobi_lds_kernel<double><<<(unsigned)batch, kSmallThreads, l64, s>>>(
+            A, (int)p, max_sweeps, tol, Vt, evals, V32, V64, sweeps_out);
+    } else if (l32 <= 160 * 1024) {
+        jacobi_lds_kernel<float><<<(unsigned)batch, kSmallThreads, l32, s>>>(
+            A, (int)p, max_sweeps, std::max(tol, 1e-7), Vt, evals, V32, V64, sweeps_out);
+    } else {
+        const size_t lds = 2 * H * sizeof(double) + 2 * (2 * H) * sizeof(int);
+        jacobi_kernel<<<(unsigned)batch, kSmallThreads, lds, s>>>(
+            A, (int)p, max_sweeps, tol, Vt, evals, V32, V64, sweeps_out);
+    }
     return check_launch("cq_jacobi_eigh");
 }
 

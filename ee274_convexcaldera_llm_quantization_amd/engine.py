@@ -143,7 +143,7 @@ class BatchState:
 class CalderaEngine:
     """Decomposes a batch of B weight matrices (B, m, n) with shared params and H."""
 
-    def __init__(self, params: EngineParams, *, solver_tol: float = 2e-6, solver_p: int | None = None,
+    def __init__(self, params: EngineParams, *, solver_tol: float = 5e-6, solver_p: int | None = None,
                  profile: bool = False):
         self.p = params
         self.solver_tol = solver_tol

@@ -83,14 +83,17 @@ class RankRSolver:
     """Top-r eigenpairs of the Gram of a batch of matrices, warm-started across calls."""
 
     def __init__(self, B: int, m: int, n: int, r: int, device, *, p: int | None = None,
-                 tol: float = 2e-6, deg_cold=(6, 8, 8, 8, 8, 8, 8, 8), deg_warm=(6, 8, 8, 8, 8, 8, 8),
-                 seed: int = 0x5EED):
+                 tol: float = 5e-6, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 10, 10, 10, 10, 10),
+                 seed: int = 0x5EED, jacobi_tol: float = 1e-13):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
         self.r = min(r, self.k)
         if p is None:
-            p = max(2 * self.r, self.r + 32)
+            # block size ~1.4 r: at r = 128 this is p = 180, the largest block whose fp64
+            # Rayleigh-Ritz matrix fits the 160 KB LDS of one CU (cq_jacobi_eigh fast path),
+            # at the same GEMM cost to tolerance as p = 2r (DESIGN.md, solver tuning).
+            p = max(int(1.4 * self.r) + 4, self.r + 16)
         p = p + (p & 1)
         self.direct = p >= self.k or self.k <= 256  # small problem: Jacobi on the full Gram
         self.p = self.k if self.direct else p
@@ -98,7 +101,9 @@ class RankRSolver:
         self.deg_cold, self.deg_warm = tuple(deg_cold), tuple(deg_warm)
         self.device = device
         self.seed = seed
-        self.X = None  # warm-start Ritz block (B, k, p)
+        self.jacobi_tol = jacobi_tol
+        self.X = None      # warm-start Ritz block (B, k, p)
+        self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
         self.stats = SolverStats()
         self._bufs = None
         self._G = None
@@ -130,7 +135,7 @@ class RankRSolver:
         K.gemm(G, X, C=Z)  # Z = G X
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
-        theta, V32, _, _ = K.jacobi_eigh(T)
+        theta, V32, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol)
         Xo = self._free(X, Z)
         K.gemm(X, V32, C=Xo)
         Zo = self._free(X, Z, Xo)
@@ -188,12 +193,16 @@ class RankRSolver:
             g = torch.Generator(device=dev)
             g.manual_seed(self.seed)
             X.copy_(torch.randn((B, k, p), generator=g, device=dev, dtype=torch.float32))
+            X, _ = self._cholqr(X)
+            X, _ = self._cholqr(X)
+            theta, X, Z = self._rr(X)
+            degs = self.deg_cold
         else:
+            # previous Ritz block and values: orthonormal, and its Ritz values bound the new
+            # spectrum closely (the residual changes in <1% of its entries between updates)
             X.copy_(self.X)
-        X, _ = self._cholqr(X)
-        X, _ = self._cholqr(X)
-        theta, X, Z = self._rr(X)
-        degs = self.deg_cold if cold else self.deg_warm
+            theta = self.theta
+            degs = self.deg_warm
         self.stats.resid_hist = []
         for d in degs:
             self.stats.outer += 1
@@ -210,4 +219,5 @@ class RankRSolver:
         if self.X is None:
             self.X = torch.empty((B, k, p), dtype=torch.float32, device=dev)
         self.X.copy_(X)
+        self.theta = theta.clone()
         return self.X[:, :, : self.r], theta[:, : self.r]

@@ -217,3 +217,51 @@ def test_ritz_residual(K):
     out = K.ritz_residual(X, Z, th, 10)
     ref = ((Z.double() - X.double() * th.view(2, 1, 40)) ** 2).sum(1).sqrt()[:, :10].max(1).values / th[:, 0]
     assert torch.allclose(out.double(), ref, rtol=1e-5)
+
+
+def test_jacobi_fp32_lds_path_p256(K):
+    """p = 256 runs the fp32-LDS Jacobi (not used by the solver for its final extraction):
+    eigenvalues to ~1e-5 relative of ||T||, V orthogonal."""
+    torch.manual_seed(9)
+    p = 256
+    X = torch.randn(2, 1024, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    ev, V32, V64, sw = K.jacobi_eigh(S.clone().to(DEV), want64=True)
+    ref = torch.linalg.eigvalsh(S).flip(-1)
+    nrm = ref[:, 0:1]
+    assert ((ev.cpu() - ref).abs() / nrm).max().item() < 1e-5
+    V = V64.cpu()
+    assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 1e-10
+    D = V.transpose(1, 2) @ S @ V
+    off = D - torch.diag_embed(torch.diagonal(D, dim1=1, dim2=2))
+    assert off.abs().max().item() < 1e-5 * nrm.max().item()
+
+
+@pytest.mark.parametrize("p", [180, 256])
+def test_jacobi_fp64_accuracy_solver_size(K, p):
+    """p <= 180 runs the fp64-LDS Jacobi used by the solver: eigenpairs to fp64 accuracy."""
+    if p > 180:
+        pytest.skip("fp32 path covered above")
+    torch.manual_seed(11)
+    X = torch.randn(2, 1024, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    ev, V32, V64, sw = K.jacobi_eigh(S.clone().to(DEV), want64=True)
+    ref = torch.linalg.eigvalsh(S).flip(-1)
+    assert ((ev.cpu() - ref).abs() / ref[:, 0:1]).max().item() < 1e-13
+    V = V64.cpu()
+    D = V.transpose(1, 2) @ S @ V
+    off = D - torch.diag_embed(torch.diagonal(D, dim1=1, dim2=2))
+    assert off.abs().max().item() < 1e-12 * ref.max().item()
+
+
+def test_whiten_blocked_p256(K):
+    torch.manual_seed(10)
+    p = 256
+    X = torch.randn(2, 2048, p, dtype=torch.float64) * torch.logspace(0, 3, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    Wt32, Wt64, info = K.spd_whiten(S.clone().to(DEV))
+    assert torch.all(info == 0)
+    Wt = Wt64.cpu()
+    I = Wt.transpose(1, 2) @ S @ Wt
+    assert (I - torch.eye(p, dtype=torch.float64)).abs().max().item() < 1e-9
+    assert torch.equal(torch.triu(Wt), Wt)
