@@ -22,7 +22,7 @@ namespace cq {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128, BN = 128, BK = 16, PAD = 4;
+constexpr int BM = 128, BN = 192, BK = 16, PAD = 4;
 constexpr int LDA_S = BM + PAD, LDB_S = BN + PAD;
 constexpr int kGemmThreads = 256;
 
@@ -38,6 +38,7 @@ struct KArgs {
     const float* w; int64_t sw;
     double* part;
     int vec_a, vec_b;
+    int64_t tri;
 };
 
 // Stage one BM x BK slice of op(A) into registers (4 floats x 2 per thread).
@@ -95,16 +96,16 @@ __device__ __forceinline__ void store_a(float* As, const float4 (&r)[2]) {
     }
 }
 
-// op(B) is K x N.  TB: B stored N x K.
-template <bool TB>
+// op(B) is K x N.  TB: B stored N x K.  BNT = tile width (64 or 128): BNT/64 float4 per thread.
+template <bool TB, int BNT>
 __device__ __forceinline__ void load_b(const KArgs& a, const float* B, int64_t n0, int64_t k0,
-                                       float4 (&r)[2]) {
+                                       float4 (&r)[3]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < BNT / 64; ++it) {
         const int idx = t + it * kGemmThreads;
-        if (!TB) {  // K x N row-major: rows of BN contiguous
-            const int kr = idx >> 5, jq = (idx & 31) * 4;
+        if (!TB) {  // K x N row-major: rows of BNT contiguous
+            const int kr = idx / (BNT / 4), jq = (idx % (BNT / 4)) * 4;
             const int64_t gk = k0 + kr, gj = n0 + jq;
             if (a.vec_b && gk < a.K && gj + 3 < a.N) {
                 r[it] = *reinterpret_cast<const float4*>(B + gk * a.ldb + gj);
@@ -131,14 +132,14 @@ __device__ __forceinline__ void load_b(const KArgs& a, const float* B, int64_t n
     }
 }
 
-template <bool TB>
-__device__ __forceinline__ void store_b(float* Bs, const float4 (&r)[2]) {
+template <bool TB, int BNT>
+__device__ __forceinline__ void store_b(float* Bs, const float4 (&r)[3]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < BNT / 64; ++it) {
         const int idx = t + it * kGemmThreads;
         if (!TB) {
-            const int kr = idx >> 5, jq = (idx & 31) * 4;
+            const int kr = idx / (BNT / 4), jq = (idx % (BNT / 4)) * 4;
             *reinterpret_cast<float4*>(Bs + kr * LDB_S + jq) = r[it];
         } else {
             const int row = idx >> 2, kq = (idx & 3) * 4;
@@ -150,65 +151,12 @@ __device__ __forceinline__ void store_b(float* Bs, const float4 (&r)[2]) {
     }
 }
 
-template <bool TA, bool TB, int EPI, bool DF16>
-__global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * BK * LDA_S + 2 * BK * LDB_S];
-    float* As0 = smem;
-    float* Bs0 = smem + 2 * BK * LDA_S;
-
-    const int64_t b = blockIdx.z;
-    const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
-    const float* A = a.A + b * a.sa;
-    const float* B = a.B + b * a.sb;
-
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    const int li = lane & 31, lk = lane >> 5;
-
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int64_t nt = ceil_div(a.K, BK);
-    float4 ra[2], rb[2];
-    if (nt > 0) {
-        load_a<TA>(a, A, m0, 0, ra);
-        load_b<TB>(a, B, n0, 0, rb);
-        store_a<TA>(As0, ra);
-        store_b<TB>(Bs0, rb);
-    }
-    __syncthreads();
-    for (int64_t t = 0; t < nt; ++t) {
-        const int cur = (int)(t & 1);
-        if (t + 1 < nt) {
-            load_a<TA>(a, A, m0, (t + 1) * BK, ra);
-            load_b<TB>(a, B, n0, (t + 1) * BK, rb);
-        }
-        const float* As = As0 + cur * BK * LDA_S;
-        const float* Bs = Bs0 + cur * BK * LDB_S;
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            const float* ar = As + (kk + lk) * LDA_S + wm * 64 + li;
-            const float* br = Bs + (kk + lk) * LDB_S + wn * 64 + li;
-            const float a0 = ar[0], a1 = ar[32];
-            const float b0 = br[0], b1 = br[32];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-        }
-        if (t + 1 < nt) {
-            store_a<TA>(As0 + (1 - cur) * BK * LDA_S, ra);
-            store_b<TB>(Bs0 + (1 - cur) * BK * LDB_S, rb);
-        }
-        __syncthreads();
-    }
-
-    // ---------------- epilogue
+// Shared epilogue: acc[bi][bj] holds the 32x32 C blocks of this wave (C/D layout of the
+// f32 MFMA: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).
+template <int EPI, bool DF16, int NB>
+__device__ __forceinline__ void gemm_epilogue(const KArgs& a, f32x16 (&acc)[2][NB], int64_t b,
+                                              int64_t m0, int64_t n0, int wm, int wn, int li,
+                                              int lk, int lane) {
     float* C = a.C ? a.C + b * a.sc : nullptr;
     const float* Df = (!DF16 && a.D) ? reinterpret_cast<const float*>(a.D) + b * a.sd : nullptr;
     const __half* Dh = (DF16 && a.D) ? reinterpret_cast<const __half*>(a.D) + b * a.sd : nullptr;
@@ -221,8 +169,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi) {
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj) {
-            const int64_t j = n0 + wn * 64 + bj * 32 + li;
+        for (int bj = 0; bj < NB; ++bj) {
+            const int64_t j = n0 + wn * (32 * NB) + bj * 32 + li;
             if (j >= a.N) continue;
             const float wj = (EPI == CQ_EPI_WERR && w) ? w[j] : 1.f;
 #pragma unroll
@@ -260,6 +208,206 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
     }
 }
 
+// NB = 32-wide MFMA column blocks per wave (2: 128x128 tile, 1: 128x64 tile for narrow N).
+// a.tri != 0: SYRK mode — grid.x enumerates the upper-triangular 128x128 tiles only.
+template <bool TA, bool TB, int EPI, bool DF16, int NB>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
+    constexpr int BNT = 64 * NB;
+    __shared__ __attribute__((aligned(16))) float smem[2 * BK * LDA_S + 2 * BK * LDB_S];
+    float* As0 = smem;
+    float* Bs0 = smem + 2 * BK * LDA_S;
+
+    const int64_t b = blockIdx.z;
+    int64_t tm = blockIdx.y, tn = blockIdx.x;
+    if (a.tri) {  // decode upper-triangular tile index (tm <= tn)
+        const int64_t T = a.tri;
+        int64_t e = blockIdx.x, row = 0;
+        while (e >= T - row) { e -= T - row; ++row; }
+        tm = row;
+        tn = row + e;
+    }
+    const int64_t m0 = tm * BM, n0 = tn * BNT;
+    const float* A = a.A + b * a.sa;
+    const float* B = a.B + b * a.sb;
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int li = lane & 31, lk = lane >> 5;
+
+    f32x16 acc[2][NB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int64_t nt = ceil_div(a.K, BK);
+    float4 ra[2], rb[3];
+    if (nt > 0) {
+        load_a<TA>(a, A, m0, 0, ra);
+        load_b<TB, BNT>(a, B, n0, 0, rb);
+        store_a<TA>(As0, ra);
+        store_b<TB, BNT>(Bs0, rb);
+    }
+    __syncthreads();
+    for (int64_t t = 0; t < nt; ++t) {
+        const int cur = (int)(t & 1);
+        if (t + 1 < nt) {
+            load_a<TA>(a, A, m0, (t + 1) * BK, ra);
+            load_b<TB, BNT>(a, B, n0, (t + 1) * BK, rb);
+        }
+        const float* As = As0 + cur * BK * LDA_S;
+        const float* Bs = Bs0 + cur * BK * LDB_S;
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2) {
+            const float* ar = As + (kk + lk) * LDA_S + wm * 64 + li;
+            const float* br = Bs + (kk + lk) * LDB_S + wn * (32 * NB) + li;
+            const float a0 = ar[0], a1 = ar[32];
+            float bv[NB];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) bv[j] = br[32 * j];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[j], acc[0][j], 0, 0, 0);
+                acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[j], acc[1][j], 0, 0, 0);
+            }
+        }
+        if (t + 1 < nt) {
+            store_a<TA>(As0 + (1 - cur) * BK * LDA_S, ra);
+            store_b<TB, BNT>(Bs0 + (1 - cur) * BK * LDB_S, rb);
+        }
+        __syncthreads();
+    }
+
+    gemm_epilogue<EPI, DF16, NB>(a, acc, b, m0, n0, wm, wn, li, lk, lane);
+}
+
+// ------------------------------------------------------------------ K-contiguous ("NT") GEMM
+// Both operands arrive with K contiguous: A row-major M x K, B stored N x K (op(B) = B^T).
+// LDS images [row][k] (row stride BK2 + 4 floats: 16 consecutive rows hit 16 distinct
+// 16-byte bank slots), filled by 16-byte ds_write_b128 straight from 16-byte global loads.
+// K is permuted inside each 32-deep slice so every lane's MFMA operands for 16 consecutive
+// MFMA steps are 16 contiguous floats: lane half h owns k = 16h .. 16h+15 of the slice and
+// step s contracts k = s (h = 0) with k = 16 + s (h = 1).  Fragments load with 4
+// ds_read_b128 per 32-row block, 64 v_mfma_f32_32x32x2_f32 per wave per slice.
+constexpr int BK2 = 32, BKP = BK2 + 4;
+
+template <int BNT>
+__device__ __forceinline__ void nt_load(const KArgs& a, const float* P, int64_t rows, int64_t ld,
+                                        int64_t r0, int64_t k0, bool vec, float4* r, int nvec) {
+    const int t = threadIdx.x;
+    for (int it = 0; it < nvec; ++it) {
+        const int idx = t + it * kGemmThreads;
+        const int row = idx >> 3, kq = (idx & 7) * 4;
+        const int64_t gr = r0 + row, gk = k0 + kq;
+        if (vec && gr < rows && gk + 3 < a.K) {
+            r[it] = *reinterpret_cast<const float4*>(P + gr * ld + gk);
+        } else {
+            float v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = (gr < rows && gk + c < a.K) ? P[gr * ld + gk + c] : 0.f;
+            r[it] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
+__device__ __forceinline__ void nt_store(float* S, const float4* r, int nvec) {
+    const int t = threadIdx.x;
+    for (int it = 0; it < nvec; ++it) {
+        const int idx = t + it * kGemmThreads;
+        const int row = idx >> 3, kq = (idx & 7) * 4;
+        *reinterpret_cast<float4*>(S + row * BKP + kq) = r[it];
+    }
+}
+
+template <int EPI, bool DF16, int NB>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(KArgs a) {
+    constexpr int BNT = 64 * NB;
+    constexpr int NVA = BM * BK2 / 4 / kGemmThreads;   // float4 per thread, A slice
+    constexpr int NVB = BNT * BK2 / 4 / kGemmThreads;  // float4 per thread, B slice
+    __shared__ __attribute__((aligned(16))) float smem[2 * BM * BKP + 2 * BNT * BKP];
+    float* As0 = smem;
+    float* Bs0 = smem + 2 * BM * BKP;
+
+    const int64_t b = blockIdx.z;
+    int64_t tm = blockIdx.y, tn = blockIdx.x;
+    if (a.tri) {
+        const int64_t T = a.tri;
+        int64_t e = blockIdx.x, row = 0;
+        while (e >= T - row) { e -= T - row; ++row; }
+        tm = row;
+        tn = row + e;
+    }
+    const int64_t m0 = tm * BM, n0 = tn * BNT;
+    const float* A = a.A + b * a.sa;
+    const float* B = a.B + b * a.sb;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int li = lane & 31, lk = lane >> 5;
+
+    f32x16 acc[2][NB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int64_t nt = ceil_div(a.K, BK2);
+    float4 ra[NVA], rb[NVB];
+    if (nt > 0) {
+        nt_load<BNT>(a, A, a.M, a.lda, m0, 0, a.vec_a, ra, NVA);
+        nt_load<BNT>(a, B, a.N, a.ldb, n0, 0, a.vec_b, rb, NVB);
+        nt_store(As0, ra, NVA);
+        nt_store(Bs0, rb, NVB);
+    }
+    __syncthreads();
+    for (int64_t t = 0; t < nt; ++t) {
+        const int cur = (int)(t & 1);
+        if (t + 1 < nt) {
+            nt_load<BNT>(a, A, a.M, a.lda, m0, (t + 1) * BK2, a.vec_a, ra, NVA);
+            nt_load<BNT>(a, B, a.N, a.ldb, n0, (t + 1) * BK2, a.vec_b, rb, NVB);
+        }
+        const float* As = As0 + cur * BM * BKP;
+        const float* Bs = Bs0 + cur * BNT * BKP;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {  // k = 16 lk + 8 half + (0..7)
+            float af[2][8], bf[NB][8];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) {
+                const float* ap = As + (wm * 64 + bi * 32 + li) * BKP + 16 * lk + 8 * half;
+                const float4 x0 = *reinterpret_cast<const float4*>(ap);
+                const float4 x1 = *reinterpret_cast<const float4*>(ap + 4);
+                af[bi][0] = x0.x; af[bi][1] = x0.y; af[bi][2] = x0.z; af[bi][3] = x0.w;
+                af[bi][4] = x1.x; af[bi][5] = x1.y; af[bi][6] = x1.z; af[bi][7] = x1.w;
+            }
+#pragma unroll
+            for (int bj = 0; bj < NB; ++bj) {
+                const float* bp = Bs + (wn * (32 * NB) + bj * 32 + li) * BKP + 16 * lk + 8 * half;
+                const float4 y0 = *reinterpret_cast<const float4*>(bp);
+                const float4 y1 = *reinterpret_cast<const float4*>(bp + 4);
+                bf[bj][0] = y0.x; bf[bj][1] = y0.y; bf[bj][2] = y0.z; bf[bj][3] = y0.w;
+                bf[bj][4] = y1.x; bf[bj][5] = y1.y; bf[bj][6] = y1.z; bf[bj][7] = y1.w;
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < NB; ++bj)
+                        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[bi][s2], bf[bj][s2],
+                                                                           acc[bi][bj], 0, 0, 0);
+        }
+        if (t + 1 < nt) {
+            nt_store(As0 + (1 - cur) * BM * BKP, ra, NVA);
+            nt_store(Bs0 + (1 - cur) * BNT * BKP, rb, NVB);
+        }
+        __syncthreads();
+    }
+    gemm_epilogue<EPI, DF16, NB>(a, acc, b, m0, n0, wm, wn, li, lk, lane);
+}
+
 __global__ void werr_finalize_kernel(const double* part, int64_t ntiles, double* out) {
     const int64_t b = blockIdx.x;
     if (threadIdx.x != 0) return;
@@ -268,23 +416,60 @@ __global__ void werr_finalize_kernel(const double* part, int64_t ntiles, double*
     out[b] = s;
 }
 
+// Copy the upper triangle of square C onto its lower triangle (SYRK completion), 64x64 tiles
+// through LDS so both the read and the transposed write are coalesced.
+__global__ __launch_bounds__(256) void mirror_upper_kernel(float* __restrict__ C, int64_t n, int64_t ldc,
+                                                            int64_t sc) {
+    __shared__ float tile[64][65];
+    const int64_t b = blockIdx.z;
+    const int64_t ti = blockIdx.y, tj = blockIdx.x;  // destination tile (ti > tj: lower)
+    if (ti <= tj) return;
+    float* Cb = C + b * sc;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    // source: upper tile (tj, ti)
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t i = tj * 64 + r, j = ti * 64 + tx;
+        tile[r][tx] = (i < n && j < n) ? Cb[i * ldc + j] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t i = ti * 64 + r, j = tj * 64 + tx;
+        if (i < n && j < n) Cb[i * ldc + j] = tile[tx][r];
+    }
+}
+
 }  // namespace cq
 
 using namespace cq;
 
+template <int EPI, bool DF16, int NB>
+static void launch_gemm_nb(bool ta, bool tb, dim3 grid, hipStream_t s, const KArgs& k) {
+    if (!ta && !tb) gemm_f32_kernel<false, false, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
+    else if (!ta && tb) gemm_f32_kernel<false, true, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
+    else if (ta && !tb) gemm_f32_kernel<true, false, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
+    else gemm_f32_kernel<true, true, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
+}
+
 template <int EPI, bool DF16>
-static void launch_gemm(bool ta, bool tb, dim3 grid, hipStream_t s, const KArgs& k) {
-    if (!ta && !tb) gemm_f32_kernel<false, false, EPI, DF16><<<grid, kGemmThreads, 0, s>>>(k);
-    else if (!ta && tb) gemm_f32_kernel<false, true, EPI, DF16><<<grid, kGemmThreads, 0, s>>>(k);
-    else if (ta && !tb) gemm_f32_kernel<true, false, EPI, DF16><<<grid, kGemmThreads, 0, s>>>(k);
-    else gemm_f32_kernel<true, true, EPI, DF16><<<grid, kGemmThreads, 0, s>>>(k);
+static void launch_gemm(bool ta, bool tb, int nb, dim3 grid, hipStream_t s, const KArgs& k) {
+    if (nb == 1) launch_gemm_nb<EPI, DF16, 1>(ta, tb, grid, s, k);
+    else if (nb == 3) launch_gemm_nb<EPI, DF16, 3>(ta, tb, grid, s, k);
+    else launch_gemm_nb<EPI, DF16, 2>(ta, tb, grid, s, k);
+}
+
+// tile width 64 * nb: a single 192-wide tile for 128 < N <= 192 (the solver block p), else
+// 128-wide tiles unless the last one would be at most half full
+static int pick_nb(int64_t N) {
+    if (N > 128 && N <= 192) return 3;
+    const int64_t r = N % 128;
+    return (N <= 64 || (r != 0 && r <= 64)) ? 1 : 2;
 }
 
 extern "C" {
 
 size_t cq_gemm_workspace(const cq_gemm_args* a) {
     if (!a || a->epi != CQ_EPI_WERR) return 0;
-    return (size_t)a->batch * ceil_div(a->M, BM) * ceil_div(a->N, BN) * sizeof(double);
+    return (size_t)a->batch * ceil_div(a->M, BM) * ceil_div(a->N, 64 * pick_nb(a->N)) * sizeof(double);
 }
 
 int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) {
@@ -301,6 +486,11 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
         CQ_REQUIRE(g->D, "cq_gemm_f32: epilogue needs D");
     }
     if (g->epi == CQ_EPI_RESID) CQ_REQUIRE(g->absmax_bits, "cq_gemm_f32: RESID needs absmax_bits");
+    if (g->syrk) {
+        CQ_REQUIRE(g->epi == CQ_EPI_LINEAR && g->M == g->N && g->beta == 0.f && !g->beta_v &&
+                       g->gamma == 0.f && !g->gamma_v && !g->alpha_v,
+                   "cq_gemm_f32: syrk needs square C, LINEAR epilogue, alpha only");
+    }
     if (g->epi == CQ_EPI_WERR) {
         CQ_REQUIRE(g->err_out, "cq_gemm_f32: WERR needs err_out");
         if (!ws || ws_bytes < cq_gemm_workspace(g))
@@ -320,18 +510,32 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     k.vec_a = al16(g->A) && g->lda % 4 == 0 && g->stride_a % 4 == 0;
     k.vec_b = al16(g->B) && g->ldb % 4 == 0 && g->stride_b % 4 == 0;
-    dim3 grid((unsigned)ceil_div(g->N, BN), (unsigned)ceil_div(g->M, BM), (unsigned)g->batch);
+    const int nb = g->syrk ? 2 : pick_nb(g->N);
+    dim3 grid((unsigned)ceil_div(g->N, 64 * nb), (unsigned)ceil_div(g->M, BM), (unsigned)g->batch);
+    k.tri = 0;
+    if (g->syrk) {
+        const int64_t T = ceil_div(g->N, BM);
+        k.tri = T;
+        grid = dim3((unsigned)(T * (T + 1) / 2), 1, (unsigned)g->batch);
+    }
     hipStream_t s = as_stream(stream);
     const bool ta = g->trans_a != 0, tb = g->trans_b != 0;
     switch (g->epi) {
-        case CQ_EPI_LINEAR: launch_gemm<CQ_EPI_LINEAR, false>(ta, tb, grid, s, k); break;
+        case CQ_EPI_LINEAR:
+            launch_gemm<CQ_EPI_LINEAR, false>(ta, tb, nb, grid, s, k);
+            if (g->syrk) {
+                const unsigned t64 = (unsigned)ceil_div(g->N, 64);
+                mirror_upper_kernel<<<dim3(t64, t64, (unsigned)g->batch), 256, 0, s>>>(
+                    g->C, g->N, g->ldc, g->stride_c);
+            }
+            break;
         case CQ_EPI_RESID:
-            if (g->d_f16) launch_gemm<CQ_EPI_RESID, true>(ta, tb, grid, s, k);
-            else launch_gemm<CQ_EPI_RESID, false>(ta, tb, grid, s, k);
+            if (g->d_f16) launch_gemm<CQ_EPI_RESID, true>(ta, tb, nb, grid, s, k);
+            else launch_gemm<CQ_EPI_RESID, false>(ta, tb, nb, grid, s, k);
             break;
         default:
-            if (g->d_f16) launch_gemm<CQ_EPI_WERR, true>(ta, tb, grid, s, k);
-            else launch_gemm<CQ_EPI_WERR, false>(ta, tb, grid, s, k);
+            if (g->d_f16) launch_gemm<CQ_EPI_WERR, true>(ta, tb, nb, grid, s, k);
+            else launch_gemm<CQ_EPI_WERR, false>(ta, tb, nb, grid, s, k);
             werr_finalize_kernel<<<(unsigned)g->batch, 64, 0, s>>>(
                 k.part, (int64_t)grid.x * grid.y, g->err_out);
             break;

@@ -327,6 +327,8 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
 // fp64 for p <= 180, fp32 for p <= 256 (fp32 rotations: near-degenerate Ritz pairs mix at
 // ~eps32*||T||/gap, far below the 1e-4 product tolerance).  The eigenvector
 // rows (Vt) stay in global memory, updated coalesced along rows for active pairs only.
+constexpr int JB = 2;  // pair blocks per thread held in registers per pass (register budget at 1024 threads)
+
 template <typename T>
 __global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double* __restrict__ A_all,
                                                                     int p, int max_sweeps, double tol,
@@ -338,35 +340,35 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double*
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int P = p + (p & 1);
     const int H = P / 2;
-    const int npk = p * (p + 1) / 2;
     double* cs = reinterpret_cast<double*>(smem_raw);       // H
     double* sn = cs + H;                                    // H
     int* pi = reinterpret_cast<int*>(sn + H);               // P ints (pi | pj)
     int* pj = pi + H;
-    int* rowoff = pi + P;                                   // p
-    T* a = reinterpret_cast<T*>(rowoff + p + ((p & 1) ? 1 : 0) + 2);  // packed upper
+    T* a = reinterpret_cast<T*>(pi + P + 2 + (P & 1));      // packed upper triangle
     __shared__ double red[16];
-    __shared__ int stop, nact;
+    __shared__ int stop;
     const int64_t b = blockIdx.x;
     const double* Ag = A_all + b * (int64_t)p * p;
     double* Vt = Vt_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = tid; i < p; i += kSmallThreads) rowoff[i] = i * p - i * (i - 1) / 2;
-    __syncthreads();
+    // packed upper index of (i, j), i <= j: row i starts at i*p - i*(i-1)/2
+    auto pk = [p](int i, int j) -> int {
+        if (i > j) { const int t = i; i = j; j = t; }
+        return i * p - ((i * (i - 1)) >> 1) + (j - i);
+    };
     for (int i = wid; i < p; i += kSmallWaves)
         for (int c = lane; c < p; c += 64) {
             Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
-            if (c >= i) a[rowoff[i] + c - i] = (T)(0.5 * (Ag[i * p + c] + Ag[c * p + i]));
+            if (c >= i) a[pk(i, c)] = (T)(0.5 * (Ag[i * p + c] + Ag[c * p + i]));
         }
     __syncthreads();
-    auto A = [&](int i, int j) -> T& { return i <= j ? a[rowoff[i] + j - i] : a[rowoff[j] + i - j]; };
     const double skip_rel = sizeof(T) == 4 ? 1e-9 : 1e-17;
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
         for (int i = wid; i < p; i += kSmallWaves)
             for (int c = i + lane; c < p; c += 64) {
-                const double v = (double)a[rowoff[i] + c - i];
+                const double v = (double)a[pk(i, c)];
                 if (c == i) dg += v * v; else off += 2.0 * v * v;
             }
         const double offs = block_sum_f64(off, red);
@@ -375,70 +377,123 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double*
         __syncthreads();
         if (stop) break;
         for (int rd = 0; rd < P - 1; ++rd) {
-            if (tid == 0) nact = 0;
-            __syncthreads();
+            int act = 0;
             for (int q = tid; q < H; q += kSmallThreads) {
                 int i, j;
                 rr_pair(P, rd, q, i, j);
                 double c = 1.0, s = 0.0;
                 if (j < p) {
-                    const double aij = (double)A(i, j);
-                    const double aii = (double)A(i, i), ajj = (double)A(j, j);
+                    const double aij = (double)a[pk(i, j)];
+                    const double aii = (double)a[pk(i, i)], ajj = (double)a[pk(j, j)];
                     if (fabs(aij) > 1e-300 && fabs(aij) > skip_rel * sqrt(fabs(aii * ajj))) {
                         const double th = (ajj - aii) / (2.0 * aij);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
                         c = 1.0 / sqrt(1.0 + t * t);
                         s = t * c;
-                        atomicAdd(&nact, 1);
+                        act = 1;
                     }
                 }
                 cs[q] = c; sn[q] = s; pi[q] = i; pj[q] = j;
             }
-            __syncthreads();
-            if (nact == 0) continue;
-            for (int w = wid; w < H; w += kSmallWaves) {
-                const int qb = (w & 1) ? (H - 1 - (w >> 1)) : (w >> 1);
-                const double cb = cs[qb], sb = sn[qb];
-                const int ib = pi[qb], jb = pj[qb];
-                const bool vb = jb < p;
-                for (int qa = lane; qa <= qb; qa += 64) {
-                    const double ca = cs[qa], sa = sn[qa];
-                    if (sa == 0.0 && sb == 0.0) continue;
-                    const int ia = pi[qa], ja = pj[qa];
-                    const bool va = ja < p;
-                    if (qa == qb) {
-                        if (!va) continue;
-                        const double x00 = A(ia, ia), x01 = A(ia, ja), x11 = A(ja, ja);
-                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                        const double y10 = cb * x01 - sb * x11, y11 = sb * x01 + cb * x11;
-                        A(ia, ia) = (T)(ca * y00 - sa * y10);
-                        A(ja, ja) = (T)(sa * y01 + ca * y11);
-                        A(ia, ja) = (T)0;
-                        continue;
+            if (!__syncthreads_or(act)) continue;
+            // ---- A <- J^T A J on pair blocks (qa <= qb), LDS.  Block e (triangular order) goes
+            //      to thread e mod 1024; a thread's <= JB blocks are loaded before any is stored.
+            {
+                const int nblk = H * (H + 1) / 2;
+                for (int e0 = tid; e0 < nblk; e0 += kSmallThreads * JB) {
+                    int o[JB][4];
+                    double x[JB][4], ca[JB], sa[JB], cb[JB], sb[JB];
+                    bool live[JB], dgn[JB];
+#pragma unroll
+                    for (int u = 0; u < JB; ++u) {
+                        const int e = e0 + u * kSmallThreads;
+                        live[u] = false;
+                        dgn[u] = false;
+                        if (e < nblk) {
+                            int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+                            if (qb * (qb + 1) / 2 > e) --qb;
+                            if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
+                            const int qa = e - qb * (qb + 1) / 2;
+                            ca[u] = cs[qa]; sa[u] = sn[qa]; cb[u] = cs[qb]; sb[u] = sn[qb];
+                            const int ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
+                            const bool va = ja < p, vb = jb < p;
+                            if ((sa[u] != 0.0 || sb[u] != 0.0) && (qa != qb || va)) {
+                                live[u] = true;
+                                dgn[u] = (qa == qb);
+                                if (dgn[u]) {
+                                    o[u][0] = pk(ia, ia); o[u][1] = pk(ia, ja);
+                                    o[u][2] = o[u][1]; o[u][3] = pk(ja, ja);
+                                } else {
+                                    o[u][0] = pk(ia, ib);
+                                    o[u][1] = vb ? pk(ia, jb) : -1;
+                                    o[u][2] = va ? pk(ja, ib) : -1;
+                                    o[u][3] = (va && vb) ? pk(ja, jb) : -1;
+                                }
+#pragma unroll
+                                for (int w4 = 0; w4 < 4; ++w4)
+                                    x[u][w4] = o[u][w4] >= 0 ? (double)a[o[u][w4]] : 0.0;
+                            }
+                        }
                     }
-                    const double x00 = A(ia, ib);
-                    const double x01 = vb ? (double)A(ia, jb) : 0.0;
-                    const double x10 = va ? (double)A(ja, ib) : 0.0;
-                    const double x11 = (va && vb) ? (double)A(ja, jb) : 0.0;
-                    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                    A(ia, ib) = (T)(ca * y00 - sa * y10);
-                    if (vb) A(ia, jb) = (T)(ca * y01 - sa * y11);
-                    if (va) A(ja, ib) = (T)(sa * y00 + ca * y10);
-                    if (va && vb) A(ja, jb) = (T)(sa * y01 + ca * y11);
+#pragma unroll
+                    for (int u = 0; u < JB; ++u) {
+                        if (!live[u]) continue;
+                        const double y00 = cb[u] * x[u][0] - sb[u] * x[u][1], y01 = sb[u] * x[u][0] + cb[u] * x[u][1];
+                        const double y10 = cb[u] * x[u][2] - sb[u] * x[u][3], y11 = sb[u] * x[u][2] + cb[u] * x[u][3];
+                        if (dgn[u]) {
+                            a[o[u][0]] = (T)(ca[u] * y00 - sa[u] * y10);
+                            a[o[u][3]] = (T)(sa[u] * y01 + ca[u] * y11);
+                            a[o[u][1]] = (T)0;
+                        } else {
+                            a[o[u][0]] = (T)(ca[u] * y00 - sa[u] * y10);
+                            if (o[u][1] >= 0) a[o[u][1]] = (T)(ca[u] * y01 - sa[u] * y11);
+                            if (o[u][2] >= 0) a[o[u][2]] = (T)(sa[u] * y00 + ca[u] * y10);
+                            if (o[u][3] >= 0) a[o[u][3]] = (T)(sa[u] * y01 + ca[u] * y11);
+                        }
+                    }
                 }
             }
-            for (int q = wid; q < H; q += kSmallWaves) {
-                const double s = sn[q];
-                if (s == 0.0) continue;
-                const double c = cs[q];
-                double* ri = Vt + pi[q] * p;
-                double* rj = Vt + pj[q] * p;
-#pragma unroll 4
-                for (int x = lane; x < p; x += 64) {
-                    const double vi = ri[x], vj = rj[x];
-                    ri[x] = c * vi - s * vj;
-                    rj[x] = s * vi + c * vj;
+            // ---- Vt rows of active pairs (global, coalesced); 3 pairs' rows in flight per wave
+            for (int q0 = wid; q0 < H; q0 += 3 * kSmallWaves) {
+                double vi[3][4], vj[3][4], cc[3], ss[3];
+                double* ri[3];
+                double* rj[3];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const int q = q0 + u * kSmallWaves;
+                    ss[u] = (q < H) ? sn[q] : 0.0;
+                    cc[u] = (q < H) ? cs[q] : 1.0;
+                    ri[u] = Vt + (q < H ? pi[q] : 0) * p;
+                    rj[u] = Vt + (q < H ? pj[q] : 0) * p;
+                    if (ss[u] != 0.0) {
+#pragma unroll
+                        for (int c4 = 0; c4 < 4; ++c4) {
+                            const int x = lane + 64 * c4;
+                            if (x < p) { vi[u][c4] = ri[u][x]; vj[u][c4] = rj[u][x]; }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    if (ss[u] == 0.0) continue;
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; ++c4) {
+                        const int x = lane + 64 * c4;
+                        if (x < p) {
+                            ri[u][x] = cc[u] * vi[u][c4] - ss[u] * vj[u][c4];
+                            rj[u][x] = ss[u] * vi[u][c4] + cc[u] * vj[u][c4];
+                        }
+                    }
+                }
+                // p > 256: remaining columns, unbatched
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    if (ss[u] == 0.0) continue;
+                    for (int x = lane + 256; x < p; x += 64) {
+                        const double a0 = ri[u][x], a1 = rj[u][x];
+                        ri[u][x] = cc[u] * a0 - ss[u] * a1;
+                        rj[u][x] = ss[u] * a0 + cc[u] * a1;
+                    }
                 }
             }
             __syncthreads();
@@ -447,10 +502,10 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double*
     if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
     int* rk = pi;  // P >= p ints
     for (int i = tid; i < p; i += kSmallThreads) {
-        const double di = (double)a[rowoff[i]];
+        const double di = (double)a[pk(i, i)];
         int rank = 0;
         for (int j = 0; j < p; ++j) {
-            const double dj = (double)a[rowoff[j]];
+            const double dj = (double)a[pk(j, j)];
             rank += (dj > di) || (dj == di && j < i);
         }
         evals[b * p + rank] = di;
@@ -469,8 +524,237 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double*
 
 static size_t jacobi_lds_bytes(int p, int esize) {
     const int P = p + (p & 1), H = P / 2;
-    return (size_t)2 * H * sizeof(double) + (size_t)(P + p + (p & 1) + 2) * sizeof(int) +
+    return (size_t)2 * H * sizeof(double) + (size_t)(P + 2 + (P & 1)) * sizeof(int) +
            (size_t)p * (p + 1) / 2 * esize + 16;
+}
+
+// ------------------------------------------------------------------ Jacobi, V in registers
+// A (fp64, packed upper triangle) lives in LDS in index space; the eigenvector matrix V
+// (fp32) lives in REGISTERS in "seat" space.  The round-robin is the circle method with
+// fixed adjacent seat pairs (2k, 2k+1): between rounds every player except seat 0 moves one
+// seat (even seats +1 pair, odd seats -1 pair, with the two end turns), so a V column only
+// ever moves to a neighbouring pair.  Thread (pair-group pg, row-group rg) holds PPT pairs x
+// RPT rows of V; a round's rotations are register-local and the seat shift is register
+// moves plus one lane shuffle up and one down per row.  V never touches memory until the
+// end, which removes the per-round O(p^2) global traffic of accumulating V.  fp32 V keeps
+// orthogonality to ~sqrt(rounds)*eps32 (~3e-6); the solver re-orthonormalises its final
+// Ritz block (CholQR), and A stays fp64 so the rotations themselves are fp64-accurate.
+template <int PPT, int RPT>
+__global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double* __restrict__ A_all,
+                                                                    int p, int max_sweeps, double tol,
+                                                                    double* __restrict__ evals,
+                                                                    float* __restrict__ V32,
+                                                                    double* __restrict__ V64,
+                                                                    int* __restrict__ sweeps_out) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int P = p + (p & 1);
+    const int H = P / 2;
+    double* cs = reinterpret_cast<double*>(smem_raw);   // H
+    double* sn = cs + H;                                // H
+    int* lo = reinterpret_cast<int*>(sn + H);           // H  (smaller index of pair k)
+    int* hi = lo + H;                                   // H
+    int* flp = hi + H;                                  // H  (seat 2k holds the larger index)
+    int* seat = flp + H;                                // P
+    int* seat2 = seat + P;                              // P
+    int* rnk = seat2 + P;                               // P
+    double* a = reinterpret_cast<double*>(rnk + P + ((7 * H + 3 * P) & 1));
+    __shared__ double red[16];
+    __shared__ int stop;
+    const int64_t b = blockIdx.x;
+    const double* Ag = A_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int pg = lane & 31;                 // pair group
+    const int rg = 2 * wid + (lane >> 5);     // row group
+    const int k0 = pg * PPT, x0 = rg * RPT;
+    auto pk = [p](int i, int j) -> int {
+        if (i > j) { const int t = i; i = j; j = t; }
+        return i * p - ((i * (i - 1)) >> 1) + (j - i);
+    };
+    for (int i = wid; i < p; i += kSmallWaves)
+        for (int c = lane; c < p; c += 64)
+            if (c >= i) a[pk(i, c)] = 0.5 * (Ag[i * p + c] + Ag[c * p + i]);
+    for (int s = tid; s < P; s += kSmallThreads) seat[s] = s;
+    float ev[PPT][RPT], od[PPT][RPT];
+#pragma unroll
+    for (int u = 0; u < PPT; ++u)
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int k = k0 + u, x = x0 + r;
+            ev[u][r] = (x == 2 * k) ? 1.f : 0.f;
+            od[u][r] = (x == 2 * k + 1) ? 1.f : 0.f;
+        }
+    __syncthreads();
+    int sweep = 0;
+    for (; sweep < max_sweeps; ++sweep) {
+        double off = 0.0, dg = 0.0;
+        for (int i = wid; i < p; i += kSmallWaves)
+            for (int c = i + lane; c < p; c += 64) {
+                const double v = a[pk(i, c)];
+                if (c == i) dg += v * v; else off += 2.0 * v * v;
+            }
+        const double offs = block_sum_f64(off, red);
+        const double dgs = block_sum_f64(dg, red);
+        if (tid == 0) stop = (offs <= tol * tol * dgs) ? 1 : 0;
+        __syncthreads();
+        if (stop) break;
+        for (int rd = 0; rd < P - 1; ++rd) {
+            int act = 0;
+            for (int k = tid; k < H; k += kSmallThreads) {
+                const int se = seat[2 * k], so = seat[2 * k + 1];
+                const int i = min(se, so), j = max(se, so);
+                double c = 1.0, s = 0.0;
+                if (j < p) {
+                    const double aij = a[pk(i, j)];
+                    const double aii = a[pk(i, i)], ajj = a[pk(j, j)];
+                    if (fabs(aij) > 1e-300 && fabs(aij) > 1e-17 * sqrt(fabs(aii * ajj))) {
+                        const double th = (ajj - aii) / (2.0 * aij);
+                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        s = t * c;
+                        act = 1;
+                    }
+                }
+                cs[k] = c; sn[k] = s; lo[k] = i; hi[k] = j; flp[k] = se > so;
+                // seats of the next round (circle shift with fixed adjacent pairs)
+                seat2[2 * k] = (k == 0) ? se : (k == 1) ? seat[1] : seat[2 * k - 2];
+                seat2[2 * k + 1] = (k == H - 1) ? se : seat[2 * k + 3];
+            }
+            const bool any = __syncthreads_or(act);
+            if (any) {
+                // ---- A <- J^T A J on pair blocks (qa <= qb) in LDS
+                const int nblk = H * (H + 1) / 2;
+                for (int e0 = tid; e0 < nblk; e0 += kSmallThreads * JB) {
+                    int o[JB][4];
+                    double x[JB][4], ca[JB], sa[JB], cb[JB], sb[JB];
+                    bool live[JB], dgn[JB];
+#pragma unroll
+                    for (int u = 0; u < JB; ++u) {
+                        const int e = e0 + u * kSmallThreads;
+                        live[u] = false;
+                        dgn[u] = false;
+                        if (e < nblk) {
+                            int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+                            if (qb * (qb + 1) / 2 > e) --qb;
+                            if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
+                            const int qa = e - qb * (qb + 1) / 2;
+                            ca[u] = cs[qa]; sa[u] = sn[qa]; cb[u] = cs[qb]; sb[u] = sn[qb];
+                            const int ia = lo[qa], ja = hi[qa], ib = lo[qb], jb = hi[qb];
+                            const bool va = ja < p, vb = jb < p;
+                            if ((sa[u] != 0.0 || sb[u] != 0.0) && (qa != qb || va)) {
+                                live[u] = true;
+                                dgn[u] = (qa == qb);
+                                if (dgn[u]) {
+                                    o[u][0] = pk(ia, ia); o[u][1] = pk(ia, ja);
+                                    o[u][2] = o[u][1]; o[u][3] = pk(ja, ja);
+                                } else {
+                                    o[u][0] = pk(ia, ib);
+                                    o[u][1] = vb ? pk(ia, jb) : -1;
+                                    o[u][2] = va ? pk(ja, ib) : -1;
+                                    o[u][3] = (va && vb) ? pk(ja, jb) : -1;
+                                }
+#pragma unroll
+                                for (int w4 = 0; w4 < 4; ++w4) x[u][w4] = o[u][w4] >= 0 ? a[o[u][w4]] : 0.0;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < JB; ++u) {
+                        if (!live[u]) continue;
+                        const double y00 = cb[u] * x[u][0] - sb[u] * x[u][1], y01 = sb[u] * x[u][0] + cb[u] * x[u][1];
+                        const double y10 = cb[u] * x[u][2] - sb[u] * x[u][3], y11 = sb[u] * x[u][2] + cb[u] * x[u][3];
+                        if (dgn[u]) {
+                            a[o[u][0]] = ca[u] * y00 - sa[u] * y10;
+                            a[o[u][3]] = sa[u] * y01 + ca[u] * y11;
+                            a[o[u][1]] = 0.0;
+                        } else {
+                            a[o[u][0]] = ca[u] * y00 - sa[u] * y10;
+                            if (o[u][1] >= 0) a[o[u][1]] = ca[u] * y01 - sa[u] * y11;
+                            if (o[u][2] >= 0) a[o[u][2]] = sa[u] * y00 + ca[u] * y10;
+                            if (o[u][3] >= 0) a[o[u][3]] = sa[u] * y01 + ca[u] * y11;
+                        }
+                    }
+                }
+                // ---- V rotations (registers)
+#pragma unroll
+                for (int u = 0; u < PPT; ++u) {
+                    const int k = k0 + u;
+                    if (k < H) {
+                        const float c = (float)cs[k], s = (float)sn[k];
+                        if (s != 0.f) {
+                            const bool f = flp[k] != 0;
+#pragma unroll
+                            for (int r = 0; r < RPT; ++r) {
+                                const float e = ev[u][r], o2 = od[u][r];
+                                if (!f) { ev[u][r] = c * e - s * o2; od[u][r] = s * e + c * o2; }
+                                else { od[u][r] = c * o2 - s * e; ev[u][r] = s * o2 + c * e; }
+                            }
+                        }
+                    }
+                }
+            }
+            // ---- seat shift of V (every round, rotations or not)
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                const float from_left = __shfl_up(ev[PPT - 1][r], 1, 32);   // ev of pair k0-1
+                const float from_right = __shfl_down(od[0][r], 1, 32);      // od of pair k0+PPT
+                float ne[PPT], no[PPT];
+#pragma unroll
+                for (int u = 0; u < PPT; ++u) {
+                    const int k = k0 + u;
+                    const float evm1 = (u == 0) ? from_left : ev[u - 1][r];
+                    const float odp1 = (u == PPT - 1) ? from_right : od[u + 1][r];
+                    ne[u] = (k == 0) ? ev[u][r] : (k == 1) ? od[u - (u > 0 ? 1 : 0)][r] : evm1;
+                    no[u] = (k == H - 1) ? ev[u][r] : odp1;
+                    if (k >= H) { ne[u] = ev[u][r]; no[u] = od[u][r]; }
+                }
+                // k == 1 with u == 0 needs od of pair 0 from the left neighbour
+                const float od0_left = __shfl_up(od[PPT - 1][r], 1, 32);
+                if (PPT == 1 && k0 == 1) ne[0] = od0_left;
+#pragma unroll
+                for (int u = 0; u < PPT; ++u) { ev[u][r] = ne[u]; od[u][r] = no[u]; }
+            }
+            __syncthreads();
+            for (int s2 = tid; s2 < P; s2 += kSmallThreads) seat[s2] = seat2[s2];
+            __syncthreads();
+        }
+    }
+    if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
+    for (int i = tid; i < p; i += kSmallThreads) {
+        const double di = a[pk(i, i)];
+        int rank = 0;
+        for (int j = 0; j < p; ++j) {
+            const double dj = a[pk(j, j)];
+            rank += (dj > di) || (dj == di && j < i);
+        }
+        evals[b * p + rank] = di;
+        rnk[i] = rank;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+        const int k = k0 + u;
+        if (k >= H) continue;
+        const int pe = seat[2 * k], po = seat[2 * k + 1];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int x = x0 + r;
+            if (x >= p) continue;
+            if (pe < p) {
+                if (V32) V32[b * (int64_t)p * p + x * p + rnk[pe]] = ev[u][r];
+                if (V64) V64[b * (int64_t)p * p + x * p + rnk[pe]] = ev[u][r];
+            }
+            if (po < p) {
+                if (V32) V32[b * (int64_t)p * p + x * p + rnk[po]] = od[u][r];
+                if (V64) V64[b * (int64_t)p * p + x * p + rnk[po]] = od[u][r];
+            }
+        }
+    }
+}
+
+static size_t jacobi_reg_bytes(int p) {
+    const int P = p + (p & 1), H = P / 2;
+    return (size_t)2 * H * sizeof(double) + (size_t)(3 * H + 3 * P + 1) * sizeof(int) + 8 +
+           (size_t)p * (p + 1) / 2 * sizeof(double) + 16;
 }
 
 // ------------------------------------------------------------------ blocked SPD whitening
@@ -676,10 +960,15 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     const int64_t H = (p + (p & 1)) / 2;
     hipStream_t s = as_stream(stream);
     double* Vt = reinterpret_cast<double*>(ws);
-    const size_t l64 = jacobi_lds_bytes((int)p, 8), l32 = jacobi_lds_bytes((int)p, 4);
-    if (l64 <= 160 * 1024) {
-        jacobi_lds_kernel<double><<<(unsigned)batch, kSmallThreads, l64, s>>>(
-            A, (int)p, max_sweeps, tol, Vt, evals, V32, V64, sweeps_out);
+    const size_t l32 = jacobi_lds_bytes((int)p, 4), lreg = jacobi_reg_bytes((int)p);
+    if (p <= 192 && lreg <= 160 * 1024) {
+        // fp64 A in LDS, V in registers (no per-round memory traffic for V)
+        if (p <= 64)
+            jacobi_reg_kernel<1, 2><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+        else if (p <= 128)
+            jacobi_reg_kernel<2, 4><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+        else
+            jacobi_reg_kernel<3, 6><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
     } else if (l32 <= 160 * 1024) {
         jacobi_lds_kernel<float><<<(unsigned)batch, kSmallThreads, l32, s>>>(
             A, (int)p, max_sweeps, std::max(tol, 1e-7), Vt, evals, V32, V64, sweeps_out);

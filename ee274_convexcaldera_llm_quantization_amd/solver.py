@@ -90,10 +90,12 @@ class RankRSolver:
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
         self.r = min(r, self.k)
         if p is None:
-            # block size ~1.4 r: at r = 128 this is p = 180, the largest block whose fp64
-            # Rayleigh-Ritz matrix fits the 160 KB LDS of one CU (cq_jacobi_eigh fast path),
-            # at the same GEMM cost to tolerance as p = 2r (solver tuning).
+            # block size ~1.4 r rounded up to a multiple of 32: at r = 128 this is p = 192,
+            # the largest block whose fp64 Rayleigh-Ritz matrix fits the 160 KB LDS of one CU
+            # (cq_jacobi_eigh register/LDS path) and one 192-wide GEMM tile; same GEMM cost to
+            # tolerance as p = 2r (solver tuning).
             p = max(int(1.4 * self.r) + 4, self.r + 16)
+            p = (p + 31) // 32 * 32
         p = p + (p & 1)
         self.direct = p >= self.k or self.k <= 256  # small problem: Jacobi on the full Gram
         self.p = self.k if self.direct else p
@@ -132,7 +134,7 @@ class RankRSolver:
     def _rr(self, X):
         G = self._G
         Z = self._free(X)
-        K.gemm(G, X, C=Z)  # Z = G X
+        K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
         theta, V32, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol)
@@ -157,7 +159,7 @@ class RankRSolver:
         fl = 2.0 * self.k * self.k * self.p * self.B
         # Y1 = (s/e) G X - (s ctr/e) X
         ev = EVENT_PROBE.start(fl)
-        K.gemm(G, X, C=Y1, D=X, alpha_v=(s / e).float(), gamma_v=(-s * ctr / e).float())
+        K.gemm(G, X, ta=True, C=Y1, D=X, alpha_v=(s / e).float(), gamma_v=(-s * ctr / e).float())
         EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = X, Y1
@@ -166,7 +168,7 @@ class RankRSolver:
             a_v, b_v, g_v = (2 * sn / e).float(), (-sn * s).float(), (-2 * sn * ctr / e).float()
             # prev <- (2 sn/e) G cur + (-sn s) prev + (-2 sn ctr/e) cur
             ev = EVENT_PROBE.start(fl)
-            K.gemm(G, cur, C=prev, D=cur, alpha_v=a_v, beta_v=b_v, gamma_v=g_v)
+            K.gemm(G, cur, ta=True, C=prev, D=cur, alpha_v=a_v, beta_v=b_v, gamma_v=g_v)
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur, s = cur, prev, sn
@@ -184,9 +186,9 @@ class RankRSolver:
             return V32[:, :, : self.r], theta[:, : self.r]
         self._alloc(dev)
         if self.left:
-            K.gemm(Y, Y, tb=True, C=self._G)  # Y Y^T
+            K.gemm(Y, Y, tb=True, C=self._G, syrk=True)  # Y Y^T (upper tiles + mirror)
         else:
-            K.gemm(Y, Y, ta=True, C=self._G)  # Y^T Y
+            K.gemm(Y, Y, ta=True, C=self._G, syrk=True)  # Y^T Y
         cold = not (warm and self.X is not None)
         X = self._bufs[0]
         if cold:
@@ -216,6 +218,9 @@ class RankRSolver:
             self.stats.resid_hist.append(mr)
             if mr <= self.tol:
                 break
+        # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
+        # one CholQR pass restores orthonormality without moving the converged subspace
+        X, _ = self._cholqr(X)
         if self.X is None:
             self.X = torch.empty((B, k, p), dtype=torch.float32, device=dev)
         self.X.copy_(X)

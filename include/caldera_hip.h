@@ -134,6 +134,9 @@ typedef struct cq_gemm_args {
     uint32_t* absmax_bits;           /* EPI_RESID: [batch], pre-zeroed by caller */
     const float* w; int64_t stride_w; /* EPI_WERR: column weights (may be NULL) */
     double* err_out;                 /* EPI_WERR: [batch] */
+    int syrk;                        /* 1: C = alpha op(A) op(B) is symmetric (A = B^T up to
+                                        op): only upper 128x128 tiles are computed, then
+                                        mirrored (LINEAR, beta = gamma = 0)               */
 } cq_gemm_args;
 
 size_t cq_gemm_workspace(const cq_gemm_args* a);

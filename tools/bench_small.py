@@ -17,7 +17,7 @@ def t(fn, n=3):
     return (time.perf_counter() - t0) / n * 1e3
 
 
-for p in (int(a) for a in (sys.argv[1:] or ["256"])):
+for p in (int(a) for a in (sys.argv[1:] or ["192"])):
     for B in (8, 32):
         torch.manual_seed(0)
         X = torch.randn(B, 4 * p, p, dtype=torch.float64, device=dev)
