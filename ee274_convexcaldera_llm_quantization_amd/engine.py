@@ -367,6 +367,12 @@ class CalderaEngine:
         dev = W.device
         out = []
         gsl = gs.tolist()
+        qs = best.Qs.tolist()
+        # compact (storage / gather) form: packed codes as kept by the engine
+        self.last_packed = [dict(codes=best.Qc[b].clone(), Q_scale=qs[b], L=best.L[b].clone(),
+                                 R=best.R[b].clone(), global_scale=gsl[b],
+                                 errors={k: v[b] for k, v in errors.items()})
+                            for b in range(B)]
         for b in range(B):
             d = {}
             if best.flag_Q[b]:
