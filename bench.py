@@ -65,6 +65,11 @@ def frob_vs_reference(dec_gpu, W_cpu, do_oracle):
     if do_oracle:
         from oracle import caldera_oracle as O  # CPU baseline leg only
         nthreads = len(os.sched_getaffinity(0))
+        try:  # threads the BLAS/LAPACK backend actually uses (OMP/OPENBLAS limits apply)
+            from threadpoolctl import threadpool_info
+            nthreads = max(int(i.get("num_threads", 1)) for i in threadpool_info()) or nthreads
+        except Exception:
+            pass
         t0 = time.perf_counter()
         d = O.caldera(O.Params(Q_bits=2, L_bits=16, R_bits=16, rank=RANK, iters=5,
                                update_order=["Q", "LR"], sigma_reg=1e-8), W_cpu.numpy())
@@ -142,11 +147,18 @@ def main():
     if probe["count"]:
         flops = probe["flops_per_launch"]
         ach = flops / (probe["avg_ms"] * 1e-3) / 1e12
+        traffic = None  # HBM bytes per launch from the committed PMC pass of this same config
+        pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+        solver_p = eng.solver.p if eng.solver is not None else None
+        if os.path.exists(pmc_path):
+            pm = json.load(open(pmc_path))
+            if pm["config"]["batch"] == B and pm["config"]["p"] == solver_p:
+                traffic = pm["hbm_bytes_per_launch"]
         result["roofline"] = {"kernel": "gemm_f32_kernel (G X subspace filter)", "bound": "mfma",
                               "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                              "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                              "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
                               "launches_timed": probe["count"], "avg_launch_ms": probe["avg_ms"],
-                              "flops_per_launch": flops}
+                              "flops_per_launch": flops, "solver_block_p": solver_p}
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
     result["solver"] = {"matvecs_per_batch": st.get("matvecs", 0), "outer_iters": st.get("outer", 0)}
     if rank == 0 and world == 1 and not args.no_parity:

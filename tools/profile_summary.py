@@ -1,0 +1,42 @@
+"""Summarise rocprofv3 outputs (kernel stats CSV + --pmc counter CSVs) into profiles/.
+
+usage: python tools/profile_summary.py <stats_dir> [<pmc_dir> ...] > profiles/<round>_summary.txt
+FETCH_SIZE / WRITE_SIZE are reported in KB per dispatch by rocprofv3; on gfx950 FETCH_SIZE
+counts half the bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md, HBM), so the
+corrected HBM read bytes are 2 x FETCH_SIZE for the streaming GEMM/quantiser kernels.
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+
+def stats(d):
+    f = glob.glob(os.path.join(d, "*kernel_stats.csv"))[0]
+    rows = list(csv.DictReader(open(f)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    print(f"# kernel stats: {f}  (total GPU kernel time {tot / 1e6:.2f} ms)")
+    print(f"{'total_ms':>10} {'pct':>6} {'calls':>6} {'avg_us':>10}  kernel")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
+        print(f"{float(r['TotalDurationNs']) / 1e6:10.2f} {float(r['Percentage']):6.2f} {r['Calls']:>6} "
+              f"{float(r['AverageNs']) / 1e3:10.1f}  {r['Name'][:110]}")
+
+
+def pmc(d):
+    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    rows = list(csv.DictReader(open(f)))
+    agg = collections.defaultdict(list)
+    for r in rows:
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    print(f"# PMC: {f}")
+    print(f"{'counter':>12} {'dispatches':>10} {'avg_KB':>14}  kernel")
+    for (k, c), v in sorted(agg.items(), key=lambda x: -sum(x[1]))[:15]:
+        print(f"{c:>12} {len(v):>10} {sum(v) / len(v):14.1f}  {k[:110]}")
+
+
+if __name__ == "__main__":
+    stats(sys.argv[1])
+    for d in sys.argv[2:]:
+        print()
+        pmc(d)
