@@ -41,6 +41,23 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class X3Args(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64), ("batch", c_i64),
+        ("Ah", c_vp), ("Al", c_vp), ("lda", c_i64), ("stride_a", c_i64),
+        ("Bh", c_vp), ("Bl", c_vp), ("ldb", c_i64), ("stride_b", c_i64),
+        ("inv_scale", c_vp),
+        ("C", c_vp), ("ldc", c_i64), ("stride_c", c_i64),
+        ("P", c_vp), ("ldp", c_i64), ("stride_p", c_i64),
+        ("D", c_vp), ("ldd", c_i64), ("stride_d", c_i64),
+        ("alpha_v", c_vp), ("beta_v", c_vp), ("gamma_v", c_vp),
+        ("out_h", c_vp), ("out_l", c_vp), ("ldo", c_i64), ("stride_o", c_i64),
+        ("out_scale", c_float),
+        ("overflow", c_vp),
+        ("tri", c_int),
+    ]
+
+
 _SIGS = {
     "cq_abi_version": (c_int, []),
     "cq_last_error": (ctypes.c_char_p, []),
@@ -70,6 +87,11 @@ _SIGS = {
     "cq_weighted_sqsum": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_scale_rc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                             c_i64, c_vp, c_i64, c_vp]),
+    "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cq_transpose_split": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
+    "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp]),
+    "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -358,3 +380,92 @@ def scale_rc(X, *, trans=False, rowscale=None, colscale=None, out=None):
     _check(load().cq_scale_rc(_p(X_), ldx, sx, int(trans), _p(Y_), ldy, sy, rows, cols, B, _p(rowscale),
                               rss, _p(colscale), css, _stream(X.device)), "cq_scale_rc")
     return out
+
+
+# ---------------------------------------------------------------------------- split-fp16 products
+def sym_split_f16(G: torch.Tensor, x_scale: float, *, hi=None, lo=None, scale=None, inv_scale=None,
+                  upper_only=False):
+    """G (B, n, n) fp32 PSD -> (hi, lo fp16, scale (B,), inv_scale (B,) = 1/(scale*x_scale)).
+    upper_only: only G's upper triangle is valid (x3 tri Gram); the split is mirrored."""
+    _require_hip(G)
+    assert G.dtype == torch.float32 and G.is_contiguous() and G.dim() == 3 and G.shape[1] == G.shape[2]
+    B, n, _ = G.shape
+    dev = G.device
+    hi = torch.empty((B, n, n), dtype=torch.float16, device=dev) if hi is None else hi
+    lo = torch.empty((B, n, n), dtype=torch.float16, device=dev) if lo is None else lo
+    scale = torch.empty(B, dtype=torch.float32, device=dev) if scale is None else scale
+    inv_scale = torch.empty(B, dtype=torch.float32, device=dev) if inv_scale is None else inv_scale
+    _check(load().cq_sym_split_f16(_p(G), n, B, int(bool(upper_only)), float(x_scale), _p(hi), _p(lo), _p(scale),
+                                   _p(inv_scale),
+                                   _stream(dev)), "cq_sym_split_f16")
+    return hi, lo, scale, inv_scale
+
+
+def transpose_split(X: torch.Tensor, *, out=None, hi=None, lo=None, scale: float | torch.Tensor = 1.0):
+    """X (B, r, c) fp32 contiguous -> X^T (B, c, r) fp32 (out) and/or its fp16 split (hi, lo)
+    scaled by `scale` (a float, or a (B,) fp32 tensor of per-matrix scales)."""
+    _require_hip(X)
+    assert X.dtype == torch.float32 and X.is_contiguous() and X.dim() == 3
+    B, r, c = X.shape
+    sv = scale if torch.is_tensor(scale) else None
+    sf = 1.0 if sv is not None else float(scale)
+    _check(load().cq_transpose_split(_p(X), r, c, B, _p(out), _p(hi), _p(lo), sf, _p(sv), _stream(X.device)),
+           "cq_transpose_split")
+    return out, hi, lo
+
+
+def pow2_scale(X: torch.Tensor, log2_target: int = 14, out=None):
+    """(B,) fp32 power-of-two scales s[b] with max|X[b]| * s[b] < 2^log2_target."""
+    _require_hip(X)
+    assert X.dtype == torch.float32 and X.is_contiguous()
+    B = X.shape[0]
+    out = torch.empty(B, dtype=torch.float32, device=X.device) if out is None else out
+    _check(load().cq_pow2_scale(_p(X), X.numel() // B, B, int(log2_target), _p(out), _stream(X.device)),
+           "cq_pow2_scale")
+    return out
+
+
+def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None):
+    """fp16 halves of X * scale (scale: float or (B,) tensor), same shape as X."""
+    _require_hip(X)
+    assert X.dtype == torch.float32 and X.is_contiguous()
+    B = X.shape[0]
+    hi = torch.empty(X.shape, dtype=torch.float16, device=X.device) if hi is None else hi
+    lo = torch.empty(X.shape, dtype=torch.float16, device=X.device) if lo is None else lo
+    sv = scale if torch.is_tensor(scale) else None
+    sf = 1.0 if sv is not None else float(scale)
+    _check(load().cq_split_f16(_p(X), X.numel() // B, B, _p(sv), sf, _p(hi), _p(lo), _stream(X.device)),
+           "cq_split_f16")
+    return hi, lo
+
+
+def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
+            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False):
+    """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
+    B = Bh + Bl (B, N, K) fp16 halves; optional fp16 split of C into out_h/out_l."""
+    _require_hip(Ah, Al, Bh, Bl, C)
+    Bt, M, Kd = Ah.shape
+    N = Bh.shape[1]
+    assert Bh.shape[2] == Kd and C.shape == (Bt, M, N)
+    for t in (Ah, Al, Bh, Bl, C, P, D, out_h, out_l):
+        assert t is None or t.is_contiguous()
+    g = X3Args()
+    g.M, g.N, g.K, g.batch = M, N, Kd, Bt
+    g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), Kd, M * Kd
+    g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), Kd, N * Kd
+    g.inv_scale = inv_scale.data_ptr()
+    g.C, g.ldc, g.stride_c = C.data_ptr(), N, M * N
+    if P is not None:
+        g.P, g.ldp, g.stride_p = P.data_ptr(), N, M * N
+    if D is not None:
+        g.D, g.ldd, g.stride_d = D.data_ptr(), N, M * N
+    g.alpha_v = alpha_v.data_ptr() if alpha_v is not None else None
+    g.beta_v = beta_v.data_ptr() if beta_v is not None else None
+    g.gamma_v = gamma_v.data_ptr() if gamma_v is not None else None
+    if out_h is not None:
+        g.out_h, g.out_l, g.ldo, g.stride_o = out_h.data_ptr(), out_l.data_ptr(), N, M * N
+        g.out_scale = out_scale
+        g.overflow = overflow.data_ptr()
+    g.tri = int(bool(tri))
+    _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
+    return C

@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from .engine import CalderaEngine, EngineParams
+from .overlap import run_interleaved
 
 
 def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
@@ -29,8 +30,14 @@ def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
 
 
 def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, scale_W=True,
-                  decomposition_cls=None, engine_kwargs=None, return_engine=False):
-    """Ws: list of (m, n) tensors or a (B, m, n) tensor.  H: None, (n,) diagonal, or (n, n)."""
+                  decomposition_cls=None, engine_kwargs=None, return_engine=False, streams=None):
+    """Ws: list of (m, n) tensors or a (B, m, n) tensor.  H: None, (n,) diagonal, or (n, n).
+
+    streams: number of parts the batch is split into, each decomposed by its own engine on
+    its own HIP stream and interleaved at host-sync points (overlap.py).  Default 1: on
+    MI355X concurrent parts measured slower (the one-CU p x p kernels need a whole CU's LDS
+    and stall behind the other part's GEMM tiles).  Results do not depend on it beyond the
+    solver tolerance."""
     if not torch.cuda.is_available():
         raise RuntimeError("caldera-mi355x: no HIP device available (this engine has no CPU path)")
     if decomposition_cls is None:
@@ -58,11 +65,25 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
     B, m, n = W.shape
     h = None if H is None else _diag_of(H.to(comp).float(), n)
     params = EngineParams.from_caldera_params(quant_params)
-    eng = CalderaEngine(params, **(engine_kwargs or {}))
-    res = eng.run(W, h, scale_W=scale_W, use_tqdm=use_tqdm)
+    if streams is None:
+        streams = 1
+    streams = max(1, min(int(streams), B))
+    bounds = [B * i // streams for i in range(streams + 1)]
+    engines = [CalderaEngine(params, **(engine_kwargs or {})) for _ in range(streams)]
+    gens = [e.run_iter(W[bounds[i]:bounds[i + 1]], h, scale_W, use_tqdm and i == 0)
+            for i, e in enumerate(engines)]
+    res = [d for part in run_interleaved(gens, comp) for d in part]
+    eng = engines[0]
+    eng.parts = engines
     out = []
     lr_dev = dev_req if dev_req.type == "cpu" else comp
-    for d in res:
+    # alg.py:81 keeps W on the host: one batched copy into pinned memory instead of B
+    # pageable copies
+    W_host = torch.empty((B, m, n), dtype=res[0]["W"].dtype, pin_memory=True)
+    for b, d in enumerate(res):
+        W_host[b].copy_(d["W"], non_blocking=True)
+    torch.cuda.current_stream(comp).synchronize()
+    for b, d in enumerate(res):
         dec = decomposition_cls(
             Q=d["Q"].to(w_dev),
             L=d["L"].to(lr_dev),
@@ -71,7 +92,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
         dec.scaleWH = None
         dec.SU = torch.ones(n, dtype=w_dtype, device=w_dev)
         dec.SV = torch.ones(m, dtype=w_dtype, device=w_dev)
-        dec.W = d["W"].cpu()
+        dec.W = W_host[b]
         for f in ("Q_idxs", "L_idxs", "R_idxs"):
             v = d[f]
             setattr(dec, f, v.to(lr_dev if f != "Q_idxs" else w_dev) if v is not None else None)

@@ -1,0 +1,472 @@
+// Split-fp16 ("f16x3") products with the symmetric Gram G for the rank-r solver's
+// Chebyshev filter (the dominant cost of the SVD replacing alg.py:217).
+//
+// Every fp32 operand x is carried as two fp16 halves, x*s = hi + lo with hi = f16(x*s) and
+// lo = f16(x*s - hi) (s a power of two), so x*s is represented to 2^-22 relative.  A product
+// sum_k a_k b_k is then hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b term is
+// 2^-22 relative), each term on v_mfma_f32_32x32x16_f16 with fp32 accumulation: three fp16
+// MFMAs at 16x the fp32 MFMA rate give fp32-grade products (measured error equal to the
+// fp32 MFMA GEMM's) at 5.3x the fp32 peak.
+//
+// Layout: the filter iterates on X^T (p x k, row-major) so both operands are K-contiguous:
+//   C[j][i] = sum_k Xt[j][k] G[i][k]   ( = (G X)^T since G = G^T )
+// Tile 192 (rows of Xt) x 256 (rows of G) x 32, 512 threads = 8 waves of 96 x 64 (3 x 2
+// MFMA blocks).  LDS images [row][k] with an 80-byte row stride (64 B data + 16 B pad) make
+// both the 16-byte stage writes and the ds_read_b128 fragment reads conflict-free; two
+// stages (140 KB) double-buffer the K loop with a register prefetch.
+#include "cq_common.h"
+
+namespace cq {
+
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x16v = __attribute__((ext_vector_type(16))) float;
+
+constexpr int X3_BM = 192, X3_BN = 256, X3_BK = 32;
+constexpr int X3_LD = 40;  // LDS row stride in halves
+constexpr int X3_THREADS = 512;
+constexpr int X3_NA = (2 * X3_BM * 4) / X3_THREADS;  // 16-B chunks per thread per stage: A (hi+lo)
+constexpr int X3_NB = (2 * X3_BN * 4) / X3_THREADS;  // B (hi+lo)
+constexpr int X3_A_HALVES = 2 * X3_BM * X3_LD;
+constexpr int X3_STAGE = X3_A_HALVES + 2 * X3_BN * X3_LD;  // halves per stage
+constexpr size_t X3_LDS_BYTES = 2 * X3_STAGE * sizeof(_Float16);
+static_assert((2 * X3_BM * 4) % X3_THREADS == 0 && (2 * X3_BN * 4) % X3_THREADS == 0, "chunking");
+
+struct X3K {
+    int64_t M, N, K, batch;
+    const _Float16 *Ah, *Al; int64_t lda, sa;
+    const _Float16 *Bh, *Bl; int64_t ldb, sb;
+    const float* inv_scale;       // per batch
+    float* C; int64_t ldc, sc;
+    const float* P; int64_t ldp, sp;    // prev (may alias C)
+    const float* D; int64_t ldd, sd;    // cur
+    const float *alpha_v, *beta_v, *gamma_v;
+    _Float16 *Oh, *Ol; int64_t ldo, so;
+    float out_scale;
+    int* overflow;
+    int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
+    int64_t tiles_n, tiles_m;
+};
+
+__device__ __forceinline__ void x3_load(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
+                                        uint4 (&ra)[X3_NA], uint4 (&rb)[X3_NB]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < X3_NA; ++it) {
+        const int idx = t + it * X3_THREADS;
+        const int part = idx / (X3_BM * 4), rem = idx % (X3_BM * 4);
+        const int row = rem >> 2, ch = rem & 3;
+        const int64_t gr = m0 + row;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (gr < a.M) {
+            const _Float16* src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + ch * 8;
+            v = *reinterpret_cast<const uint4*>(src);
+        }
+        ra[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < X3_NB; ++it) {
+        const int idx = t + it * X3_THREADS;
+        const int part = idx / (X3_BN * 4), rem = idx % (X3_BN * 4);
+        const int row = rem >> 2, ch = rem & 3;
+        const int64_t gr = n0 + row;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (gr < a.N) {
+            const _Float16* src = (part ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + ch * 8;
+            v = *reinterpret_cast<const uint4*>(src);
+        }
+        rb[it] = v;
+    }
+}
+
+__device__ __forceinline__ void x3_store(_Float16* st, const uint4 (&ra)[X3_NA], const uint4 (&rb)[X3_NB]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < X3_NA; ++it) {
+        const int idx = t + it * X3_THREADS;
+        const int part = idx / (X3_BM * 4), rem = idx % (X3_BM * 4);
+        const int row = rem >> 2, ch = rem & 3;
+        *reinterpret_cast<uint4*>(st + part * X3_BM * X3_LD + row * X3_LD + ch * 8) = ra[it];
+    }
+    _Float16* sb = st + X3_A_HALVES;
+#pragma unroll
+    for (int it = 0; it < X3_NB; ++it) {
+        const int idx = t + it * X3_THREADS;
+        const int part = idx / (X3_BN * 4), rem = idx % (X3_BN * 4);
+        const int row = rem >> 2, ch = rem & 3;
+        *reinterpret_cast<uint4*>(sb + part * X3_BN * X3_LD + row * X3_LD + ch * 8) = rb[it];
+    }
+}
+
+__device__ __forceinline__ void x3_compute(f32x16v (&acc)[3][2], const _Float16* sA, int wm, int wn, int lr, int lh) {
+    const _Float16* sB = sA + X3_A_HALVES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int ko = 16 * s + 8 * lh;
+        f16x8 ah[3], al[3], bh[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int row = 96 * wm + 32 * i + lr;
+            ah[i] = *reinterpret_cast<const f16x8*>(sA + row * X3_LD + ko);
+            al[i] = *reinterpret_cast<const f16x8*>(sA + X3_BM * X3_LD + row * X3_LD + ko);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = 64 * wn + 32 * j + lr;
+            bh[j] = *reinterpret_cast<const f16x8*>(sB + row * X3_LD + ko);
+            bl[j] = *reinterpret_cast<const f16x8*>(sB + X3_BN * X3_LD + row * X3_LD + ko);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+    }
+}
+
+template <int PF>
+__global__ __launch_bounds__(X3_THREADS, 1) void gemm_x3_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char x3_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(x3_smem_raw);
+
+    // XCD-aware tile order: consecutive hardware workgroup ids go round-robin over the 8
+    // XCDs; give each XCD a contiguous run of logical tiles so the tiles of one matrix
+    // (which share the X^T slices) meet in the same L2.
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    int64_t lin = blockIdx.x;
+    if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+    const int64_t tn = lin % a.tiles_n;
+    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
+    const int64_t b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * X3_BM, n0 = tn * X3_BN;
+    if (a.tri && n0 + X3_BN <= m0) return;  // strictly below the diagonal: mirrored later
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;  // wave tile: rows 96 wm .. +96, cols 64 wn .. +64
+    const int lr = lane & 31, lh = lane >> 5;
+
+    f32x16v acc[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int64_t nt = a.K / X3_BK;
+    if (PF == 1) {
+        uint4 ra[X3_NA], rb[X3_NB];
+        if (nt > 0) {
+            x3_load(a, b, m0, n0, 0, ra, rb);
+            x3_store(smem, ra, rb);
+        }
+        __syncthreads();
+        for (int64_t t = 0; t < nt; ++t) {
+            const int cur = (int)(t & 1);
+            if (t + 1 < nt) x3_load(a, b, m0, n0, (t + 1) * X3_BK, ra, rb);
+            x3_compute(acc, smem + cur * X3_STAGE, wm, wn, lr, lh);
+            if (t + 1 < nt) x3_store(smem + (1 - cur) * X3_STAGE, ra, rb);
+            __syncthreads();
+        }
+    } else {
+        // prefetch distance 2: the loads of step t+2 are issued before step t computes and
+        // land in LDS at the end of step t+1, so two steps of MFMA work cover their latency
+        uint4 ra0[X3_NA], rb0[X3_NB], ra1[X3_NA], rb1[X3_NB];
+        if (nt > 0) {
+            x3_load(a, b, m0, n0, 0, ra0, rb0);
+            if (nt > 1) x3_load(a, b, m0, n0, X3_BK, ra1, rb1);
+            x3_store(smem, ra0, rb0);
+        }
+        __syncthreads();
+        for (int64_t t = 0; t < nt; t += 2) {
+            if (t + 2 < nt) x3_load(a, b, m0, n0, (t + 2) * X3_BK, ra0, rb0);
+            x3_compute(acc, smem, wm, wn, lr, lh);
+            if (t + 1 < nt) x3_store(smem + X3_STAGE, ra1, rb1);
+            __syncthreads();
+            if (t + 1 >= nt) break;
+            if (t + 3 < nt) x3_load(a, b, m0, n0, (t + 3) * X3_BK, ra1, rb1);
+            x3_compute(acc, smem + X3_STAGE, wm, wn, lr, lh);
+            if (t + 2 < nt) x3_store(smem, ra0, rb0);
+            __syncthreads();
+        }
+    }
+
+    // epilogue: C = alpha * acc * inv_scale + beta * P + gamma * D; optional fp16 split of C
+    const float sc = a.inv_scale[b];
+    const float al_ = a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = a.gamma_v ? a.gamma_v[b] : 0.f;
+    bool ovf = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t col = n0 + 64 * wn + 32 * j + lr;
+            if (col >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + 96 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (row >= a.M) continue;
+                float v = al_ * (acc[i][j][r] * sc);
+                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
+                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
+                a.C[b * a.sc + row * a.ldc + col] = v;
+                if (a.Oh) {
+                    const float hs = v * a.out_scale;
+                    const _Float16 h = (_Float16)hs;
+                    const _Float16 l = (_Float16)(hs - (float)h);
+                    a.Oh[b * a.so + row * a.ldo + col] = h;
+                    a.Ol[b * a.so + row * a.ldo + col] = l;
+                    ovf |= !(fabsf(hs) < 65504.f);
+                }
+            }
+        }
+    if (ovf) atomicOr(a.overflow + b, 1);
+}
+
+// ------------------------------------------------------------------ split / transpose helpers
+
+// Per-batch power-of-two scale s = 2^(14 - ceil(log2 max_i G_ii)) for a PSD G (|G_ij| <=
+// max diag), so the scaled hi halves stay <= 2^14 (fp16 max 65504) with headroom; the
+// kernel stores 1 / (s * x_scale) for the GEMM epilogue and s for the split.
+__global__ void sym_scale_kernel(const float* __restrict__ G, int64_t n, int64_t ldg, int64_t sg,
+                                 float x_scale, float* __restrict__ s_out, float* __restrict__ inv_out) {
+    const int64_t b = blockIdx.x;
+    float m = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(G[b * sg + i * ldg + i]));
+    m = wave_max(m);
+    __shared__ float red[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mm = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mm = fmaxf(mm, red[w]);
+        int e = 0;
+        if (mm > 0.f && isfinite(mm)) {
+            frexpf(mm, &e);  // mm in [2^(e-1), 2^e)
+        }
+        const float s = ldexpf(1.f, 14 - e);
+        s_out[b] = s;
+        inv_out[b] = 1.f / (s * x_scale);
+    }
+}
+
+__global__ void split_kernel(const float* __restrict__ X, int64_t n_per, const float* __restrict__ s_v,
+                             float s_fixed, _Float16* __restrict__ hi, _Float16* __restrict__ lo, int64_t batch) {
+    const int64_t tot4 = batch * n_per / 4;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < tot4; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = q * 4;
+        const float s = s_v ? s_v[e / n_per] : s_fixed;
+        const float4 v = *reinterpret_cast<const float4*>(X + e);
+        const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+        _Float16 h[4], l[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            h[u] = (_Float16)xs[u];
+            l[u] = (_Float16)(xs[u] - (float)h[u]);
+        }
+        *reinterpret_cast<uint2*>(hi + e) = *reinterpret_cast<const uint2*>(h);
+        *reinterpret_cast<uint2*>(lo + e) = *reinterpret_cast<const uint2*>(l);
+    }
+}
+
+// Split of a symmetric matrix of which only the upper triangle (j >= i) is valid: 64 x 64
+// tiles, lower tiles read from the transposed upper tile through LDS.
+__global__ __launch_bounds__(256) void sym_split_upper_kernel(const float* __restrict__ G, int64_t n,
+                                                              const float* __restrict__ s_v,
+                                                              _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+    __shared__ float tile[64][65];
+    const int64_t b = blockIdx.z;
+    const int64_t ti = blockIdx.y, tj = blockIdx.x;
+    const float* Gb = G + b * n * n;
+    const float s = s_v[b];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const bool lower = ti > tj;
+    const int64_t si = lower ? tj : ti, sj = lower ? ti : tj;  // source tile (upper)
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t i = si * 64 + r, j = sj * 64 + tx;
+        // inside a diagonal tile, take (min, max) so only upper entries are read
+        float v = 0.f;
+        if (i < n && j < n) v = (j >= i) ? Gb[i * n + j] : Gb[j * n + i];
+        tile[r][tx] = v;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t i = ti * 64 + r, j = tj * 64 + tx;
+        if (i < n && j < n) {
+            const float v = (lower ? tile[tx][r] : tile[r][tx]) * s;
+            const _Float16 h = (_Float16)v;
+            hi[b * n * n + i * n + j] = h;
+            lo[b * n * n + i * n + j] = (_Float16)(v - (float)h);
+        }
+    }
+}
+
+// Per-batch max |x| as uint bits (atomicMax into a zeroed buffer), then
+// s[b] = 2^(log2_target - e) with max in [2^(e-1), 2^e): the scaled values stay below 2^log2_target.
+__global__ void absmax_bits_kernel(const float* __restrict__ X, int64_t n_per, uint32_t* __restrict__ out) {
+    const int64_t b = blockIdx.y;
+    const float* Xb = X + b * n_per;
+    uint32_t m = 0;
+    const int64_t n4 = n_per / 4;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = *reinterpret_cast<const float4*>(Xb + 4 * q);
+        m = max(m, max(max(abs_bits(v.x), abs_bits(v.y)), max(abs_bits(v.z), abs_bits(v.w))));
+    }
+    for (int64_t q = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n_per;
+         q += (int64_t)gridDim.x * blockDim.x)
+        m = max(m, abs_bits(Xb[q]));
+    m = wave_max_u32(m);
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out + b, m);
+}
+
+__global__ void pow2_scale_kernel(float* __restrict__ s, int64_t batch, int log2_target) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    const float mm = __uint_as_float(reinterpret_cast<const uint32_t*>(s)[b]);
+    int e = 0;
+    if (mm > 0.f && isfinite(mm)) frexpf(mm, &e);
+    s[b] = ldexpf(1.f, log2_target - e);
+}
+
+// Batched transpose Y = X^T (X rows x cols, row-major) through a 64 x 65 LDS tile, with an
+// optional fp16 split of Y (scale s).
+__global__ __launch_bounds__(256) void transpose_split_kernel(const float* __restrict__ X, int64_t rows, int64_t cols,
+                                                              float* __restrict__ Y, _Float16* __restrict__ hi,
+                                                              _Float16* __restrict__ lo, float s_fixed,
+                                                              const float* __restrict__ s_v) {
+    __shared__ float tile[64][65];
+    const int64_t b = blockIdx.z;
+    const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+    const float* Xb = X + b * rows * cols;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = r0 + i, c = c0 + tx;
+        tile[i][tx] = (r < rows && c < cols) ? Xb[r * cols + c] : 0.f;
+    }
+    __syncthreads();
+    const int64_t ob = b * rows * cols;
+    const float s = s_v ? s_v[b] : s_fixed;
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t orow = c0 + i, ocol = r0 + tx;  // Y is cols x rows
+        if (orow < cols && ocol < rows) {
+            const float v = tile[tx][i];
+            if (Y) Y[ob + orow * rows + ocol] = v;
+            if (hi) {
+                const float xs = v * s;
+                const _Float16 h = (_Float16)xs;
+                hi[ob + orow * rows + ocol] = h;
+                lo[ob + orow * rows + ocol] = (_Float16)(xs - (float)h);
+            }
+        }
+    }
+}
+
+}  // namespace cq
+
+using namespace cq;
+
+extern "C" {
+
+int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, float x_scale, uint16_t* Gh,
+                     uint16_t* Gl, float* scale_out, float* inv_scale_out, void* stream) {
+    CQ_REQUIRE(G && Gh && Gl && scale_out && inv_scale_out, "cq_sym_split_f16: null pointer");
+    CQ_REQUIRE(n > 0 && batch > 0 && (n * n) % 4 == 0, "cq_sym_split_f16: bad shape");
+    CQ_REQUIRE(x_scale > 0.f, "cq_sym_split_f16: x_scale must be > 0");
+    hipStream_t s = as_stream(stream);
+    sym_scale_kernel<<<(unsigned)batch, 256, 0, s>>>(G, n, n, n * n, x_scale, scale_out, inv_scale_out);
+    if (upper_only) {
+        CQ_REQUIRE(batch < 65536, "cq_sym_split_f16: batch too large");
+        const unsigned t64 = (unsigned)ceil_div(n, 64);
+        sym_split_upper_kernel<<<dim3(t64, t64, (unsigned)batch), 256, 0, s>>>(
+            G, n, scale_out, reinterpret_cast<_Float16*>(Gh), reinterpret_cast<_Float16*>(Gl));
+        return check_launch("cq_sym_split_f16");
+    }
+    const int64_t tot4 = batch * n * n / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(tot4, 256), 8192);
+    split_kernel<<<grid, 256, 0, s>>>(G, n * n, scale_out, 1.f, reinterpret_cast<_Float16*>(Gh),
+                                      reinterpret_cast<_Float16*>(Gl), batch);
+    return check_launch("cq_sym_split_f16");
+}
+
+int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target, float* scale_out, void* stream) {
+    CQ_REQUIRE(X && scale_out, "cq_pow2_scale: null pointer");
+    CQ_REQUIRE(n_per > 0 && batch > 0 && batch < 65536 && n_per % 4 == 0, "cq_pow2_scale: bad shape");
+    CQ_REQUIRE(log2_target > -100 && log2_target < 100, "cq_pow2_scale: bad target");
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(scale_out, 0, batch * sizeof(float), s) != hipSuccess)
+        return set_error(CQ_EHIP, "cq_pow2_scale: memset failed");
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_per / 4, 256), std::max<int64_t>(1, 2048 / batch)));
+    absmax_bits_kernel<<<dim3(gx, (unsigned)batch), 256, 0, s>>>(X, n_per, reinterpret_cast<uint32_t*>(scale_out));
+    pow2_scale_kernel<<<(unsigned)ceil_div(batch, 256), 256, 0, s>>>(scale_out, batch, log2_target);
+    return check_launch("cq_pow2_scale");
+}
+
+int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scale_v, float scale, uint16_t* hi,
+                 uint16_t* lo, void* stream) {
+    CQ_REQUIRE(X && hi && lo, "cq_split_f16: null pointer");
+    CQ_REQUIRE(n_per > 0 && batch > 0 && n_per % 4 == 0, "cq_split_f16: n_per must be a positive multiple of 4");
+    const int64_t tot4 = batch * n_per / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(tot4, 256), 8192);
+    split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, n_per, scale_v, scale, reinterpret_cast<_Float16*>(hi),
+                                                      reinterpret_cast<_Float16*>(lo), batch);
+    return check_launch("cq_split_f16");
+}
+
+int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch, float* Y, uint16_t* hi,
+                       uint16_t* lo, float scale, const float* scale_v, void* stream) {
+    CQ_REQUIRE(X && (Y || (hi && lo)), "cq_transpose_split: null pointer");
+    CQ_REQUIRE(!hi == !lo, "cq_transpose_split: hi and lo go together");
+    CQ_REQUIRE(rows > 0 && cols > 0 && batch > 0 && batch < 65536, "cq_transpose_split: bad shape");
+    dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64), (unsigned)batch);
+    transpose_split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, rows, cols, Y, reinterpret_cast<_Float16*>(hi),
+                                                                 reinterpret_cast<_Float16*>(lo), scale, scale_v);
+    return check_launch("cq_transpose_split");
+}
+
+int cq_gemm_x3(const cq_x3_args* g, void* stream) {
+    CQ_REQUIRE(g, "cq_gemm_x3: null args");
+    CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && g->C && g->inv_scale, "cq_gemm_x3: null operand");
+    CQ_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0 && g->batch > 0, "cq_gemm_x3: bad shape");
+    CQ_REQUIRE(g->K % X3_BK == 0, "cq_gemm_x3: K must be a multiple of 32");
+    CQ_REQUIRE(g->lda % 8 == 0 && g->ldb % 8 == 0 && g->stride_a % 8 == 0 && g->stride_b % 8 == 0,
+               "cq_gemm_x3: operand rows must be 16-byte aligned");
+    CQ_REQUIRE(g->lda >= g->K && g->ldb >= g->K && g->ldc >= g->N, "cq_gemm_x3: leading dimension too small");
+    CQ_REQUIRE(!g->out_h == !g->out_l, "cq_gemm_x3: out_h and out_l go together");
+    CQ_REQUIRE(!g->out_h || (g->overflow && g->out_scale > 0.f), "cq_gemm_x3: split output needs overflow flags");
+    CQ_REQUIRE(!g->beta_v || g->P, "cq_gemm_x3: beta_v needs P");
+    CQ_REQUIRE(!g->gamma_v || g->D, "cq_gemm_x3: gamma_v needs D");
+    X3K a;
+    a.M = g->M; a.N = g->N; a.K = g->K; a.batch = g->batch;
+    a.Ah = reinterpret_cast<const _Float16*>(g->Ah); a.Al = reinterpret_cast<const _Float16*>(g->Al);
+    a.lda = g->lda; a.sa = g->stride_a;
+    a.Bh = reinterpret_cast<const _Float16*>(g->Bh); a.Bl = reinterpret_cast<const _Float16*>(g->Bl);
+    a.ldb = g->ldb; a.sb = g->stride_b;
+    a.inv_scale = g->inv_scale;
+    a.C = g->C; a.ldc = g->ldc; a.sc = g->stride_c;
+    a.P = g->P; a.ldp = g->ldp; a.sp = g->stride_p;
+    a.D = g->D; a.ldd = g->ldd; a.sd = g->stride_d;
+    a.alpha_v = g->alpha_v; a.beta_v = g->beta_v; a.gamma_v = g->gamma_v;
+    a.Oh = reinterpret_cast<_Float16*>(g->out_h); a.Ol = reinterpret_cast<_Float16*>(g->out_l);
+    a.ldo = g->ldo; a.so = g->stride_o; a.out_scale = g->out_scale;
+    a.overflow = g->overflow;
+    CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && !g->out_h),
+               "cq_gemm_x3: tri needs a square plain product");
+    a.tri = g->tri;
+    a.tiles_n = ceil_div(g->N, X3_BN);
+    a.tiles_m = ceil_div(g->M, X3_BM);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+    static const int pf = [] {
+        const char* e = getenv("CQ_X3_PREFETCH");
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    if (pf == 1) gemm_x3_kernel<1><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
+    else gemm_x3_kernel<2><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
+    return check_launch("cq_gemm_x3");
+}
+
+}  // extern "C"

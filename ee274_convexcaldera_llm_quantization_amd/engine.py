@@ -24,6 +24,7 @@ from dataclasses import dataclass, field
 import torch
 
 from . import _lib as K
+from .overlap import run_to_end
 from .solver import RankRSolver
 
 
@@ -118,24 +119,28 @@ class BatchState:
         self.L_scale = self.R_scale = None
 
     def snapshot_into(self, dst: "BatchState", sel: list[int]):
+        """Copy the state of matrices `sel` into dst (one gather/scatter per tensor)."""
+        B = self.B
+        if dst.L.shape != self.L.shape:
+            dst.L = torch.zeros_like(self.L)
+            dst.R = torch.zeros_like(self.R)
+        if self.L_idxs is not None and (dst.L_idxs is None or dst.L_idxs.shape != self.L_idxs.shape):
+            dst.L_idxs = torch.zeros_like(self.L_idxs)
+            dst.R_idxs = torch.zeros_like(self.R_idxs)
+            dst.L_scale = torch.zeros_like(self.L_scale)
+            dst.R_scale = torch.zeros_like(self.R_scale)
+        pairs = [(dst.Qc, self.Qc), (dst.Qs, self.Qs), (dst.L, self.L), (dst.R, self.R)]
+        if self.L_idxs is not None:
+            pairs += [(dst.L_idxs, self.L_idxs), (dst.R_idxs, self.R_idxs),
+                      (dst.L_scale, self.L_scale), (dst.R_scale, self.R_scale)]
+        if len(sel) == B:
+            for d, s in pairs:
+                d.copy_(s)
+        else:
+            idx = torch.tensor(sel, dtype=torch.long, device=self.Qc.device)
+            for d, s in pairs:
+                d.index_copy_(0, idx, s.index_select(0, idx))
         for b in sel:
-            dst.Qc[b].copy_(self.Qc[b])
-            dst.Qs[b].copy_(self.Qs[b])
-            if dst.L.shape != self.L.shape:
-                dst.L = torch.zeros_like(self.L)
-                dst.R = torch.zeros_like(self.R)
-            dst.L[b].copy_(self.L[b])
-            dst.R[b].copy_(self.R[b])
-            if self.L_idxs is not None:
-                if dst.L_idxs is None or dst.L_idxs.shape != self.L_idxs.shape:
-                    dst.L_idxs = torch.zeros_like(self.L_idxs)
-                    dst.R_idxs = torch.zeros_like(self.R_idxs)
-                    dst.L_scale = torch.zeros_like(self.L_scale)
-                    dst.R_scale = torch.zeros_like(self.R_scale)
-                dst.L_idxs[b].copy_(self.L_idxs[b])
-                dst.R_idxs[b].copy_(self.R_idxs[b])
-                dst.L_scale[b].copy_(self.L_scale[b])
-                dst.R_scale[b].copy_(self.R_scale[b])
             dst.flag_Q[b] = self.has_Q
             dst.flag_LR[b] = self.has_LR
 
@@ -144,10 +149,11 @@ class CalderaEngine:
     """Decomposes a batch of B weight matrices (B, m, n) with shared params and H."""
 
     def __init__(self, params: EngineParams, *, solver_tol: float = 5e-6, solver_p: int | None = None,
-                 profile: bool = False):
+                 filter_precision: str = "f16x3", profile: bool = False):
         self.p = params
         self.solver_tol = solver_tol
         self.solver_p = solver_p
+        self.filter_precision = filter_precision
         self.profile = profile
         self.timings = {}
         self.solver = None
@@ -191,9 +197,10 @@ class CalderaEngine:
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
         Y = Ysrc
         if self.solver is None:
-            self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p)
+            self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
+                                      filter_precision=self.filter_precision)
         sv = self.solver
-        vecs, theta = sv.solve(Ysrc)
+        vecs, theta = yield from sv.solve_iter(Ysrc)
         r = sv.r
         S = torch.sqrt(theta.clamp_min(0.0))  # singular values (fp64)
         S32 = S.float()
@@ -227,7 +234,7 @@ class CalderaEngine:
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
                 K.scale_rc(V, trans=True, rowscale=sq, out=R)
         if quantized:
-            L, R = self._lplr(st, Y, res, L, R, wts)
+            L, R = yield from self._lplr(st, Y, res, L, R, wts)
         st.L, st.R = L, R
         st.has_LR = True
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
@@ -286,7 +293,9 @@ class CalderaEngine:
             else:
                 K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.lplr, err_out=err)
             e32 = torch.sqrt(err).float().double()  # torch.linalg.matrix_norm in fp32
-            better = (e32 < best_err).tolist()
+            better = e32 < best_err
+            yield
+            better = better.tolist()
             sel = [b for b in range(B) if better[b]]
             for b in sel:
                 best["L"][b].copy_(L[b])
@@ -304,7 +313,13 @@ class CalderaEngine:
     def run(self, W: torch.Tensor, h: torch.Tensor | None = None, scale_W: bool = True,
             use_tqdm: bool = False):
         """W (B, m, n) fp16/fp32 on a HIP device; h: (n,) diagonal of H or None.
-        Returns a dict of batched results (see api.py for the dataclass view)."""
+        Returns a list of per-matrix result dicts (see api.py for the dataclass view)."""
+        return run_to_end(self.run_iter(W, h, scale_W, use_tqdm))
+
+    def run_iter(self, W: torch.Tensor, h: torch.Tensor | None = None, scale_W: bool = True,
+                 use_tqdm: bool = False):
+        """Generator form of run(): yields before each host synchronisation, so several
+        engines can be interleaved on their own streams (overlap.run_interleaved)."""
         p = self.p
         if W.dim() == 2:
             W = W.unsqueeze(0)
@@ -336,13 +351,15 @@ class CalderaEngine:
             for mtx in p.update_order:
                 num = None
                 if mtx == "LR" and p.compute_low_rank_factors:
-                    num = self._lr_update(st, Ws, work, res, wts, den)
+                    num = yield from self._lr_update(st, Ws, work, res, wts, den)
                 elif mtx == "Q" and p.compute_quantized_component:
                     num = self._q_update(st, Ws, work, wts, den)
                 updated[mtx] = True
                 if num is None:  # no update: error of the unchanged state
                     num = self._state_error(st, Ws, work, wts)
-                e = torch.sqrt((num.float() / den.float())).tolist()  # fp32 ratio + sqrt (alg.py:297-301)
+                e = torch.sqrt((num.float() / den.float()))  # fp32 ratio + sqrt (alg.py:297-301)
+                yield
+                e = e.tolist()
                 for b in range(B):
                     errors[mtx][b].append(float(e[b]))
                 if all(updated.values()):

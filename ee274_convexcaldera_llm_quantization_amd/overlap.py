@@ -1,0 +1,53 @@
+"""Cooperative interleaving of independent matrix batches on separate HIP streams.
+
+The hot path alternates device-wide GEMMs with one-workgroup-per-matrix p x p kernels
+(Jacobi, whitening, fp64 Grams) that occupy only B of the 256 CUs, and it reads a few
+scalars back to the host once per outer iteration (solver convergence, error history).
+Splitting a batch into parts that run on their own streams lets one part's latency-bound
+kernels and host round trips overlap another part's GEMMs.
+
+The engine and solver are written as generators that `yield` right before every host
+synchronisation; `run_interleaved` resumes each generator with its own stream made
+current, so the work one part queues before its sync point is already on the GPU while
+the host waits for the other part.  No threads: the GIL and the caching allocator see a
+single host thread.
+"""
+from __future__ import annotations
+
+import torch
+
+
+def run_to_end(gen):
+    """Drive one generator to completion on the current stream; return its value."""
+    try:
+        while True:
+            next(gen)
+    except StopIteration as stop:
+        return stop.value
+
+
+def run_interleaved(gens, device):
+    """Round-robin over generators, each on a fresh stream of `device`.  Returns the list
+    of their return values.  The caller's stream is joined before and after."""
+    if len(gens) == 1:
+        return [run_to_end(gens[0])]
+    caller = torch.cuda.current_stream(device)
+    streams = [torch.cuda.Stream(device=device) for _ in gens]
+    for s in streams:
+        s.wait_stream(caller)
+    out = [None] * len(gens)
+    live = list(range(len(gens)))
+    try:
+        while live:
+            for i in list(live):
+                torch.cuda.set_stream(streams[i])
+                try:
+                    next(gens[i])
+                except StopIteration as stop:
+                    out[i] = stop.value
+                    live.remove(i)
+    finally:
+        torch.cuda.set_stream(caller)
+    for s in streams:
+        caller.wait_stream(s)
+    return out

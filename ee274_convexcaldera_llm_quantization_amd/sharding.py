@@ -163,6 +163,7 @@ def engine_decompose_batch(quant_params, device, H_of=None):
     """decompose_batch for the MI355X engine: synthetic fp16 weights randn*0.02 per seed
     (random-init model, no checkpoint access), H_of(name) -> diagonal or None."""
     from .engine import CalderaEngine, EngineParams
+    from .overlap import run_interleaved
 
     def run(batch_items):
         ws = []
@@ -171,10 +172,15 @@ def engine_decompose_batch(quant_params, device, H_of=None):
             ws.append((torch.randn(m, n) * 0.02).to(torch.float16))
         W = torch.stack(ws).to(device)
         h = H_of(batch_items[0][0]) if H_of is not None else None
-        eng = CalderaEngine(EngineParams.from_caldera_params(quant_params))
-        eng.run(W, h)
+        B = W.shape[0]
+        parts = 1
+        bounds = [B * i // parts for i in range(parts + 1)]
+        engines = [CalderaEngine(EngineParams.from_caldera_params(quant_params)) for _ in range(parts)]
+        run_interleaved([e.run_iter(W[bounds[i]:bounds[i + 1]], h) for i, e in enumerate(engines)],
+                        W.device)
+        packed = [d for e in engines for d in e.last_packed]
         out = []
-        for (name, m, n, seed), d in zip(batch_items, eng.last_packed):
+        for (name, m, n, seed), d in zip(batch_items, packed):
             out.append(MatrixResult(name, m, n, d["L"].shape[1], quant_params.Q_bits, d["codes"],
                                     d["Q_scale"], d["L"], d["R"], d["global_scale"], d["errors"]))
         return out

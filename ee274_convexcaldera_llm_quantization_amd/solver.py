@@ -15,68 +15,84 @@ Algorithm, for a batch of B same-shape matrices Y (m x n) in lockstep:
             X <- CholQR2(X)                       (fp64 Gram + symmetric elimination)
             Z = G X; T = X^T Z (fp64); T = V diag(theta) V^T (Jacobi); X <- X V, Z <- Z V
             c <- theta_p (cut);  stop when max_{i<r} ||Z_i - theta_i X_i|| / theta_0 <= tol
-The dense products run on cq_gemm_f32 (v_mfma_f32_32x32x2_f32); the p x p problems run
-one workgroup per matrix (cq_gram_f64 / cq_spd_whiten / cq_jacobi_eigh).  The per-matrix
+The filter products G X run as split-fp16 MFMA products (cq_gemm_x3: each fp32 operand
+carried as two fp16 halves, three v_mfma_f32_32x32x16_f16 per product, fp32 accumulation;
+measured error at or below the fp32 MFMA GEMM's) on X^T so both operands are K-contiguous;
+should a filter iterate ever overflow the fp16 range, the outer iteration is redone with
+the fp32 filter.  The Rayleigh-Ritz product and everything that decides convergence run on
+cq_gemm_f32 (v_mfma_f32_32x32x2_f32); the p x p problems run one workgroup per matrix
+(cq_gram_f64 / cq_spd_whiten / cq_jacobi_eigh).  The per-matrix
 filter coefficients are passed as per-batch vectors, so the whole batch stays on device;
 the only host synchronisation is the convergence test once per outer iteration.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib as K
+from .overlap import run_to_end
 
 
 class _EventProbe:
     """HIP-event timing of the dominant kernel (the G X filter GEMM) on the stream it is
-    launched on; used by bench.py inside its timed region (roofline.achieved)."""
+    launched on; used by bench.py inside its timed region (roofline.achieved).  The event
+    pairs are created up front (hipEventCreate per launch costs more than the launch) and
+    the first `max_pairs` filter launches of the timed region are sampled."""
 
     def __init__(self):
         self.on = False
-        self.pairs = []
+        self.pool = []
+        self.used = 0
         self.flops = 0
 
-    def enable(self, on: bool):
+    def enable(self, on: bool, max_pairs: int = 96):
         self.on = on
         if on:
-            self.pairs = []
+            self.pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                         for _ in range(max_pairs)]
+            self.used = 0
 
-    def start(self, flops):
-        if not self.on:
+    def start(self, flops, nbytes=0.0, kernel=""):
+        if not self.on or self.used >= len(self.pool):
             return None
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        self.flops = flops
-        return (e0, e1)
+        ev = self.pool[self.used]
+        self.used += 1
+        ev[0].record()
+        self.flops, self.nbytes, self.kernel = flops, nbytes, kernel
+        return ev
 
     def stop(self, ev):
         if ev is not None:
             ev[1].record()
-            self.pairs.append(ev)
 
     def summary(self):
-        if not self.pairs:
+        if not self.used:
             return {"count": 0}
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b in self.pairs]
-        return {"count": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": self.flops}
+        ms = [a.elapsed_time(b) for a, b in self.pool[: self.used]]
+        return {"count": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": self.flops,
+                "bytes_per_launch": self.nbytes, "kernel": self.kernel}
 
 
 EVENT_PROBE = _EventProbe()
+
+
+X3_SCALE = 2.0 ** 6  # power-of-two scale of the filter iterates' fp16 halves (entries <= ~1)
 
 
 class SolverStats:
     def __init__(self):
         self.outer = 0
         self.matvecs = 0
+        self.x3_fallbacks = 0
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
 
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
-                    max_resid=self.max_resid)
+                    max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks)
 
 
 class RankRSolver:
@@ -84,7 +100,7 @@ class RankRSolver:
 
     def __init__(self, B: int, m: int, n: int, r: int, device, *, p: int | None = None,
                  tol: float = 5e-6, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 10, 10, 10, 10, 10),
-                 seed: int = 0x5EED, jacobi_tol: float = 1e-13):
+                 seed: int = 0x5EED, jacobi_tol: float = 1e-13, filter_precision: str = "f16x3"):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -109,13 +125,29 @@ class RankRSolver:
         self.stats = SolverStats()
         self._bufs = None
         self._G = None
+        self._yh = self._yl = None
+        if filter_precision not in ("f16x3", "f32"):
+            raise ValueError(f"filter_precision must be 'f16x3' or 'f32', got {filter_precision!r}")
+        # split-fp16 filter needs K (= k) a multiple of 32 and 16-byte aligned rows
+        self.x3 = filter_precision == "f16x3" and not self.direct and self.k % 32 == 0
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
         B, k, p = self.B, self.k, self.p
         if self._bufs is None:
-            self._bufs = [torch.empty((B, k, p), dtype=torch.float32, device=dev) for _ in range(4)]
+            # 5 buffers: an outer iteration keeps its input alive until its overflow check
+            self._bufs = [torch.empty((B, k, p), dtype=torch.float32, device=dev) for _ in range(5)]
             self._G = torch.empty((B, k, k), dtype=torch.float32, device=dev)
+            if self.x3:
+                f16 = torch.float16
+                self._Gh = torch.empty((B, k, k), dtype=f16, device=dev)
+                self._Gl = torch.empty((B, k, k), dtype=f16, device=dev)
+                self._gscale = torch.empty(B, dtype=torch.float32, device=dev)
+                self._ginv = torch.empty(B, dtype=torch.float32, device=dev)
+                self._xt = [torch.empty((B, p, k), dtype=torch.float32, device=dev) for _ in range(2)]
+                self._xh = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
+                self._xl = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
+                self._ovf = torch.zeros(B, dtype=torch.int32, device=dev)
 
     def _free(self, *used):
         for b in self._bufs:
@@ -131,52 +163,111 @@ class RankRSolver:
         K.gemm(X, Wt32, C=out)
         return out, info
 
-    def _rr(self, X):
+    def _rr(self, X, *keep):
         G = self._G
-        Z = self._free(X)
-        K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
+        Z = self._free(X, *keep)
+        if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
+            K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE)
+            K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0])
+            K.transpose_split(self._xt[0], out=Z)
+        else:
+            K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
         theta, V32, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol)
-        Xo = self._free(X, Z)
+        Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
-        Zo = self._free(X, Z, Xo)
+        Zo = self._free(X, Z, Xo, *keep)
         K.gemm(Z, V32, C=Zo)
         return theta, Xo, Zo
 
-    def _filter(self, X, theta, deg):
-        """X <- p_d(G) X, p_d = Chebyshev polynomial of degree deg damping [0, c], c = theta_p,
-        scaled to 1 at theta_0 (scaled 3-term recurrence).  Overwrites X's buffer."""
-        G = self._G
-        c = theta[:, self.p - 1].clamp_min(0.0)
-        ref = theta[:, 0]
+    def _cheb_coeffs(self, ends, deg, dev):
+        """Coefficients of the scaled 3-term recurrence, from the host copy of the Ritz values
+        ends = [(theta_0, theta_{p-1}) per matrix] (fp64, as read back at the convergence
+        check).  Returns a (deg, 3, B) fp32 device tensor: step i computes
+        X_{i+1} = a_i G X_i + b_i X_{i-1} + c_i X_i."""
+        ref = ends[:, 0]
+        c = np.maximum(ends[:, 1], 0.0)
         ok = (c > 0) & (ref > c * (1 + 1e-6))
-        e = torch.where(ok, c / 2.0, torch.ones_like(c))
-        ctr = torch.where(ok, c / 2.0, torch.zeros_like(c))
-        t0 = torch.where(ok, (ref - ctr) / e, torch.full_like(c, 2.0))
+        e = np.where(ok, c / 2.0, 1.0)
+        ctr = np.where(ok, c / 2.0, 0.0)
+        t0 = np.where(ok, (ref - ctr) / e, 2.0)
         s = 1.0 / t0
-        Y1 = self._free(X)
-        fl = 2.0 * self.k * self.k * self.p * self.B
-        # Y1 = (s/e) G X - (s ctr/e) X
-        ev = EVENT_PROBE.start(fl)
-        K.gemm(G, X, ta=True, C=Y1, D=X, alpha_v=(s / e).float(), gamma_v=(-s * ctr / e).float())
-        EVENT_PROBE.stop(ev)
-        self.stats.matvecs += 1
-        prev, cur = X, Y1
+        rows = [(s / e, np.zeros_like(s), -s * ctr / e)]
         for _ in range(1, deg):
             sn = 1.0 / (2.0 * t0 - s)
-            a_v, b_v, g_v = (2 * sn / e).float(), (-sn * s).float(), (-2 * sn * ctr / e).float()
-            # prev <- (2 sn/e) G cur + (-sn s) prev + (-2 sn ctr/e) cur
-            ev = EVENT_PROBE.start(fl)
-            K.gemm(G, cur, ta=True, C=prev, D=cur, alpha_v=a_v, beta_v=b_v, gamma_v=g_v)
+            rows.append((2 * sn / e, -sn * s, -2 * sn * ctr / e))
+            s = sn
+        tab = torch.from_numpy(np.asarray(rows, dtype=np.float64).astype(np.float32))
+        return tab.to(dev)
+
+    def _filter(self, X, coef):
+        """X <- p_d(G) X, p_d = Chebyshev polynomial of degree d = len(coef) damping [0, c],
+        c = theta_p, scaled to 1 at theta_0 (scaled 3-term recurrence).  Returns a buffer
+        other than X's (X is left intact)."""
+        if self.x3:
+            return self._filter_x3(X, coef)
+        G = self._G
+        deg = coef.shape[0]
+        X0 = self._free(X)  # the recurrence overwrites its buffers: keep the input intact
+        X0.copy_(X)
+        Y1 = self._free(X, X0)
+        fl = 2.0 * self.k * self.k * self.p * self.B
+        nb = float(self.B) * (4.0 * self.k * self.k + 16.0 * self.p * self.k)
+        kn = "gemm_f32_kernel (fp32 G X, Chebyshev filter)"
+        ev = EVENT_PROBE.start(fl, nb, kn)
+        K.gemm(G, X0, ta=True, C=Y1, D=X0, alpha_v=coef[0, 0], gamma_v=coef[0, 2])
+        EVENT_PROBE.stop(ev)
+        self.stats.matvecs += 1
+        prev, cur = X0, Y1
+        for i in range(1, deg):
+            # prev <- a G cur + b prev + c cur
+            ev = EVENT_PROBE.start(fl, nb, kn)
+            K.gemm(G, cur, ta=True, C=prev, D=cur, alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2])
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
-            prev, cur, s = cur, prev, sn
+            prev, cur = cur, prev
         return cur
+
+    def _filter_x3(self, X, coef):
+        """Same recurrence on X^T with split-fp16 products (cq_gemm_x3); X is left intact."""
+        deg = coef.shape[0]
+        xt, xh, xl = self._xt, self._xh, self._xl
+        K.transpose_split(X, out=xt[0], hi=xh[0], lo=xl[0], scale=X3_SCALE)
+        fl = 2.0 * self.k * self.k * self.p * self.B
+        # bytes a recurrence step moves: G halves (4 B/elem) + X^T halves + prev, cur in,
+        # new out (fp32) + new halves out
+        nb = float(self.B) * (4.0 * self.k * self.k + 20.0 * self.p * self.k)
+        kn = "gemm_x3_kernel (split-fp16 G X, Chebyshev filter)"
+        last = deg == 1
+        ev = EVENT_PROBE.start(fl, nb, kn)
+        K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
+                  gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
+                  out_scale=X3_SCALE, overflow=self._ovf)
+        EVENT_PROBE.stop(ev)
+        self.stats.matvecs += 1
+        prev, cur = 0, 1
+        for i in range(1, deg):
+            last = i == deg - 1
+            ev = EVENT_PROBE.start(fl, nb, kn)
+            K.gemm_x3(xh[cur], xl[cur], self._Gh, self._Gl, self._ginv, xt[prev], P=xt[prev], D=xt[cur],
+                      alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
+                      out_h=None if last else xh[prev], out_l=None if last else xl[prev],
+                      out_scale=X3_SCALE, overflow=self._ovf)
+            EVENT_PROBE.stop(ev)
+            self.stats.matvecs += 1
+            prev, cur = cur, prev
+        out = self._free(X)
+        K.transpose_split(xt[cur], out=out)
+        return out
 
     # ------------------------------------------------------------------ main entry
     def solve(self, Y: torch.Tensor, warm: bool = True):
         """Y (B, m, n) fp32 -> (vecs (B, k, r), theta (B, r) fp64 eigenvalues of G, descending)."""
+        return run_to_end(self.solve_iter(Y, warm))
+
+    def solve_iter(self, Y: torch.Tensor, warm: bool = True):
+        """Generator form of solve(): yields before each host synchronisation (overlap.py)."""
         B, k, p = self.B, self.k, self.p
         dev = Y.device
         self.stats.calls += 1
@@ -185,35 +276,78 @@ class RankRSolver:
             theta, V32, _, _ = K.jacobi_eigh(Gd)
             return V32[:, :, : self.r], theta[:, : self.r]
         self._alloc(dev)
-        if self.left:
+        self._g_upper_only = False
+        if self.x3 and (self.n if self.left else self.m) % 32 == 0:
+            # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two
+            if self._yh is None:
+                self._yh = torch.empty((B, k, Y.shape[1] + Y.shape[2] - k), dtype=torch.float16, device=dev)
+                self._yl = torch.empty_like(self._yh)
+                self._ys = torch.empty(B, dtype=torch.float32, device=dev)
+            K.pow2_scale(Y, 14, out=self._ys)
+            if self.left:
+                K.split_f16(Y, self._ys, hi=self._yh, lo=self._yl)
+            else:
+                K.transpose_split(Y, hi=self._yh, lo=self._yl, scale=self._ys)
+            yinv = 1.0 / (self._ys * self._ys)
+            K.gemm_x3(self._yh, self._yl, self._yh, self._yl, yinv, self._G, tri=True)  # upper triangle
+            self._g_upper_only = True
+        elif self.left:
             K.gemm(Y, Y, tb=True, C=self._G, syrk=True)  # Y Y^T (upper tiles + mirror)
         else:
             K.gemm(Y, Y, ta=True, C=self._G, syrk=True)  # Y^T Y
+        if self.x3:
+            K.sym_split_f16(self._G, X3_SCALE, hi=self._Gh, lo=self._Gl, scale=self._gscale,
+                            inv_scale=self._ginv, upper_only=self._g_upper_only)
+            self._ovf.zero_()
         cold = not (warm and self.X is not None)
-        X = self._bufs[0]
         if cold:
+            # same start block for every matrix: a matrix's result does not depend on its
+            # position in the batch or on how the batch is split across streams
+            X = self._bufs[0]
             g = torch.Generator(device=dev)
             g.manual_seed(self.seed)
-            X.copy_(torch.randn((B, k, p), generator=g, device=dev, dtype=torch.float32))
+            X.copy_(torch.randn((1, k, p), generator=g, device=dev, dtype=torch.float32).expand(B, k, p))
             X, _ = self._cholqr(X)
             X, _ = self._cholqr(X)
             theta, X, Z = self._rr(X)
+            ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
+            yield
+            ends = ends.cpu().numpy()
             degs = self.deg_cold
         else:
-            # previous Ritz block and values: orthonormal, and its Ritz values bound the new
-            # spectrum closely (the residual changes in <1% of its entries between updates)
-            X.copy_(self.X)
+            # previous Ritz block (kept in self.X, never handed out by the pool) and values:
+            # orthonormal, and its Ritz values bound the new spectrum closely (the residual
+            # changes in <1% of its entries between updates)
+            X = self.X
             theta = self.theta
+            ends = self._ends
             degs = self.deg_warm
         self.stats.resid_hist = []
         for d in degs:
             self.stats.outer += 1
-            Xf = self._filter(X, theta, d)
-            Xa, _ = self._cholqr(Xf)
-            Xb, _ = self._cholqr(Xa)
-            theta, X, Z = self._rr(Xb)
-            res = K.ritz_residual(X, Z, theta, self.r)
-            mr = float(res.max().item())
+            while True:
+                coef = self._cheb_coeffs(ends, d, dev)
+                Xf = self._filter(X, coef)
+                Xa, _ = self._cholqr(Xf, X)
+                Xb, _ = self._cholqr(Xa, X)
+                theta_n, Xn, Zn = self._rr(Xb, X)
+                res = K.ritz_residual(Xn, Zn, theta_n, self.r).max()
+                ovf = self._ovf.max().double() if self.x3 else torch.zeros((), dtype=torch.float64, device=dev)
+                chk = torch.cat([res.double().view(1), ovf.view(1), theta_n[:, 0], theta_n[:, p - 1]])
+                yield
+                chk = chk.cpu().numpy()
+                if self.x3 and chk[1] != 0:
+                    # an fp16 half overflowed: redo this outer iteration with the fp32 filter
+                    self.x3 = False
+                    self.stats.x3_fallbacks += 1
+                    if self._g_upper_only:  # the fp32 products need the full G
+                        self._G.copy_(torch.triu(self._G) + torch.triu(self._G, 1).transpose(1, 2))
+                        self._g_upper_only = False
+                    continue
+                break
+            theta, X, Z = theta_n, Xn, Zn
+            ends = np.stack([chk[2:2 + B], chk[2 + B:2 + 2 * B]], 1)
+            mr = float(chk[0])
             self.stats.max_resid = mr
             self.stats.resid_hist.append(mr)
             if mr <= self.tol:
@@ -225,4 +359,5 @@ class RankRSolver:
             self.X = torch.empty((B, k, p), dtype=torch.float32, device=dev)
         self.X.copy_(X)
         self.theta = theta.clone()
+        self._ends = ends
         return self.X[:, :, : self.r], theta[:, : self.r]

@@ -174,6 +174,53 @@ int cq_ritz_residual(const float* X, const float* Z, const double* theta, int64_
                      int64_t p, int64_t r, int64_t batch, float* out, void* ws,
                      size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Split-fp16 ("f16x3") products with a symmetric Gram, fp32-grade accuracy on the fp16
+ * MFMA (the subspace filter of the SVD replacing alg.py:217).  A value x*s (s a power of
+ * two) is held as two fp16 halves hi = f16(x*s), lo = f16(x*s - hi); fp16 buffers are
+ * passed as uint16_t.
+ */
+/* Gh/Gl[b] = split of G[b] (n x n PSD, row-major) scaled by scale_out[b] = 2^(14 -
+ * ceil(log2 max_i G_ii)); inv_scale_out[b] = 1 / (scale_out[b] * x_scale).  upper_only:
+ * only G's upper triangle (j >= i) is read and mirrored into the full split. */
+int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, float x_scale,
+                     uint16_t* Gh, uint16_t* Gl, float* scale_out, float* inv_scale_out,
+                     void* stream);
+/* scale_out[b] = 2^(log2_target - e) with max|X[b]| in [2^(e-1), 2^e) (1 for all-zero X[b]). */
+int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target, float* scale_out,
+                  void* stream);
+/* hi/lo[b] = split of X[b] (n_per values) scaled by scale_v[b] (or scale if scale_v NULL). */
+int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scale_v, float scale,
+                 uint16_t* hi, uint16_t* lo, void* stream);
+/* Y[b] = X[b]^T (X rows x cols row-major -> Y cols x rows), and/or its split (scale_v[b], or
+ * scale if scale_v is NULL). */
+int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch, float* Y,
+                       uint16_t* hi, uint16_t* lo, float scale, const float* scale_v, void* stream);
+
+typedef struct cq_x3_args {
+    int64_t M, N, K, batch;
+    const uint16_t *Ah, *Al;       /* M x K halves (row-major, ld lda, batch stride) */
+    int64_t lda, stride_a;
+    const uint16_t *Bh, *Bl;       /* N x K halves: op(B)[k][n] = B[n][k] */
+    int64_t ldb, stride_b;
+    const float* inv_scale;        /* [batch]: 1 / (scale_A * scale_B) */
+    float* C;                      /* M x N fp32 */
+    int64_t ldc, stride_c;
+    const float* P;                /* beta term operand (may alias C) */
+    int64_t ldp, stride_p;
+    const float* D;                /* gamma term operand */
+    int64_t ldd, stride_d;
+    const float *alpha_v, *beta_v, *gamma_v;  /* [batch] each; NULL = 1, 0, 0 */
+    uint16_t *out_h, *out_l;       /* optional split of C (scale out_scale) */
+    int64_t ldo, stride_o;
+    float out_scale;
+    int* overflow;                 /* [batch]: set to 1 when |C * out_scale| >= 65504 */
+    int tri;                       /* C symmetric (M == N, plain product): tiles entirely below
+                                      the diagonal are skipped; the upper triangle is exact */
+} cq_x3_args;
+/* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
+int cq_gemm_x3(const cq_x3_args* a, void* stream);
+
 /* Chebyshev 3-term recurrence support and elementwise helpers. */
 /* out[b] = sum(x[b]^2 * w[j % ncols]) fp64 (w may be NULL) — denominators of alg.py:298 */
 int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel,

@@ -31,13 +31,17 @@ def test_library_exports_every_header_symbol():
     assert isinstance(lib.cq_last_error(), bytes)
 
 
+def _struct_fields(name):
+    txt = open(HEADER).read()
+    body = txt[txt.index(f"typedef struct {name}"):txt.index(f"}} {name};")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    return re.findall(r"([A-Za-z_][A-Za-z0-9_]*)\s*[;,]", body.split("{", 1)[1])
+
+
 def test_gemm_args_struct_matches_header():
     import ee274_convexcaldera_llm_quantization_amd._lib as K
-    txt = open(HEADER).read()
-    body = txt[txt.index("typedef struct cq_gemm_args"):txt.index("} cq_gemm_args;")]
-    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    fields = re.findall(r"([A-Za-z_][A-Za-z0-9_]*)\s*[;,]", body.split("{", 1)[1])
-    assert [f for f, _ in K.GemmArgs._fields_] == fields
+    assert [f for f, _ in K.GemmArgs._fields_] == _struct_fields("cq_gemm_args")
+    assert [f for f, _ in K.X3Args._fields_] == _struct_fields("cq_x3_args")
 
 
 def test_caldera_params_defaults_match_reference():

@@ -5,6 +5,7 @@ update codes, teacher-forced quantise calls); float tolerance where an SVD or ls
 between (1e-4 relative Frobenius on Q+LR, the north-star bar).  Later outer iterations of
 the reference are chaotic: there, errors are compared loosely."""
 import hashlib
+import math
 
 import numpy as np
 import pytest
@@ -136,3 +137,49 @@ def test_cfg2_full_size(api, large):
     ref = large["cfg2_sketch_QLR"]
     rel = np.linalg.norm(sk - ref) / np.linalg.norm(ref)
     assert rel < 1e-4, rel
+
+
+def test_stream_split_matches_single_stream():
+    """A batch split across two interleaved HIP streams (overlap.py) gives the same
+    decompositions as one stream: integer work bit-exact, Q+LR to the solver tolerance."""
+    from ee274_convexcaldera_llm_quantization_amd.api import caldera_batch
+    from src.caldera.utils.dataclasses import CalderaParams
+    qp = CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=32, iters=3, update_order=["Q", "LR"],
+                       sigma_reg=1e-8)
+    g = torch.Generator().manual_seed(7)
+    W = (torch.randn(4, 512, 1024, generator=g) * 0.02).half().to(DEV)
+    one = caldera_batch(qp, W, None, device=DEV, streams=1)
+    two = caldera_batch(qp, W, None, device=DEV, streams=2)
+    for a, b in zip(one, two):
+        assert a.global_scale == b.global_scale
+        assert abs(a.errors["Q"][0] - b.errors["Q"][0]) == 0.0  # first Q update: no SVD before it
+        qa = a.Q.double() + a.L.double() @ a.R.double()
+        qb = b.Q.double() + b.L.double() @ b.R.double()
+        assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qa)) < 1e-4
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "f32", "overflow"])
+def test_solver_filter_precisions(prec, monkeypatch):
+    """Top-r eigenpairs of Y Y^T from the split-fp16 filter, the fp32 filter, and the fp32
+    fallback after a forced fp16 overflow all match LAPACK (fp64) to the solver tolerance."""
+    from ee274_convexcaldera_llm_quantization_amd import solver as S
+    g = torch.Generator().manual_seed(11)
+    m, n, r = 512, 768, 32
+    Y = (torch.randn(2, m, n, generator=g) * 0.3).to(DEV)
+    if prec == "overflow":
+        monkeypatch.setattr(S, "X3_SCALE", 2.0 ** 18)  # iterates' halves exceed the fp16 range
+    sv = S.RankRSolver(2, m, n, r, DEV, filter_precision="f32" if prec == "f32" else "f16x3")
+    U, th = sv.solve(Y)
+    assert sv.stats.max_resid <= 5e-6
+    if prec == "overflow":
+        assert sv.stats.x3_fallbacks == 1 and not sv.x3
+    elif prec == "f16x3":
+        assert sv.x3 and sv.stats.x3_fallbacks == 0
+    Yd = Y.double().cpu()
+    for b in range(2):
+        ev, V = torch.linalg.eigh(Yd[b] @ Yd[b].T)
+        ev, V = ev.flip(0)[:r], V.flip(1)[:, :r]
+        assert torch.allclose(th[b].cpu(), ev, rtol=1e-6, atol=0)
+        P1 = U[b].double().cpu() @ U[b].double().cpu().T
+        P2 = V @ V.T
+        assert torch.linalg.norm(P1 - P2) / math.sqrt(r) < 1e-4

@@ -1,4 +1,6 @@
 """HIP kernels (through the C-ABI) against the reference fixtures and fp64 references."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -284,3 +286,132 @@ def test_gemm_syrk_mode(K, ta, n):
     assert torch.isfinite(Cc).all()
     assert (Cc - ref).abs().max().item() < 1e-5 * ref.abs().max().item()
     assert torch.equal(Cc, Cc.transpose(1, 2))
+
+
+# ------------------------------------------------------------------ split-fp16 (f16x3) products
+def _x3_split_ref(x, s):
+    xs = x * s
+    hi = xs.half()
+    lo = (xs - hi.float()).half()
+    return hi, lo
+
+
+def test_transpose_split_exact(K):
+    g = torch.Generator(device=DEV).manual_seed(3)
+    X = torch.randn(3, 200, 130, device=DEV, generator=g)
+    Y = torch.empty(3, 130, 200, device=DEV)
+    hi = torch.empty(3, 130, 200, device=DEV, dtype=torch.float16)
+    lo = torch.empty_like(hi)
+    K.transpose_split(X, out=Y, hi=hi, lo=lo, scale=64.0)
+    assert torch.equal(Y, X.transpose(1, 2))
+    rh, rl = _x3_split_ref(X.transpose(1, 2).contiguous(), 64.0)
+    assert torch.equal(hi, rh) and torch.equal(lo, rl)
+    # hi + lo carries x * s to 2^-22 relative
+    rec = (hi.double() + lo.double()) / 64.0
+    # (plus the fp16 subnormal spacing of lo, 2^-24, for the smallest entries)
+    xt = X.transpose(1, 2).double()
+    assert ((rec - xt).abs() <= 2.0 ** -21 * xt.abs() + 2.0 ** -24 / 64.0).all()
+
+
+def test_sym_split_scale_and_halves(K):
+    g = torch.Generator(device=DEV).manual_seed(4)
+    Y = torch.randn(2, 96, 300, device=DEV, generator=g) * torch.tensor([0.01, 3.0], device=DEV).view(2, 1, 1)
+    G = torch.matmul(Y, Y.transpose(1, 2)).contiguous()
+    hi, lo, s, inv = K.sym_split_f16(G, 64.0)
+    for b in range(2):
+        mx = torch.diagonal(G[b]).max().item()
+        sb = s[b].item()
+        assert math.log2(sb) == int(math.log2(sb))          # power of two
+        assert 2.0 ** 13 <= mx * sb < 2.0 ** 14 + 1e-3       # hi halves stay <= 2^14
+        assert inv[b].item() == pytest.approx(1.0 / (sb * 64.0), rel=0, abs=0)
+        rh, rl = _x3_split_ref(G[b], sb)
+        assert torch.equal(hi[b], rh) and torch.equal(lo[b], rl)
+    # upper-only input (lower triangle garbage) gives the same split
+    Gu = torch.triu(G) + torch.tril(torch.full_like(G, 7.0), -1)
+    hu, lu, su, _ = K.sym_split_f16(Gu, 64.0, upper_only=True)
+    assert torch.equal(hu, hi) and torch.equal(lu, lo) and torch.equal(su, s)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(192, 256, 512), (96, 320, 256), (200, 520, 1024)])
+def test_gemm_x3_matches_fp64(K, M, N, Kd):
+    """C = A B^T from fp16 halves, fp32-grade: column errors within 3x the fp32 GEMM's
+    (unsymmetric B checks the row/column placement)."""
+    Bt = 3
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g) * 0.1
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g) * 5.0
+    sa, sb = 2.0 ** 6, 2.0 ** 10
+    Ah, Al = _x3_split_ref(A, sa)
+    Bh, Bl = _x3_split_ref(Bm, sb)
+    inv = torch.full((Bt,), 1.0 / (sa * sb), device=DEV)
+    C = torch.empty(Bt, M, N, device=DEV)
+    K.gemm_x3(Ah.contiguous(), Al.contiguous(), Bh.contiguous(), Bl.contiguous(), inv, C)
+    ref = torch.matmul(A.double(), Bm.double().transpose(1, 2))
+    c32 = torch.matmul(A, Bm.transpose(1, 2)).double()
+    err = ((C.double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    err32 = ((c32 - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < max(3 * err32, 1e-6), (err, err32)
+
+
+def test_gemm_x3_tri_upper_exact(K):
+    """tri mode: the upper triangle of Y Y^T equals the full product's bit for bit."""
+    g = torch.Generator(device=DEV).manual_seed(21)
+    Y = torch.randn(2, 600, 320, device=DEV, generator=g)
+    s = K.pow2_scale(Y, 14)
+    yh, yl = K.split_f16(Y, s)
+    inv = 1.0 / (s * s)
+    full = torch.empty(2, 600, 600, device=DEV)
+    K.gemm_x3(yh, yl, yh, yl, inv, full)
+    up = torch.full_like(full, float("nan"))
+    K.gemm_x3(yh, yl, yh, yl, inv, up, tri=True)
+    iu = torch.triu_indices(600, 600, device=DEV)
+    assert torch.equal(up[:, iu[0], iu[1]], full[:, iu[0], iu[1]])
+
+
+def test_gemm_x3_recurrence_epilogue_and_split(K):
+    Bt, M, N, Kd = 2, 192, 256, 256
+    g = torch.Generator(device=DEV).manual_seed(9)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g)
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g)
+    P = torch.randn(Bt, M, N, device=DEV, generator=g)
+    D = torch.randn(Bt, M, N, device=DEV, generator=g)
+    Ah, Al = _x3_split_ref(A, 1.0)
+    Bh, Bl = _x3_split_ref(Bm, 1.0)
+    inv = torch.ones(Bt, device=DEV)
+    al = torch.tensor([0.5, 2.0], device=DEV)
+    be = torch.tensor([-1.0, 0.25], device=DEV)
+    ga = torch.tensor([0.125, -3.0], device=DEV)
+    C = P.clone()  # in place: prev is overwritten by the new iterate
+    Oh = torch.empty(Bt, M, N, device=DEV, dtype=torch.float16)
+    Ol = torch.empty_like(Oh)
+    ovf = torch.zeros(Bt, dtype=torch.int32, device=DEV)
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C, P=C, D=D, alpha_v=al, beta_v=be, gamma_v=ga, out_h=Oh, out_l=Ol,
+              out_scale=4.0, overflow=ovf)
+    prod = torch.matmul(A.double(), Bm.double().transpose(1, 2))
+    ref = al.double().view(-1, 1, 1) * prod + be.double().view(-1, 1, 1) * P.double() + ga.double().view(-1, 1, 1) * D.double()
+    assert ((C.double() - ref).abs().max() / ref.abs().max()).item() < 2e-6
+    rh, rl = _x3_split_ref(C, 4.0)
+    assert torch.equal(Oh, rh) and torch.equal(Ol, rl)
+    assert ovf.tolist() == [0, 0]
+    # overflow of the fp16 split is flagged per batch
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C, alpha_v=torch.tensor([1.0, 1e6], device=DEV), out_h=Oh, out_l=Ol,
+              out_scale=4.0, overflow=ovf)
+    assert ovf.tolist() == [0, 1]
+
+
+def test_pow2_scale_and_split(K):
+    g = torch.Generator(device=DEV).manual_seed(5)
+    X = torch.randn(3, 100, 64, device=DEV, generator=g) * torch.tensor([1e-3, 1.0, 0.0], device=DEV).view(3, 1, 1)
+    s = K.pow2_scale(X, 14)
+    assert s[2].item() == 2.0 ** 14  # all-zero matrix: max 0 -> e = 0
+    for b in range(2):
+        mx = X[b].abs().max().item()
+        assert 2.0 ** 13 <= mx * s[b].item() < 2.0 ** 14
+    hi, lo = K.split_f16(X, s)
+    rh, rl = _x3_split_ref(X, s.view(3, 1, 1))
+    assert torch.equal(hi, rh) and torch.equal(lo, rl)
+    Y = torch.empty(3, 64, 100, device=DEV)
+    th = torch.empty(3, 64, 100, device=DEV, dtype=torch.float16)
+    tl = torch.empty_like(th)
+    K.transpose_split(X, out=Y, hi=th, lo=tl, scale=s)
+    assert torch.equal(th, rh.transpose(1, 2)) and torch.equal(tl, rl.transpose(1, 2))
