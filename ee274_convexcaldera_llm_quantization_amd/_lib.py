@@ -55,6 +55,7 @@ class X3Args(ctypes.Structure):
         ("out_scale", c_float),
         ("overflow", c_vp),
         ("tri", c_int),
+        ("b_blocked", c_int),
     ]
 
 
@@ -87,7 +88,7 @@ _SIGS = {
     "cq_weighted_sqsum": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_scale_rc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                             c_i64, c_vp, c_i64, c_vp]),
-    "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cq_transpose_split": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp]),
@@ -384,7 +385,7 @@ def scale_rc(X, *, trans=False, rowscale=None, colscale=None, out=None):
 
 # ---------------------------------------------------------------------------- split-fp16 products
 def sym_split_f16(G: torch.Tensor, x_scale: float, *, hi=None, lo=None, scale=None, inv_scale=None,
-                  upper_only=False):
+                  upper_only=False, blocked=False):
     """G (B, n, n) fp32 PSD -> (hi, lo fp16, scale (B,), inv_scale (B,) = 1/(scale*x_scale)).
     upper_only: only G's upper triangle is valid (x3 tri Gram); the split is mirrored."""
     _require_hip(G)
@@ -395,7 +396,8 @@ def sym_split_f16(G: torch.Tensor, x_scale: float, *, hi=None, lo=None, scale=No
     lo = torch.empty((B, n, n), dtype=torch.float16, device=dev) if lo is None else lo
     scale = torch.empty(B, dtype=torch.float32, device=dev) if scale is None else scale
     inv_scale = torch.empty(B, dtype=torch.float32, device=dev) if inv_scale is None else inv_scale
-    _check(load().cq_sym_split_f16(_p(G), n, B, int(bool(upper_only)), float(x_scale), _p(hi), _p(lo), _p(scale),
+    _check(load().cq_sym_split_f16(_p(G), n, B, int(bool(upper_only)), int(bool(blocked)), float(x_scale), _p(hi),
+                                   _p(lo), _p(scale),
                                    _p(inv_scale),
                                    _stream(dev)), "cq_sym_split_f16")
     return hi, lo, scale, inv_scale
@@ -440,9 +442,10 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None):
 
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
-            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False):
+            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
-    B = Bh + Bl (B, N, K) fp16 halves; optional fp16 split of C into out_h/out_l."""
+    B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
+    same storage size); optional fp16 split of C into out_h/out_l."""
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, M, Kd = Ah.shape
     N = Bh.shape[1]
@@ -452,7 +455,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g = X3Args()
     g.M, g.N, g.K, g.batch = M, N, Kd, Bt
     g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), Kd, M * Kd
-    g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), Kd, N * Kd
+    g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), (N if b_blocked else Kd), N * Kd
     g.inv_scale = inv_scale.data_ptr()
     g.C, g.ldc, g.stride_c = C.data_ptr(), N, M * N
     if P is not None:
@@ -467,5 +470,6 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         g.out_scale = out_scale
         g.overflow = overflow.data_ptr()
     g.tri = int(bool(tri))
+    g.b_blocked = int(bool(b_blocked))
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
     return C

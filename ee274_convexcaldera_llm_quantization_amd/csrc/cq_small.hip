@@ -327,6 +327,9 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
 // fp64 for p <= 180, fp32 for p <= 256 (fp32 rotations: near-degenerate Ritz pairs mix at
 // ~eps32*||T||/gap, far below the 1e-4 product tolerance).  The eigenvector
 // rows (Vt) stay in global memory, updated coalesced along rows for active pairs only.
+#ifndef CQ_JAC_ABL
+#define CQ_JAC_ABL 0  // diagnostic builds only (tools/jacobi_ablate.sh): 1 no A update, 2 no V rotation, 4 no seat shift
+#endif
 constexpr int JB = 2;  // pair blocks per thread held in registers per pass (register budget at 1024 threads)
 
 template <typename T>
@@ -539,8 +542,8 @@ static size_t jacobi_lds_bytes(int p, int esize) {
 // end, which removes the per-round O(p^2) global traffic of accumulating V.  fp32 V keeps
 // orthogonality to ~sqrt(rounds)*eps32 (~3e-6); the solver re-orthonormalises its final
 // Ritz block (CholQR), and A stays fp64 so the rotations themselves are fp64-accurate.
-template <int PPT, int RPT>
-__global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double* __restrict__ A_all,
+template <int PPT, int RPT, int JBR, int NTH>
+__global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restrict__ A_all,
                                                                     int p, int max_sweeps, double tol,
                                                                     double* __restrict__ evals,
                                                                     float* __restrict__ V32,
@@ -570,10 +573,10 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
         if (i > j) { const int t = i; i = j; j = t; }
         return i * p - ((i * (i - 1)) >> 1) + (j - i);
     };
-    for (int i = wid; i < p; i += kSmallWaves)
+    for (int i = wid; i < p; i += (NTH / 64))
         for (int c = lane; c < p; c += 64)
             if (c >= i) a[pk(i, c)] = 0.5 * (Ag[i * p + c] + Ag[c * p + i]);
-    for (int s = tid; s < P; s += kSmallThreads) seat[s] = s;
+    for (int s = tid; s < P; s += NTH) seat[s] = s;
     float ev[PPT][RPT], od[PPT][RPT];
 #pragma unroll
     for (int u = 0; u < PPT; ++u)
@@ -587,7 +590,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
-        for (int i = wid; i < p; i += kSmallWaves)
+        for (int i = wid; i < p; i += (NTH / 64))
             for (int c = i + lane; c < p; c += 64) {
                 const double v = a[pk(i, c)];
                 if (c == i) dg += v * v; else off += 2.0 * v * v;
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
         if (stop) break;
         for (int rd = 0; rd < P - 1; ++rd) {
             int act = 0;
-            for (int k = tid; k < H; k += kSmallThreads) {
+            for (int k = tid; k < H; k += NTH) {
                 const int se = seat[2 * k], so = seat[2 * k + 1];
                 const int i = min(se, so), j = max(se, so);
                 double c = 1.0, s = 0.0;
@@ -622,14 +625,54 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
             const bool any = __syncthreads_or(act);
             if (any) {
                 // ---- A <- J^T A J on pair blocks (qa <= qb) in LDS
-                const int nblk = H * (H + 1) / 2;
-                for (int e0 = tid; e0 < nblk; e0 += kSmallThreads * JB) {
-                    int o[JB][4];
-                    double x[JB][4], ca[JB], sa[JB], cb[JB], sb[JB];
-                    bool live[JB], dgn[JB];
+                const int nblk = (CQ_JAC_ABL & 1) ? 0 : H * (H + 1) / 2;
+                if constexpr (JBR == 1) {
+                    // one pair block at a time, few live values (V stays in registers)
+#pragma unroll 1
+                    for (int e = tid; e < nblk; e += NTH) {
+                        int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+                        if (qb * (qb + 1) / 2 > e) --qb;
+                        if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
+                        const int qa = e - qb * (qb + 1) / 2;
+                        const double sa = sn[qa], sb = sn[qb];
+                        if (sa == 0.0 && sb == 0.0) continue;
+                        const double ca = cs[qa], cb = cs[qb];
+                        const int ia = lo[qa], ja = hi[qa], ib = lo[qb], jb = hi[qb];
+                        const bool va = ja < p, vb = jb < p;
+                        if (qa == qb) {
+                            if (!va) continue;
+                            const int o0 = pk(ia, ia), o1 = pk(ia, ja), o3 = pk(ja, ja);
+                            const double x0 = a[o0], x1 = a[o1], x3 = a[o3];
+                            const double y00 = cb * x0 - sb * x1, y01 = sb * x0 + cb * x1;
+                            const double y10 = cb * x1 - sb * x3, y11 = sb * x1 + cb * x3;
+                            a[o0] = ca * y00 - sa * y10;
+                            a[o3] = sa * y01 + ca * y11;
+                            a[o1] = 0.0;
+                        } else {
+                            const int o0 = pk(ia, ib);
+                            const int o1 = vb ? pk(ia, jb) : -1;
+                            const int o2 = va ? pk(ja, ib) : -1;
+                            const int o3 = (va && vb) ? pk(ja, jb) : -1;
+                            const double x0 = a[o0];
+                            const double x1 = o1 >= 0 ? a[o1] : 0.0;
+                            const double x2 = o2 >= 0 ? a[o2] : 0.0;
+                            const double x3 = o3 >= 0 ? a[o3] : 0.0;
+                            const double y00 = cb * x0 - sb * x1, y01 = sb * x0 + cb * x1;
+                            const double y10 = cb * x2 - sb * x3, y11 = sb * x2 + cb * x3;
+                            a[o0] = ca * y00 - sa * y10;
+                            if (o1 >= 0) a[o1] = ca * y01 - sa * y11;
+                            if (o2 >= 0) a[o2] = sa * y00 + ca * y10;
+                            if (o3 >= 0) a[o3] = sa * y01 + ca * y11;
+                        }
+                    }
+                } else
+                for (int e0 = tid; e0 < nblk; e0 += NTH * JBR) {
+                    int o[JBR][4];
+                    double x[JBR][4], ca[JBR], sa[JBR], cb[JBR], sb[JBR];
+                    bool live[JBR], dgn[JBR];
 #pragma unroll
-                    for (int u = 0; u < JB; ++u) {
-                        const int e = e0 + u * kSmallThreads;
+                    for (int u = 0; u < JBR; ++u) {
+                        const int e = e0 + u * NTH;
                         live[u] = false;
                         dgn[u] = false;
                         if (e < nblk) {
@@ -658,7 +701,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
                         }
                     }
 #pragma unroll
-                    for (int u = 0; u < JB; ++u) {
+                    for (int u = 0; u < JBR; ++u) {
                         if (!live[u]) continue;
                         const double y00 = cb[u] * x[u][0] - sb[u] * x[u][1], y01 = sb[u] * x[u][0] + cb[u] * x[u][1];
                         const double y10 = cb[u] * x[u][2] - sb[u] * x[u][3], y11 = sb[u] * x[u][2] + cb[u] * x[u][3];
@@ -676,7 +719,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
                 }
                 // ---- V rotations (registers)
 #pragma unroll
-                for (int u = 0; u < PPT; ++u) {
+                for (int u = 0; u < ((CQ_JAC_ABL & 2) ? 0 : PPT); ++u) {
                     const int k = k0 + u;
                     if (k < H) {
                         const float c = (float)cs[k], s = (float)sn[k];
@@ -694,7 +737,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
             }
             // ---- seat shift of V (every round, rotations or not)
 #pragma unroll
-            for (int r = 0; r < RPT; ++r) {
+            for (int r = 0; r < ((CQ_JAC_ABL & 4) ? 0 : RPT); ++r) {
                 const float from_left = __shfl_up(ev[PPT - 1][r], 1, 32);   // ev of pair k0-1
                 const float from_right = __shfl_down(od[0][r], 1, 32);      // od of pair k0+PPT
                 float ne[PPT], no[PPT];
@@ -714,12 +757,12 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_reg_kernel(const double*
                 for (int u = 0; u < PPT; ++u) { ev[u][r] = ne[u]; od[u][r] = no[u]; }
             }
             __syncthreads();
-            for (int s2 = tid; s2 < P; s2 += kSmallThreads) seat[s2] = seat2[s2];
+            for (int s2 = tid; s2 < P; s2 += NTH) seat[s2] = seat2[s2];
             __syncthreads();
         }
     }
     if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
-    for (int i = tid; i < p; i += kSmallThreads) {
+    for (int i = tid; i < p; i += NTH) {
         const double di = a[pk(i, i)];
         int rank = 0;
         for (int j = 0; j < p; ++j) {
@@ -964,11 +1007,11 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     if (p <= 192 && lreg <= 160 * 1024) {
         // fp64 A in LDS, V in registers (no per-round memory traffic for V)
         if (p <= 64)
-            jacobi_reg_kernel<1, 2><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+            jacobi_reg_kernel<1, 2, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
         else if (p <= 128)
-            jacobi_reg_kernel<2, 4><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+            jacobi_reg_kernel<2, 4, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
         else
-            jacobi_reg_kernel<3, 6><<<(unsigned)batch, kSmallThreads, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+            jacobi_reg_kernel<3, 6, 1, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
     } else if (l32 <= 160 * 1024) {
         jacobi_lds_kernel<float><<<(unsigned)batch, kSmallThreads, l32, s>>>(
             A, (int)p, max_sweeps, std::max(tol, 1e-7), Vt, evals, V32, V64, sweeps_out);

@@ -44,6 +44,7 @@ struct X3K {
     float out_scale;
     int* overflow;
     int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
+    int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
     int64_t tiles_n, tiles_m;
 };
 
@@ -226,6 +227,148 @@ __global__ __launch_bounds__(X3_THREADS, 1) void gemm_x3_kernel(X3K a) {
     if (ovf) atomicOr(a.overflow + b, 1);
 }
 
+
+// ------------------------------------------------------------------ LDS-DMA pipelined variant
+// Tile 192 x 192 x 32, 512 threads = 8 waves of 96 x 48 (6 x 3 blocks of
+// v_mfma_f32_16x16x32_f16).  Operands go global -> LDS by global_load_lds_dwordx4 (no
+// register staging) into a 3-stage ring (48 KB per stage: hi/lo of 192 A rows and 192 B
+// rows, 64 B each); the loads of stage t+2 are issued right after the barrier of step t
+// and stay in flight across it (counted vmcnt, raw s_barrier: a __syncthreads() would
+// drain them).  LDS images are linear per wave-instruction (16 rows x 64 B) with the 16-B
+// chunk index XOR-swizzled by (row >> 2) & 3 on the global source address, so the
+// fragment reads (16 rows x one chunk per 16 lanes) are conflict-free.
+constexpr int XG_BM = 192, XG_BN = 192, XG_BK = 32;
+constexpr int XG_THREADS = 512;
+constexpr int XG_PART = XG_BM * XG_BK;              // halves per part image (A and B alike)
+constexpr int XG_STAGE = 4 * XG_PART;                // Ah, Al, Bh, Bl
+constexpr int XG_NSTAGE = 3;
+constexpr size_t XG_LDS_BYTES = (size_t)XG_NSTAGE * XG_STAGE * sizeof(_Float16);  // 144 KB
+constexpr int XG_INSTR = 4 * XG_BM / 16;             // wave-instructions per stage (48)
+constexpr int XG_PER_WAVE = XG_INSTR / (XG_THREADS / 64);  // 6
+static_assert(XG_BM == XG_BN, "parts share one geometry");
+static_assert(XG_PER_WAVE == 6, "vmcnt counts below assume 6 loads per wave per stage");
+
+using f16x8g = __attribute__((ext_vector_type(8))) _Float16;
+using f32x4v = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ void xg_issue(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
+                                         _Float16* stage, int wid, int lane) {
+#pragma unroll
+    for (int u = 0; u < XG_PER_WAVE; ++u) {
+        const int I = wid * XG_PER_WAVE + u;
+        const int part = I / 12, sub = I % 12;       // part: 0 Ah, 1 Al, 2 Bh, 3 Bl
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);  // logical chunk stored at this lane's slot
+        const bool isA = part < 2;
+        const int64_t base = isA ? m0 : n0;
+        const int64_t lim = isA ? a.M : a.N;
+        int64_t gr = base + row;
+        gr = gr < lim ? gr : lim - 1;                 // clamp: rows past the edge feed only unstored outputs
+        const _Float16* src;
+        if (isA) src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + c * 8;
+        else if (a.b_blocked) src = (part == 3 ? a.Bl : a.Bh) + b * a.sb + (k0 >> 5) * (a.ldb * 32) + gr * 32 + c * 8;
+        else src = (part == 3 ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + c * 8;
+        _Float16* dst = stage + part * XG_PART + (16 * sub) * XG_BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ f16x8g xg_frag(const _Float16* img, int row, int chunk) {
+    const int pc = chunk ^ ((row >> 2) & 3);
+    return *reinterpret_cast<const f16x8g*>(img + row * XG_BK + pc * 8);
+}
+
+__global__ __launch_bounds__(XG_THREADS, 1) void gemm_x3g_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char xg_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(xg_smem_raw);
+
+    // bijective XCD remap: the tiles of one matrix run on one XCD (shared X^T slices in L2)
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+    const int64_t tn = lin % a.tiles_n;
+    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
+    const int64_t b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * XG_BM, n0 = tn * XG_BN;
+    if (a.tri && n0 + XG_BN <= m0) return;
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 48 wn .. +48
+    const int l16 = lane & 15, lq = lane >> 4;
+
+    f32x4v acc[6][3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nt = a.K / XG_BK;
+    xg_issue(a, b, m0, n0, 0, smem, wid, lane);
+    if (nt > 1) xg_issue(a, b, m0, n0, XG_BK, smem + XG_STAGE, wid, lane);
+    for (int64_t t = 0; t < nt; ++t) {
+        // stage t landed (this wave's part): leave stage t+1's 6 loads in flight
+        if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's part of stage t landed; stage t-1 fully read
+        if (t + 2 < nt) xg_issue(a, b, m0, n0, (t + 2) * XG_BK, smem + ((t + 2) % XG_NSTAGE) * XG_STAGE, wid, lane);
+        const _Float16* st = smem + (t % XG_NSTAGE) * XG_STAGE;
+        f16x8g ah[6], al[6], bh[3], bl[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int row = 48 * wn + 16 * j + l16;
+            bh[j] = xg_frag(st + 2 * XG_PART, row, lq);
+            bl[j] = xg_frag(st + 3 * XG_PART, row, lq);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int row = 96 * wm + 16 * i + l16;
+            ah[i] = xg_frag(st, row, lq);
+            al[i] = xg_frag(st + XG_PART, row, lq);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+    }
+
+    const float sc = a.inv_scale[b];
+    const float al_ = a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = a.gamma_v ? a.gamma_v[b] : 0.f;
+    bool ovf = false;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int64_t col = n0 + 48 * wn + 16 * j + l16;
+            if (col >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + 96 * wm + 16 * i + 4 * lq + r;
+                if (row >= a.M) continue;
+                float v = al_ * (acc[i][j][r] * sc);
+                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
+                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
+                a.C[b * a.sc + row * a.ldc + col] = v;
+                if (a.Oh) {
+                    const float hs = v * a.out_scale;
+                    const _Float16 h = (_Float16)hs;
+                    const _Float16 l = (_Float16)(hs - (float)h);
+                    a.Oh[b * a.so + row * a.ldo + col] = h;
+                    a.Ol[b * a.so + row * a.ldo + col] = l;
+                    ovf |= !(fabsf(hs) < 65504.f);
+                }
+            }
+        }
+    if (ovf) atomicOr(a.overflow + b, 1);
+}
+
 // ------------------------------------------------------------------ split / transpose helpers
 
 // Per-batch power-of-two scale s = 2^(14 - ceil(log2 max_i G_ii)) for a PSD G (|G_ij| <=
@@ -275,9 +418,14 @@ __global__ void split_kernel(const float* __restrict__ X, int64_t n_per, const f
 
 // Split of a symmetric matrix of which only the upper triangle (j >= i) is valid: 64 x 64
 // tiles, lower tiles read from the transposed upper tile through LDS.
+__device__ __forceinline__ int64_t blk_off(int64_t i, int64_t j, int64_t n, int blocked) {
+    return blocked ? ((j >> 5) * n * 32 + i * 32 + (j & 31)) : (i * n + j);
+}
+
 __global__ __launch_bounds__(256) void sym_split_upper_kernel(const float* __restrict__ G, int64_t n,
                                                               const float* __restrict__ s_v,
-                                                              _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+                                                              _Float16* __restrict__ hi, _Float16* __restrict__ lo,
+                                                              int blocked) {
     __shared__ float tile[64][65];
     const int64_t b = blockIdx.z;
     const int64_t ti = blockIdx.y, tj = blockIdx.x;
@@ -299,8 +447,9 @@ __global__ __launch_bounds__(256) void sym_split_upper_kernel(const float* __res
         if (i < n && j < n) {
             const float v = (lower ? tile[tx][r] : tile[r][tx]) * s;
             const _Float16 h = (_Float16)v;
-            hi[b * n * n + i * n + j] = h;
-            lo[b * n * n + i * n + j] = (_Float16)(v - (float)h);
+            const int64_t o = b * n * n + blk_off(i, j, n, blocked);
+            hi[o] = h;
+            lo[o] = (_Float16)(v - (float)h);
         }
     }
 }
@@ -371,18 +520,19 @@ using namespace cq;
 
 extern "C" {
 
-int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, float x_scale, uint16_t* Gh,
-                     uint16_t* Gl, float* scale_out, float* inv_scale_out, void* stream) {
+int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, int blocked, float x_scale,
+                     uint16_t* Gh, uint16_t* Gl, float* scale_out, float* inv_scale_out, void* stream) {
     CQ_REQUIRE(G && Gh && Gl && scale_out && inv_scale_out, "cq_sym_split_f16: null pointer");
     CQ_REQUIRE(n > 0 && batch > 0 && (n * n) % 4 == 0, "cq_sym_split_f16: bad shape");
     CQ_REQUIRE(x_scale > 0.f, "cq_sym_split_f16: x_scale must be > 0");
     hipStream_t s = as_stream(stream);
     sym_scale_kernel<<<(unsigned)batch, 256, 0, s>>>(G, n, n, n * n, x_scale, scale_out, inv_scale_out);
-    if (upper_only) {
+    CQ_REQUIRE(!blocked || n % 32 == 0, "cq_sym_split_f16: blocked layout needs n % 32 == 0");
+    if (upper_only || blocked) {
         CQ_REQUIRE(batch < 65536, "cq_sym_split_f16: batch too large");
         const unsigned t64 = (unsigned)ceil_div(n, 64);
         sym_split_upper_kernel<<<dim3(t64, t64, (unsigned)batch), 256, 0, s>>>(
-            G, n, scale_out, reinterpret_cast<_Float16*>(Gh), reinterpret_cast<_Float16*>(Gl));
+            G, n, scale_out, reinterpret_cast<_Float16*>(Gh), reinterpret_cast<_Float16*>(Gl), blocked);
         return check_launch("cq_sym_split_f16");
     }
     const int64_t tot4 = batch * n * n / 4;
@@ -456,16 +606,25 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && !g->out_h),
                "cq_gemm_x3: tri needs a square plain product");
     a.tri = g->tri;
-    a.tiles_n = ceil_div(g->N, X3_BN);
-    a.tiles_m = ceil_div(g->M, X3_BM);
-    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-    CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-    static const int pf = [] {
-        const char* e = getenv("CQ_X3_PREFETCH");
-        return (e && e[0] == '1') ? 1 : 2;
+    a.b_blocked = g->b_blocked;
+    CQ_REQUIRE(!g->b_blocked || g->ldb >= g->N, "cq_gemm_x3: blocked B needs ldb = rows >= N");
+    static const int variant = [] {
+        const char* e = getenv("CQ_X3_KERNEL");  // A/B switch for benchmarking: "reg" = register-staged
+        return (e && e[0] == 'r') ? 1 : 0;
     }();
-    if (pf == 1) gemm_x3_kernel<1><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
-    else gemm_x3_kernel<2><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
+    if (variant == 0 || g->b_blocked) {
+        a.tiles_n = ceil_div(g->N, XG_BN);
+        a.tiles_m = ceil_div(g->M, XG_BM);
+        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+        gemm_x3g_kernel<<<(unsigned)total, XG_THREADS, XG_LDS_BYTES, as_stream(stream)>>>(a);
+    } else {
+        a.tiles_n = ceil_div(g->N, X3_BN);
+        a.tiles_m = ceil_div(g->M, X3_BM);
+        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+        gemm_x3_kernel<1><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
+    }
     return check_launch("cq_gemm_x3");
 }
 

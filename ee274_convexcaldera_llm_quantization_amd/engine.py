@@ -149,8 +149,9 @@ class CalderaEngine:
     """Decomposes a batch of B weight matrices (B, m, n) with shared params and H."""
 
     def __init__(self, params: EngineParams, *, solver_tol: float = 5e-6, solver_p: int | None = None,
-                 filter_precision: str = "f16x3", profile: bool = False):
+                 filter_precision: str = "f16x3", profile: bool = False, solver_kwargs: dict | None = None):
         self.p = params
+        self.solver_kwargs = dict(solver_kwargs or {})
         self.solver_tol = solver_tol
         self.solver_p = solver_p
         self.filter_precision = filter_precision
@@ -198,7 +199,7 @@ class CalderaEngine:
         Y = Ysrc
         if self.solver is None:
             self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
-                                      filter_precision=self.filter_precision)
+                                      filter_precision=self.filter_precision, **self.solver_kwargs)
         sv = self.solver
         vecs, theta = yield from sv.solve_iter(Ysrc)
         r = sv.r

@@ -89,6 +89,7 @@ class SolverStats:
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
+        self.history = []  # per solve call: (cold, degrees used, residual after each)
 
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
@@ -99,8 +100,8 @@ class RankRSolver:
     """Top-r eigenpairs of the Gram of a batch of matrices, warm-started across calls."""
 
     def __init__(self, B: int, m: int, n: int, r: int, device, *, p: int | None = None,
-                 tol: float = 5e-6, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 10, 10, 10, 10, 10),
-                 seed: int = 0x5EED, jacobi_tol: float = 1e-13, filter_precision: str = "f16x3"):
+                 tol: float = 5e-6, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 6, 6, 6, 6, 6),
+                 seed: int = 0x5EED, jacobi_tol: float = 1e-10, filter_precision: str = "f16x3"):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -130,6 +131,7 @@ class RankRSolver:
             raise ValueError(f"filter_precision must be 'f16x3' or 'f32', got {filter_precision!r}")
         # split-fp16 filter needs K (= k) a multiple of 32 and 16-byte aligned rows
         self.x3 = filter_precision == "f16x3" and not self.direct and self.k % 32 == 0
+        self._g_blocked = True  # K-blocked G halves: each K step of a tile is one contiguous run
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
@@ -168,7 +170,7 @@ class RankRSolver:
         Z = self._free(X, *keep)
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
             K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE)
-            K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0])
+            K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked)
             K.transpose_split(self._xt[0], out=Z)
         else:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
@@ -243,7 +245,7 @@ class RankRSolver:
         ev = EVENT_PROBE.start(fl, nb, kn)
         K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
                   gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
-                  out_scale=X3_SCALE, overflow=self._ovf)
+                  out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked)
         EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = 0, 1
@@ -253,7 +255,7 @@ class RankRSolver:
             K.gemm_x3(xh[cur], xl[cur], self._Gh, self._Gl, self._ginv, xt[prev], P=xt[prev], D=xt[cur],
                       alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
                       out_h=None if last else xh[prev], out_l=None if last else xl[prev],
-                      out_scale=X3_SCALE, overflow=self._ovf)
+                      out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked)
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur = cur, prev
@@ -297,7 +299,7 @@ class RankRSolver:
             K.gemm(Y, Y, ta=True, C=self._G, syrk=True)  # Y^T Y
         if self.x3:
             K.sym_split_f16(self._G, X3_SCALE, hi=self._Gh, lo=self._Gl, scale=self._gscale,
-                            inv_scale=self._ginv, upper_only=self._g_upper_only)
+                            inv_scale=self._ginv, upper_only=self._g_upper_only, blocked=self._g_blocked)
             self._ovf.zero_()
         cold = not (warm and self.X is not None)
         if cold:
@@ -323,6 +325,7 @@ class RankRSolver:
             ends = self._ends
             degs = self.deg_warm
         self.stats.resid_hist = []
+        used = []
         for d in degs:
             self.stats.outer += 1
             while True:
@@ -350,8 +353,10 @@ class RankRSolver:
             mr = float(chk[0])
             self.stats.max_resid = mr
             self.stats.resid_hist.append(mr)
+            used.append(d)
             if mr <= self.tol:
                 break
+        self.stats.history.append((cold, used, list(self.stats.resid_hist)))
         # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
         # one CholQR pass restores orthonormality without moving the converged subspace
         X, _ = self._cholqr(X)

@@ -182,10 +182,12 @@ int cq_ritz_residual(const float* X, const float* Z, const double* theta, int64_
  */
 /* Gh/Gl[b] = split of G[b] (n x n PSD, row-major) scaled by scale_out[b] = 2^(14 -
  * ceil(log2 max_i G_ii)); inv_scale_out[b] = 1 / (scale_out[b] * x_scale).  upper_only:
- * only G's upper triangle (j >= i) is read and mirrored into the full split. */
-int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, float x_scale,
-                     uint16_t* Gh, uint16_t* Gl, float* scale_out, float* inv_scale_out,
-                     void* stream);
+ * only G's upper triangle (j >= i) is read and mirrored into the full split.  blocked:
+ * halves written K-blocked, element (i, j) at (j / 32) * n * 32 + i * 32 + j % 32, so a
+ * 32-deep K step of any row range is one contiguous run (cq_x3_args.b_blocked). */
+int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, int blocked,
+                     float x_scale, uint16_t* Gh, uint16_t* Gl, float* scale_out,
+                     float* inv_scale_out, void* stream);
 /* scale_out[b] = 2^(log2_target - e) with max|X[b]| in [2^(e-1), 2^e) (1 for all-zero X[b]). */
 int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target, float* scale_out,
                   void* stream);
@@ -217,6 +219,7 @@ typedef struct cq_x3_args {
     int* overflow;                 /* [batch]: set to 1 when |C * out_scale| >= 65504 */
     int tri;                       /* C symmetric (M == N, plain product): tiles entirely below
                                       the diagonal are skipped; the upper triangle is exact */
+    int b_blocked;                 /* B halves K-blocked (see cq_sym_split_f16); ldb = rows */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

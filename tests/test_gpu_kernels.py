@@ -330,6 +330,26 @@ def test_sym_split_scale_and_halves(K):
     Gu = torch.triu(G) + torch.tril(torch.full_like(G, 7.0), -1)
     hu, lu, su, _ = K.sym_split_f16(Gu, 64.0, upper_only=True)
     assert torch.equal(hu, hi) and torch.equal(lu, lo) and torch.equal(su, s)
+    # K-blocked layout: (i, j) at (j // 32) * n * 32 + i * 32 + j % 32
+    hb, lb, _, _ = K.sym_split_f16(G, 64.0, blocked=True)
+    n = G.shape[1]
+    ref_b = hi.view(2, n, n // 32, 32).permute(0, 2, 1, 3).reshape(2, n, n)
+    assert torch.equal(hb, ref_b)
+
+
+def test_gemm_x3_blocked_b_matches_rowmajor(K):
+    g = torch.Generator(device=DEV).manual_seed(8)
+    Y = torch.randn(2, 320, 96, device=DEV, generator=g)
+    G = torch.matmul(Y, Y.transpose(1, 2)).contiguous()
+    gh, gl, gs, ginv = K.sym_split_f16(G, 64.0)
+    bh, bl, _, _ = K.sym_split_f16(G, 64.0, blocked=True)
+    X = torch.randn(2, 200, 320, device=DEV, generator=g)
+    xh, xl = _x3_split_ref(X, 64.0)
+    C1 = torch.empty(2, 200, 320, device=DEV)
+    C2 = torch.empty_like(C1)
+    K.gemm_x3(xh, xl, gh, gl, ginv, C1)
+    K.gemm_x3(xh, xl, bh, bl, ginv, C2, b_blocked=True)
+    assert torch.equal(C1, C2)
 
 
 @pytest.mark.parametrize("M,N,Kd", [(192, 256, 512), (96, 320, 256), (200, 520, 1024)])

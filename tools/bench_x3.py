@@ -28,7 +28,7 @@ G = torch.empty(B, k, k, device=dev)
 K.gemm(Y, Y, tb=True, C=G, syrk=True)
 del Y
 xs = 2.0 ** 6
-Gh, Gl, gs, inv = K.sym_split_f16(G, xs)
+Gh, Gl, gs, inv = K.sym_split_f16(G, xs, blocked=True)
 for p in (192, 256, 384):
     X = torch.linalg.qr(torch.randn(B, k, p, device=dev))[0].contiguous()
     Xt = torch.empty(B, p, k, device=dev)
@@ -39,16 +39,16 @@ for p in (192, 256, 384):
     ovf = torch.zeros(B, dtype=torch.int32, device=dev)
     a = torch.full((B,), 0.5, device=dev); b = torch.full((B,), -0.25, device=dev); c = torch.full((B,), 0.1, device=dev)
     fl = 2 * k * k * p * B
-    bench(f"x3  C^T = X^T G  p={p}", lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct), fl)
+    bench(f"x3  C^T = X^T G  p={p}", lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, b_blocked=True), fl)
     bench(f"x3  + cheb epilogue + split p={p}", lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, P=Ct, D=Xt, alpha_v=a,
                                                                beta_v=b, gamma_v=c, out_h=Oh, out_l=Ol,
-                                                               out_scale=xs, overflow=ovf), fl)
+                                                               out_scale=xs, overflow=ovf, b_blocked=True), fl)
     C = torch.empty(B, k, p, device=dev)
     bench(f"f32 G X ta  p={p}", lambda: K.gemm(G, X, ta=True, C=C), fl)
-    K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct)
+    K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, b_blocked=True)
     K.gemm(G, X, ta=True, C=C)
     ref = torch.matmul(G.double(), X.double())
     e3 = ((Ct.transpose(1, 2).double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     e32 = ((C.double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     print(f"   max column rel err: x3 {e3:.3e}   fp32 {e32:.3e}", flush=True)
-bench("sym_split_f16", lambda: K.sym_split_f16(G, xs, hi=Gh, lo=Gl, scale=gs, inv_scale=inv), 0.0 + 1)
+bench("sym_split_f16 blocked", lambda: K.sym_split_f16(G, xs, hi=Gh, lo=Gl, scale=gs, inv_scale=inv, blocked=True), 0.0 + 1)
