@@ -56,6 +56,7 @@ class X3Args(ctypes.Structure):
         ("overflow", c_vp),
         ("tri", c_int),
         ("b_blocked", c_int),
+        ("active", c_vp),
     ]
 
 
@@ -442,7 +443,7 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None):
 
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
-            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False):
+            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l."""
@@ -471,5 +472,6 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         g.overflow = overflow.data_ptr()
     g.tri = int(bool(tri))
     g.b_blocked = int(bool(b_blocked))
+    g.active = active.data_ptr() if active is not None else None
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
     return C

@@ -45,6 +45,7 @@ struct X3K {
     int* overflow;
     int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
     int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
+    const int* active;  // per batch (NULL = all): inactive entries skip the product, C = D
     int64_t tiles_n, tiles_m;
 };
 
@@ -156,7 +157,8 @@ __global__ __launch_bounds__(X3_THREADS, 1) void gemm_x3_kernel(X3K a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int64_t nt = a.K / X3_BK;
+    const bool live = !a.active || a.active[b];
+    const int64_t nt = live ? a.K / X3_BK : 0;
     if (PF == 1) {
         uint4 ra[X3_NA], rb[X3_NB];
         if (nt > 0) {
@@ -196,9 +198,10 @@ __global__ __launch_bounds__(X3_THREADS, 1) void gemm_x3_kernel(X3K a) {
 
     // epilogue: C = alpha * acc * inv_scale + beta * P + gamma * D; optional fp16 split of C
     const float sc = a.inv_scale[b];
-    const float al_ = a.alpha_v ? a.alpha_v[b] : 1.f;
-    const float be_ = a.beta_v ? a.beta_v[b] : 0.f;
-    const float ga_ = a.gamma_v ? a.gamma_v[b] : 0.f;
+    // inactive entries (converged matrices) pass D through unchanged
+    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
     bool ovf = false;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -303,8 +306,9 @@ __global__ __launch_bounds__(XG_THREADS, 1) void gemm_x3g_kernel(X3K a) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-    const int64_t nt = a.K / XG_BK;
-    xg_issue(a, b, m0, n0, 0, smem, wid, lane);
+    const bool live = !a.active || a.active[b];
+    const int64_t nt = live ? a.K / XG_BK : 0;
+    if (nt > 0) xg_issue(a, b, m0, n0, 0, smem, wid, lane);
     if (nt > 1) xg_issue(a, b, m0, n0, XG_BK, smem + XG_STAGE, wid, lane);
     for (int64_t t = 0; t < nt; ++t) {
         // stage t landed (this wave's part): leave stage t+1's 6 loads in flight
@@ -338,9 +342,10 @@ __global__ __launch_bounds__(XG_THREADS, 1) void gemm_x3g_kernel(X3K a) {
     }
 
     const float sc = a.inv_scale[b];
-    const float al_ = a.alpha_v ? a.alpha_v[b] : 1.f;
-    const float be_ = a.beta_v ? a.beta_v[b] : 0.f;
-    const float ga_ = a.gamma_v ? a.gamma_v[b] : 0.f;
+    // inactive entries (converged matrices) pass D through unchanged
+    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
     bool ovf = false;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -351,6 +356,137 @@ __global__ __launch_bounds__(XG_THREADS, 1) void gemm_x3g_kernel(X3K a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t row = m0 + 96 * wm + 16 * i + 4 * lq + r;
+                if (row >= a.M) continue;
+                float v = al_ * (acc[i][j][r] * sc);
+                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
+                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
+                a.C[b * a.sc + row * a.ldc + col] = v;
+                if (a.Oh) {
+                    const float hs = v * a.out_scale;
+                    const _Float16 h = (_Float16)hs;
+                    const _Float16 l = (_Float16)(hs - (float)h);
+                    a.Oh[b * a.so + row * a.ldo + col] = h;
+                    a.Ol[b * a.so + row * a.ldo + col] = l;
+                    ovf |= !(fabsf(hs) < 65504.f);
+                }
+            }
+        }
+    if (ovf) atomicOr(a.overflow + b, 1);
+}
+
+
+// ------------------------------------------------------------------ wide-tile LDS-DMA variant
+// Tile 192 x 384 x 32 (12 waves of 96 x 64, 3 x 2 blocks of v_mfma_f32_32x32x16_f16), two
+// 72 KB stages.  Per K step the CU loads 72 KB for 2x the MFMA work of the 192 x 192 tile
+// (48 KB): the X^T slice is re-read by half as many tiles, which is what bounds the filter
+// product (per-CU load path, ~10 B/clk/CU).
+constexpr int XW_BM = 192, XW_BN = 384, XW_BK = 32;
+constexpr int XW_THREADS = 768;
+constexpr int XW_APART = XW_BM * XW_BK, XW_BPART = XW_BN * XW_BK;   // halves
+constexpr int XW_STAGE = 2 * XW_APART + 2 * XW_BPART;
+constexpr size_t XW_LDS_BYTES = (size_t)2 * XW_STAGE * sizeof(_Float16);  // 144 KB
+constexpr int XW_PER_WAVE = (2 * XW_BM / 16 + 2 * XW_BN / 16) / (XW_THREADS / 64);  // 6
+static_assert(XW_PER_WAVE == 6, "load split");
+
+__device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
+                                         _Float16* stage, int wid, int lane) {
+#pragma unroll
+    for (int u = 0; u < XW_PER_WAVE; ++u) {
+        const int I = wid * XW_PER_WAVE + u;  // 0..71: Ah 0-11, Al 12-23, Bh 24-47, Bl 48-71
+        const bool isA = I < 24;
+        const int part = isA ? (I >= 12) : (I >= 48);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        const int64_t lim = isA ? a.M : a.N;
+        int64_t gr = (isA ? m0 : n0) + row;
+        gr = gr < lim ? gr : lim - 1;
+        const _Float16* src;
+        if (isA) src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + c * 8;
+        else if (a.b_blocked) src = (part ? a.Bl : a.Bh) + b * a.sb + (k0 >> 5) * (a.ldb * 32) + gr * 32 + c * 8;
+        else src = (part ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + c * 8;
+        _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char xw_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(xw_smem_raw);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+    const int64_t tn = lin % a.tiles_n;
+    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
+    const int64_t b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
+    if (a.tri && n0 + XW_BN <= m0) return;
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
+    const int lr = lane & 31, lh = lane >> 5;
+
+    f32x16v acc[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const bool live = !a.active || a.active[b];
+    const int64_t nt = live ? a.K / XW_BK : 0;
+    if (nt > 0) xw_issue(a, b, m0, n0, 0, smem, wid, lane);
+    for (int64_t t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
+        if (t + 1 < nt) xw_issue(a, b, m0, n0, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, lane);
+        const _Float16* sA = smem + (t & 1) * XW_STAGE;
+        const _Float16* sB = sA + 2 * XW_APART;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int ch = 2 * s2 + lh;
+            f16x8 ah[3], al[3], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int row = 96 * wm + 32 * i + lr;
+                ah[i] = xg_frag(sA, row, ch);
+                al[i] = xg_frag(sA + XW_APART, row, ch);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 64 * wn + 32 * j + lr;
+                bh[j] = xg_frag(sB, row, ch);
+                bl[j] = xg_frag(sB + XW_BPART, row, ch);
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+    }
+
+    const float sc = a.inv_scale[b];
+    // inactive entries (converged matrices) pass D through unchanged
+    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
+    bool ovf = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t col = n0 + 64 * wn + 32 * j + lr;
+            if (col >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + 96 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
                 if (row >= a.M) continue;
                 float v = al_ * (acc[i][j][r] * sc);
                 if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
@@ -607,12 +743,23 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
                "cq_gemm_x3: tri needs a square plain product");
     a.tri = g->tri;
     a.b_blocked = g->b_blocked;
+    a.active = g->active;
+    CQ_REQUIRE(!g->active || g->D, "cq_gemm_x3: active needs D (the pass-through value)");
     CQ_REQUIRE(!g->b_blocked || g->ldb >= g->N, "cq_gemm_x3: blocked B needs ldb = rows >= N");
     static const int variant = [] {
-        const char* e = getenv("CQ_X3_KERNEL");  // A/B switch for benchmarking: "reg" = register-staged
-        return (e && e[0] == 'r') ? 1 : 0;
+        // A/B switch for benchmarking: "reg" register-staged 192x256, "g" LDS-DMA 192x192,
+        // default LDS-DMA 192x384
+        const char* e = getenv("CQ_X3_KERNEL");
+        if (!e) return 2;
+        return e[0] == 'r' ? 1 : e[0] == 'g' ? 0 : 2;
     }();
-    if (variant == 0 || g->b_blocked) {
+    if (variant == 2) {
+        a.tiles_n = ceil_div(g->N, XW_BN);
+        a.tiles_m = ceil_div(g->M, XW_BM);
+        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+        gemm_x3w_kernel<<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    } else if (variant == 0 || g->b_blocked) {
         a.tiles_n = ceil_div(g->N, XG_BN);
         a.tiles_m = ceil_div(g->M, XG_BM);
         const int64_t total = a.tiles_n * a.tiles_m * a.batch;

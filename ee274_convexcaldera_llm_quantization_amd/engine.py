@@ -239,6 +239,13 @@ class CalderaEngine:
         st.L, st.R = L, R
         st.has_LR = True
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
+        if sv.left and p.activation_aware_LR and not quantized:
+            # L = U (orthonormal columns), L R = U U^T Y diag(1/sqrt(h)) with h the error
+            # weights, so the weighted residual is (I - U U^T) Y and, by Pythagoras,
+            # sum_j h_j (res - L R)_ij^2 = ||Y||^2 - ||U^T Y||^2 = ||Y||^2 - sum_j h_j R_ij^2
+            # (two fp64 reductions instead of an m x n x r product; U orthonormal to ~1e-7)
+            return (K.weighted_sqsum(Ysrc, None, n) -
+                    K.weighted_sqsum(R, wts.err if wts.ycol is not None else None, n))
         err = torch.empty(B, dtype=torch.float64, device=dev)
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err

@@ -150,6 +150,7 @@ class RankRSolver:
                 self._xh = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
                 self._xl = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
                 self._ovf = torch.zeros(B, dtype=torch.int32, device=dev)
+            self._active = torch.ones(B, dtype=torch.int32, device=dev)
 
     def _free(self, *used):
         for b in self._bufs:
@@ -245,7 +246,7 @@ class RankRSolver:
         ev = EVENT_PROBE.start(fl, nb, kn)
         K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
                   gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
-                  out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked)
+                  out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked, active=self._active)
         EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = 0, 1
@@ -255,7 +256,8 @@ class RankRSolver:
             K.gemm_x3(xh[cur], xl[cur], self._Gh, self._Gl, self._ginv, xt[prev], P=xt[prev], D=xt[cur],
                       alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
                       out_h=None if last else xh[prev], out_l=None if last else xl[prev],
-                      out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked)
+                      out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked,
+                      active=self._active)
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur = cur, prev
@@ -297,6 +299,7 @@ class RankRSolver:
             K.gemm(Y, Y, tb=True, C=self._G, syrk=True)  # Y Y^T (upper tiles + mirror)
         else:
             K.gemm(Y, Y, ta=True, C=self._G, syrk=True)  # Y^T Y
+        self._active.fill_(1)
         if self.x3:
             K.sym_split_f16(self._G, X3_SCALE, hi=self._Gh, lo=self._Gl, scale=self._gscale,
                             inv_scale=self._ginv, upper_only=self._g_upper_only, blocked=self._g_blocked)
@@ -334,12 +337,12 @@ class RankRSolver:
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._cholqr(Xa, X)
                 theta_n, Xn, Zn = self._rr(Xb, X)
-                res = K.ritz_residual(Xn, Zn, theta_n, self.r).max()
+                res = K.ritz_residual(Xn, Zn, theta_n, self.r)  # (B,) per-matrix max residual
                 ovf = self._ovf.max().double() if self.x3 else torch.zeros((), dtype=torch.float64, device=dev)
-                chk = torch.cat([res.double().view(1), ovf.view(1), theta_n[:, 0], theta_n[:, p - 1]])
+                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res.double()])
                 yield
                 chk = chk.cpu().numpy()
-                if self.x3 and chk[1] != 0:
+                if self.x3 and chk[0] != 0:
                     # an fp16 half overflowed: redo this outer iteration with the fp32 filter
                     self.x3 = False
                     self.stats.x3_fallbacks += 1
@@ -349,8 +352,11 @@ class RankRSolver:
                     continue
                 break
             theta, X, Z = theta_n, Xn, Zn
-            ends = np.stack([chk[2:2 + B], chk[2 + B:2 + 2 * B]], 1)
-            mr = float(chk[0])
+            ends = np.stack([chk[1:1 + B], chk[1 + B:1 + 2 * B]], 1)
+            resid = chk[1 + 2 * B:]
+            mr = float(resid.max())
+            # converged matrices sit out the remaining filter products (their X passes through)
+            self._active.copy_(torch.from_numpy((resid > self.tol).astype(np.int32)))
             self.stats.max_resid = mr
             self.stats.resid_hist.append(mr)
             used.append(d)

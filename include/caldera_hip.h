@@ -220,6 +220,8 @@ typedef struct cq_x3_args {
     int tri;                       /* C symmetric (M == N, plain product): tiles entirely below
                                       the diagonal are skipped; the upper triangle is exact */
     int b_blocked;                 /* B halves K-blocked (see cq_sym_split_f16); ldb = rows */
+    const int* active;             /* [batch] or NULL: entries with active[b] == 0 skip the
+                                      product and write C = D (and its split) unchanged */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
