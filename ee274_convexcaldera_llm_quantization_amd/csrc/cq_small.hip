@@ -92,6 +92,113 @@ __global__ void gram_reduce_kernel(const double* __restrict__ part, int64_t MN, 
     }
 }
 
+
+// fp64-MFMA variant for the non-transposed case (C = A^T B, A: K x M, B: K x N, row-major):
+// v_mfma_f64_16x16x4_f64 on fp32 operands converted exactly to fp64 (products exact, fp64
+// accumulation: the same arithmetic contract as gram_f64_kernel).  64 x 64 tile per
+// workgroup, 4 waves of 32 x 32 (2 x 2 blocks), GK-deep LDS slices filled by float4 loads
+// with a one-slice register prefetch.  sym (A == B): tiles below the block diagonal are
+// skipped and mirrored by the reduction.
+using f64x4v = __attribute__((ext_vector_type(4))) double;
+
+__global__ __launch_bounds__(kGramThreads) void gram_f64_mfma_kernel(
+    int64_t M, int64_t N, int64_t K, int64_t kchunk, int splits, const float* __restrict__ A,
+    int64_t lda, int64_t sa, const float* __restrict__ B, int64_t ldb, int64_t sb, int sym,
+    double* __restrict__ part) {
+    __shared__ float As[2][GK][GT + 4];
+    __shared__ float Bs[2][GK][GT + 4];
+    const int64_t b = blockIdx.z / splits;
+    const int split = blockIdx.z % splits;
+    if (sym && blockIdx.x < blockIdx.y) return;
+    const int64_t i0 = (int64_t)blockIdx.y * GT, j0 = (int64_t)blockIdx.x * GT;
+    const float* Ab = A + b * sa;
+    const float* Bb = B + b * sb;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int wi = wid >> 1, wj = wid & 1;  // wave block: rows 32 wi, cols 32 wj
+    // slice loader: GK rows x 64 columns of A and of B, 2 float4 per thread each
+    const int lr = t >> 4, lc = (t & 15) * 4;  // rows lr and lr + 16, columns lc .. lc+3
+    const int64_t kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+    auto ld4 = [&](const float* base, int64_t ld, int64_t lim, int64_t k, int64_t c0) -> float4 {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k < kend) {
+            const float* src = base + k * ld + c0;
+            if (c0 + 3 < lim) v = *reinterpret_cast<const float4*>(src);
+            else {
+                if (c0 < lim) v.x = src[0];
+                if (c0 + 1 < lim) v.y = src[1];
+                if (c0 + 2 < lim) v.z = src[2];
+            }
+        }
+        return v;
+    };
+    f64x4v acc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) acc[u][v] = f64x4v{0.0, 0.0, 0.0, 0.0};
+    float4 ra[2], rb[2];
+    auto fetch = [&](int64_t k0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            ra[h] = ld4(Ab, lda, M, k0 + lr + 16 * h, i0 + lc);
+            rb[h] = ld4(Bb, ldb, N, k0 + lr + 16 * h, j0 + lc);
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<float4*>(&As[buf][lr + 16 * h][lc]) = ra[h];
+            *reinterpret_cast<float4*>(&Bs[buf][lr + 16 * h][lc]) = rb[h];
+        }
+    };
+    const int nsl = (int)ceil_div(kend - kbeg, GK);
+    if (nsl > 0) { fetch(kbeg); stash(0); }
+    __syncthreads();
+    const int li = lane & 15, lk = lane >> 4;
+    for (int sl = 0; sl < nsl; ++sl) {
+        const int cur = sl & 1;
+        if (sl + 1 < nsl) fetch(kbeg + (int64_t)(sl + 1) * GK);
+#pragma unroll
+        for (int kk = 0; kk < GK; kk += 4) {
+            double a0 = (double)As[cur][kk + lk][32 * wi + li];
+            double a1 = (double)As[cur][kk + lk][32 * wi + 16 + li];
+            double b0 = (double)Bs[cur][kk + lk][32 * wj + li];
+            double b1 = (double)Bs[cur][kk + lk][32 * wj + 16 + li];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (sl + 1 < nsl) stash(1 - cur);
+        __syncthreads();
+    }
+    double* P = part + ((int64_t)b * splits + split) * M * N;
+    // C/D map of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = i0 + 32 * wi + 16 * u + lk + 4 * r;
+                const int64_t j = j0 + 32 * wj + 16 * v + li;
+                if (i < M && j < N) P[i * N + j] = acc[u][v][r];
+            }
+}
+
+__global__ void gram_reduce_sym_kernel(const double* __restrict__ part, int64_t M, int splits,
+                                       int64_t batch, double* __restrict__ C) {
+    const int64_t MN = M * M, total = batch * MN;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = e / MN, o = e % MN, i = o / M, j = o % M;
+        const int64_t src = (i / GT > j / GT) ? j * M + i : o;  // lower tiles were skipped
+        double s = 0.0;
+        for (int t2 = 0; t2 < splits; ++t2) s += part[(b * splits + t2) * MN + src];
+        C[e] = s;
+    }
+}
+
 static int gram_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
     const int64_t tiles = ceil_div(M, GT) * ceil_div(N, GT) * batch;
     int64_t s = ceil_div(1024, tiles);
@@ -965,12 +1072,22 @@ int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, 
     const int64_t kchunk = ceil_div(ceil_div(K, splits), GK) * GK;
     hipStream_t s = as_stream(stream);
     dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT), (unsigned)(batch * splits));
+    const int64_t tot = batch * M * N;
+    const unsigned rgrid = (unsigned)std::min<int64_t>(ceil_div(tot, 256), 4096);
+    if (!trans_a && !trans_b && lda % 4 == 0 && ldb % 4 == 0 && stride_a % 4 == 0 && stride_b % 4 == 0) {
+        const int sym = (A == B && lda == ldb && stride_a == stride_b && M == N) ? 1 : 0;
+        gram_f64_mfma_kernel<<<grid, kGramThreads, 0, s>>>(M, N, K, kchunk, splits, A, lda, stride_a, B, ldb,
+                                                           stride_b, sym, reinterpret_cast<double*>(ws));
+        if (sym)
+            gram_reduce_sym_kernel<<<rgrid, 256, 0, s>>>(reinterpret_cast<double*>(ws), M, splits, batch, C);
+        else
+            gram_reduce_kernel<<<rgrid, 256, 0, s>>>(reinterpret_cast<double*>(ws), M * N, splits, batch, C);
+        return check_launch("cq_gram_f64");
+    }
     gram_f64_kernel<<<grid, kGramThreads, 0, s>>>(M, N, K, kchunk, splits, A, trans_a, lda,
                                                    stride_a, B, trans_b, ldb, stride_b,
                                                    reinterpret_cast<double*>(ws));
-    const int64_t tot = batch * M * N;
-    gram_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(tot, 256), 4096), 256, 0, s>>>(
-        reinterpret_cast<double*>(ws), M * N, splits, batch, C);
+    gram_reduce_kernel<<<rgrid, 256, 0, s>>>(reinterpret_cast<double*>(ws), M * N, splits, batch, C);
     return check_launch("cq_gram_f64");
 }
 

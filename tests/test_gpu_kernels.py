@@ -167,6 +167,20 @@ def test_gram_f64(K, ta, tb):
     assert (C.cpu() - ref).abs().max().item() < 1e-9
 
 
+@pytest.mark.parametrize("M,N,Kd,sym", [(192, 192, 4096, True), (130, 96, 1000, False), (190, 190, 333, True)])
+def test_gram_f64_mfma_paths(K, M, N, Kd, sym):
+    """Non-transposed Grams (fp64 MFMA path; symmetric X^T X skips and mirrors lower tiles)."""
+    g = torch.Generator().manual_seed(M + Kd)
+    A = torch.randn(3, Kd, M, generator=g)
+    Bm = A if sym else torch.randn(3, Kd, N, generator=g)
+    Ad = A.to(DEV)
+    C = K.gram_f64(Ad, Ad if sym else Bm.to(DEV))
+    ref = A.double().transpose(1, 2) @ Bm.double()
+    assert ((C.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-13
+    if sym:
+        assert torch.equal(C, C.transpose(1, 2))
+
+
 def test_spd_whiten_and_jacobi(K):
     torch.manual_seed(2)
     p = 96

@@ -25,14 +25,15 @@ W = bench.synth_batch(B, 0, dev)
 ep = EngineParams.from_caldera_params(bench.make_params())
 import json
 skw = json.loads(sys.argv[2]) if len(sys.argv) > 2 else {}
-eng = CalderaEngine(ep, solver_kwargs=skw)
+sp = skw.pop("p", None)
+eng = CalderaEngine(ep, solver_kwargs=skw, solver_p=sp)
 eng.run(W, None)
 torch.cuda.synchronize()
 for h in eng.solver.stats.history:
     print("solve cold=%s degs=%s resid=%s" % (h[0], h[1], ["%.2e" % r for r in h[2]]))
 print("matvecs", eng.solver.stats.matvecs, "jacobi calls", len(calls))
 W0 = bench.synth_batch(1, 0, dev)
-d0 = CalderaEngine(ep, solver_kwargs=skw).run(W0, None)[0]
+d0 = CalderaEngine(ep, solver_kwargs=skw, solver_p=sp).run(W0, None)[0]
 import numpy as np
 g = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "sum_large.npz"))
 om = np.random.default_rng(1234).standard_normal((4096, 16))
