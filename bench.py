@@ -172,7 +172,8 @@ def main():
         solver_p = eng.solver.p if eng.solver is not None else None
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
-            if pm["config"]["batch"] == B // parts and pm["config"]["p"] == solver_p and pm["kernel"] == probe["kernel"]:
+            if (pm["config"]["batch"] == B // parts and pm["config"]["p"] == solver_p
+                    and pm["kernel"] == probe["kernel"]):
                 traffic = pm["hbm_bytes_per_launch"]
         ach_tf = flops / t / 1e12
         ach_gb = nbytes / t / 1e9

@@ -15,3 +15,4 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm_x3 -d $
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gemm_x3 -d $OUT/pmc_write -o run \
     --output-format csv -- python3 bench.py --batch $B --steps 1 --warmup 0 --no-parity > $OUT/pmc_write.log 2>&1
 python3 tools/profile_summary.py $OUT/stats $OUT/pmc_fetch $OUT/pmc_write > $OUT/summary.txt
+python3 tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $B 192 4096 > $OUT/pmc_traffic.json
