@@ -94,6 +94,9 @@ _SIGS = {
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
+    "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -475,3 +478,32 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.active = active.data_ptr() if active is not None else None
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
     return C
+
+
+def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None, bits: int, *, eps: float = 1e-8,
+                codes=None, packed=None, scale=None, err_w=None, err_out=None):
+    """Fused Q update: quantise res = W - L R (W alone if L is None) per matrix, never
+    materialising res.  W (B, m, n) fp16/fp32, L (B, m, r), R (B, r, n) fp32 with r % 32 == 0.
+    Fills packed (B, m*n*bits/8) uint8 and/or codes, scale (B,), err_out (B,) fp64."""
+    _require_hip(W, L, R, codes, packed, scale, err_w, err_out)
+    assert W.is_contiguous()
+    B, m, n = W.shape
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[W.dtype]
+    dev = W.device
+    r = 0 if L is None else L.shape[-1]
+    halves = [None] * 4
+    inv = None
+    if r:
+        sL = pow2_scale(L.contiguous(), 14)
+        sR = pow2_scale(R.contiguous(), 14)
+        Lh, Ll = split_f16(L.contiguous(), sL)
+        Rth = torch.empty((B, n, r), dtype=torch.float16, device=dev)
+        Rtl = torch.empty_like(Rth)
+        transpose_split(R.contiguous(), hi=Rth, lo=Rtl, scale=sR)
+        inv = 1.0 / (sL * sR)
+        halves = [Lh, Ll, Rth, Rtl]
+    lib = load()
+    ws = workspace(lib.cq_q_update_workspace(m, n, B), dev)
+    _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),
+                              _p(packed), _p(scale), _p(err_w), _p(err_out), _p(ws), ws.numel(), _stream(dev)),
+           "cq_q_update_x3")

@@ -65,6 +65,21 @@ __device__ __forceinline__ double block_sum_f64(double v, double* lds /* >= 16 *
     return s;
 }
 
+// ---- uniform quantiser arithmetic (quantization.py:93-105, :244-269), shared by the
+// standalone quantiser and the fused Q update
+__device__ __forceinline__ float quant_scale(uint32_t bits, float eps) {
+    const float m = __uint_as_float(bits);
+    return (m != m) ? m : fmaxf(m, eps);  // torch.maximum propagates NaN; fmaxf would not
+}
+
+// code = rint((x / s) * k): two IEEE roundings then round-half-even (quantization.py:95-96,266)
+__device__ __forceinline__ float quant_code(float x, float s, float k) {
+    const float norm = x / s;
+    const float scaled = norm * k;
+    return rintf(scaled);
+}
+__device__ __forceinline__ float dequant(float c, float k, float s) { return (c / k) * s; }
+
 }  // namespace cq
 
 #define CQ_REQUIRE(cond, ...)                                  \

@@ -39,19 +39,6 @@ int check_launch(const char* what) {
 
 constexpr int kThreads = 256;
 
-__device__ __forceinline__ float quant_scale(uint32_t bits, float eps) {
-    const float m = __uint_as_float(bits);
-    return (m != m) ? m : fmaxf(m, eps);  // torch.maximum propagates NaN; fmaxf would not
-}
-
-// code = rint((x / s) * k): two IEEE roundings then round-half-even (quantization.py:95-96,266)
-__device__ __forceinline__ float quant_code(float x, float s, float k) {
-    const float norm = x / s;
-    const float scaled = norm * k;
-    return rintf(scaled);
-}
-__device__ __forceinline__ float dequant(float c, float k, float s) { return (c / k) * s; }
-
 // ------------------------------------------------------------------ RMS scale (alg.py:38-42)
 template <int DT>
 __global__ __launch_bounds__(kThreads) void rms_partial_kernel(const void* __restrict__ W,

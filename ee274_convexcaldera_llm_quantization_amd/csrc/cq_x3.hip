@@ -388,8 +388,11 @@ constexpr size_t XW_LDS_BYTES = (size_t)2 * XW_STAGE * sizeof(_Float16);  // 144
 constexpr int XW_PER_WAVE = (2 * XW_BM / 16 + 2 * XW_BN / 16) / (XW_THREADS / 64);  // 6
 static_assert(XW_PER_WAVE == 6, "load split");
 
-__device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
-                                         _Float16* stage, int wid, int lane) {
+// Load plan: the wave-uniform part of each of this wave's 6 LDS-DMA loads (which image,
+// which 16-row group) is scalar; the per-lane part is a 32-bit element offset computed once
+// per tile, so a K step costs one 64-bit add per load (keeps the loop free of spills).
+__device__ __forceinline__ void xw_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
+                                        uint32_t (&off)[XW_PER_WAVE]) {
 #pragma unroll
     for (int u = 0; u < XW_PER_WAVE; ++u) {
         const int I = wid * XW_PER_WAVE + u;  // 0..71: Ah 0-11, Al 12-23, Bh 24-47, Bl 48-71
@@ -401,48 +404,49 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t m0, in
         const int64_t lim = isA ? a.M : a.N;
         int64_t gr = (isA ? m0 : n0) + row;
         gr = gr < lim ? gr : lim - 1;
-        const _Float16* src;
-        if (isA) src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + c * 8;
-        else if (a.b_blocked) src = (part ? a.Bl : a.Bh) + b * a.sb + (k0 >> 5) * (a.ldb * 32) + gr * 32 + c * 8;
-        else src = (part ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + c * 8;
-        _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        off[u] = (uint32_t)(isA ? gr * a.lda + c * 8 : a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8);
     }
 }
 
-__global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
-    extern __shared__ __attribute__((aligned(16))) char xw_smem_raw[];
-    _Float16* smem = reinterpret_cast<_Float16*>(xw_smem_raw);
-    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-    const int64_t tn = lin % a.tiles_n;
-    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
-    const int64_t b = lin / (a.tiles_n * a.tiles_m);
-    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
-    if (a.tri && n0 + XW_BN <= m0) return;
+__device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                         const uint32_t (&off)[XW_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW_PER_WAVE; ++u) {
+        const int I = wid * XW_PER_WAVE + u;
+        const bool isA = I < 24;
+        const int part = isA ? (I >= 12) : (I >= 48);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + k0
+                                   : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
+        _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
+                                         16, 0, 0);
+    }
+}
 
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
+// The 192 x 384 tile's K loop (shared by the filter/Gram product and the fused Q update):
+// acc = A[m0.., :] B[n0.., :]^T over K, split-fp16 products; nt = 0 leaves acc = 0.
+__device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
+                                            _Float16* smem, int wid, int lane, int wm, int wn,
+                                            f32x16v (&acc)[3][2]) {
     const int lr = lane & 31, lh = lane >> 5;
-
-    f32x16v acc[3][2];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const bool live = !a.active || a.active[b];
-    const int64_t nt = live ? a.K / XW_BK : 0;
-    if (nt > 0) xw_issue(a, b, m0, n0, 0, smem, wid, lane);
+    wid = __builtin_amdgcn_readfirstlane(wid);  // wave-uniform: load selection stays scalar
+    uint32_t off[XW_PER_WAVE];
+    if (nt > 0) {
+        xw_plan(a, m0, n0, wid, lane, off);
+        xw_issue(a, b, 0, smem, wid, off);
+    }
     for (int64_t t = 0; t < nt; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
-        if (t + 1 < nt) xw_issue(a, b, m0, n0, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, lane);
+        if (t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
         const _Float16* sA = smem + (t & 1) * XW_STAGE;
         const _Float16* sB = sA + 2 * XW_APART;
 #pragma unroll
@@ -471,6 +475,29 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
                 }
         }
     }
+}
+
+__global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char xw_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(xw_smem_raw);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+    const int64_t tn = lin % a.tiles_n;
+    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
+    const int64_t b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
+    if (a.tri && n0 + XW_BN <= m0) return;
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
+    const int lr = lane & 31, lh = lane >> 5;
+
+    f32x16v acc[3][2];
+    const bool live = !a.active || a.active[b];
+    const int64_t nt = live ? a.K / XW_BK : 0;
+    xw_mainloop(a, b, m0, n0, nt, smem, wid, lane, wm, wn, acc);
 
     const float sc = a.inv_scale[b];
     // inactive entries (converged matrices) pass D through unchanged
@@ -503,6 +530,148 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
             }
         }
     if (ovf) atomicOr(a.overflow + b, 1);
+}
+
+
+// ------------------------------------------------------------------ fused Q update
+// maybe_update_Q (alg.py:253-283) + quantize_matrix (alg.py:245-250, quantization.py:244-269)
+// without materialising the residual: res = W - L R is recomputed per 192 x 384 tile from
+// the split-fp16 halves of L (m x r) and R^T (n x r) (K = r; r = 0: res = W exactly) in two
+// passes over W:
+//   pass 0: per-matrix max |res| (uint bits, NaN sorts above inf like torch.max) -> atomicMax;
+//   pass 1: scale = max(absmax, eps); code = rint((res / scale) k) (IEEE division, then the
+//           multiply, round-half-even: the reference's two roundings); packed offset-binary
+//           codes (c + k, MSB-first: 4 per byte at 2 bits, 2 per byte at 4 bits) or int8/int16
+//           codes; sum_j w_j (deq - res)^2 per tile in fp64 (deterministic 2-stage sum).
+// Both passes evaluate res with identical code, so pass 1 sees pass 0's values bit for bit.
+struct QUK {
+    X3K x;                       // A = L halves, B = R^T halves, inv_scale, K = r, tiling
+    const void* W; int wf16;     // W (m x n), fp16 or fp32
+    int64_t m, n;
+    uint32_t* absmax;            // [batch] bits, zeroed before pass 0
+    float eps;
+    void* codes;                 // int8 / int16 (m x n), or NULL
+    uint8_t* packed;             // packed bytes (m n bits / 8), or NULL
+    float* scale;                // [batch] out (pass 1)
+    const float* ew;             // error column weights [n] or NULL (= 1)
+    double* part;                // [batch * tiles] error partials
+};
+
+template <int PASS, int BITS>
+__global__ __launch_bounds__(XW_THREADS, 1) void q_update_x3_kernel(QUK q) {
+    extern __shared__ __attribute__((aligned(16))) char qu_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(qu_smem_raw);
+    const X3K& a = q.x;
+    const int64_t tiles = a.tiles_n * a.tiles_m;
+    const int64_t total = tiles * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
+    const int64_t tile = lin % tiles;
+    const int64_t tn = tile % a.tiles_n, tm = tile / a.tiles_n;
+    const int64_t b = lin / tiles;
+    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    // transposed product: A operand = R^T (tile rows = columns of W), B operand = L (tile
+    // columns = rows of W), so each lane owns one row of W and holds 4 runs of 4 consecutive
+    // columns: W loads are 8-byte vectors and 4 two-bit codes make one byte in-lane
+    f32x16v acc[3][2];
+    xw_mainloop(a, b, m0, n0, a.K / XW_BK, smem, wid, lane, wm, wn, acc);
+    const float sc = a.K > 0 ? a.inv_scale[b] : 0.f;
+    const int64_t MN = q.m * q.n;
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN;
+    const float* Wf = reinterpret_cast<const float*>(q.W) + b * MN;
+
+    constexpr float kq = (float)((1 << (BITS - 1)) - 1);
+    uint32_t mx = 0;
+    double err = 0.0;
+    float s = 0.f;
+    if (PASS == 1) s = quant_scale(q.absmax[b], q.eps);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int64_t row = n0 + 64 * wn + 32 * j + lr;  // row of W (tile column)
+        if (row >= q.m) continue;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int64_t col = m0 + 96 * wm + 32 * i + 8 * g4 + 4 * lh;  // 4 consecutive columns
+                if (col >= q.n) continue;  // n % 4 == 0: a run is all in or all out
+                const int64_t e = row * q.n + col;
+                float w4[4];
+                if (q.wf16) {
+                    const uint2 raw = *reinterpret_cast<const uint2*>(Wh + e);
+                    const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) w4[u] = (float)hv[u];
+                } else {
+                    const float4 f = *reinterpret_cast<const float4*>(Wf + e);
+                    w4[0] = f.x; w4[1] = f.y; w4[2] = f.z; w4[3] = f.w;
+                }
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    v[u] = a.K > 0 ? w4[u] - acc[i][j][4 * g4 + u] * sc : w4[u];  // res = W - L R (alg.py:262)
+                if (PASS == 0) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) mx = max(mx, abs_bits(v[u]));
+                } else {
+                    float c[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        c[u] = quant_code(v[u], s, kq);
+                        const float d = dequant(c[u], kq, s) - v[u];
+                        err += (double)(d * d) * (q.ew ? (double)q.ew[col + u] : 1.0);
+                    }
+                    if constexpr (BITS <= 4) {
+                        if (q.packed) {
+                            uint32_t uq[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) uq[u] = (uint32_t)((int)c[u] + (int)kq);
+                            if (BITS == 2) {
+                                q.packed[(b * MN + e) / 4] = (uint8_t)((uq[0] << 6) | (uq[1] << 4) | (uq[2] << 2) | uq[3]);
+                            } else {
+                                *reinterpret_cast<uchar2*>(q.packed + (b * MN + e) / 2) =
+                                    make_uchar2((uint8_t)((uq[0] << 4) | uq[1]), (uint8_t)((uq[2] << 4) | uq[3]));
+                            }
+                        }
+                    }
+                    if (q.codes) {
+                        if (BITS <= 8)
+                            *reinterpret_cast<char4*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) =
+                                make_char4((signed char)(int)c[0], (signed char)(int)c[1], (signed char)(int)c[2],
+                                           (signed char)(int)c[3]);
+                        else
+                            *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(q.codes) + b * MN + e) =
+                                make_short4((short)(int)c[0], (short)(int)c[1], (short)(int)c[2], (short)(int)c[3]);
+                    }
+                }
+            }
+    }
+    if (PASS == 0) {
+        mx = wave_max_u32(mx);
+        if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
+    } else if (q.part) {
+        __shared__ double red[16];
+        const double tsum = block_sum_f64(err, red);
+        if (threadIdx.x == 0) q.part[b * tiles + tile] = tsum;
+    }
+}
+
+__global__ void q_update_finalize_kernel(const uint32_t* absmax, const double* part, int64_t tiles, int64_t batch,
+                                         float eps, float* scale, double* err_out) {
+    const int64_t b = blockIdx.x;
+    if (b >= batch) return;
+    double s = 0.0;
+    for (int64_t t = threadIdx.x; t < tiles; t += 64) s += part[b * tiles + t];
+    s = wave_sum(s);  // one wave: fixed order -> deterministic
+    if (threadIdx.x == 0) {
+        if (scale) scale[b] = quant_scale(absmax[b], eps);
+        if (err_out) err_out[b] = s;
+    }
 }
 
 // ------------------------------------------------------------------ split / transpose helpers
@@ -711,6 +880,61 @@ int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch
     transpose_split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, rows, cols, Y, reinterpret_cast<_Float16*>(hi),
                                                                  reinterpret_cast<_Float16*>(lo), scale, scale_v);
     return check_launch("cq_transpose_split");
+}
+
+
+size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
+    const int64_t tiles = ceil_div(n, XW_BM) * ceil_div(m, XW_BN);
+    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) + (size_t)batch * tiles * sizeof(double);
+}
+
+int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
+                   const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl, const float* inv_scale, int bits,
+                   float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w, double* err_out,
+                   void* ws, size_t ws_bytes, void* stream) {
+    CQ_REQUIRE(W && m > 0 && n > 0 && batch > 0 && r >= 0, "cq_q_update_x3: bad shape");
+    CQ_REQUIRE(dtype == CQ_F16 || dtype == CQ_F32, "cq_q_update_x3: dtype must be f16/f32");
+    if (bits != 2 && bits != 4 && bits != 8 && bits != 16) return set_error(CQ_EINVAL, "Bit-width not supported!");
+    CQ_REQUIRE(r == 0 || (Lh && Ll && Rth && Rtl && inv_scale), "cq_q_update_x3: null factor halves");
+    CQ_REQUIRE(r % XW_BK == 0, "cq_q_update_x3: rank must be a multiple of 32");
+    CQ_REQUIRE(n % 4 == 0, "cq_q_update_x3: n must be a multiple of 4");
+    CQ_REQUIRE(!packed || bits <= 4, "cq_q_update_x3: packing needs bits <= 4");
+    CQ_REQUIRE(codes || packed, "cq_q_update_x3: no code output");
+    if (!ws || ws_bytes < cq_q_update_workspace(m, n, batch)) return set_error(CQ_EWORKSPACE, "cq_q_update_x3: workspace too small");
+    QUK q;
+    X3K& a = q.x;
+    memset(&a, 0, sizeof(a));
+    // A operand R^T (n x r): tile rows run over W's columns; B operand L (m x r): tile
+    // columns run over W's rows (see q_update_x3_kernel)
+    a.M = n; a.N = m; a.K = r; a.batch = batch;
+    a.Ah = reinterpret_cast<const _Float16*>(Rth); a.Al = reinterpret_cast<const _Float16*>(Rtl);
+    a.lda = r; a.sa = n * r;
+    a.Bh = reinterpret_cast<const _Float16*>(Lh); a.Bl = reinterpret_cast<const _Float16*>(Ll);
+    a.ldb = r; a.sb = m * r;
+    a.inv_scale = inv_scale;
+    a.tiles_n = ceil_div(m, XW_BN);
+    a.tiles_m = ceil_div(n, XW_BM);
+    const int64_t tiles = a.tiles_n * a.tiles_m;
+    CQ_REQUIRE(tiles * batch < (1ll << 31), "cq_q_update_x3: grid too large");
+    q.W = W; q.wf16 = dtype == CQ_F16; q.m = m; q.n = n;
+    q.absmax = reinterpret_cast<uint32_t*>(ws);
+    q.part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + align_up((size_t)batch * sizeof(uint32_t), 256));
+    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w;
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(q.absmax, 0, batch * sizeof(uint32_t), s) != hipSuccess)
+        return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
+    const unsigned grid = (unsigned)(tiles * batch);
+#define CQ_QU(B) do { q_update_x3_kernel<0, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); \
+                      q_update_x3_kernel<1, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); } while (0)
+    switch (bits) {
+        case 2: CQ_QU(2); break;
+        case 4: CQ_QU(4); break;
+        case 8: CQ_QU(8); break;
+        default: CQ_QU(16); break;
+    }
+#undef CQ_QU
+    q_update_finalize_kernel<<<(unsigned)batch, 64, 0, s>>>(q.absmax, q.part, tiles, batch, eps, scale_out, err_out);
+    return check_launch("cq_q_update_x3");
 }
 
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {

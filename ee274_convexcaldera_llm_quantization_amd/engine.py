@@ -169,8 +169,19 @@ class CalderaEngine:
         """maybe_update_Q / update_Q_non_data_aware (alg.py:253-283) + error (:286-302)."""
         p = self.p
         B, m, n = st.B, st.m, st.n
-        absmax = torch.zeros(B, dtype=torch.int32, device=Ws.device)  # |res| max as uint32 bits
         Kdim = st.L.shape[-1] if (p.compute_low_rank_factors and st.has_LR) else 0
+        if Kdim % 32 == 0:
+            # fused: res = W - L R recomputed per tile on split-fp16 products, never stored
+            err = torch.empty(B, dtype=torch.float64, device=Ws.device)
+            Lm = st.L if Kdim else None
+            Rm = st.R if Kdim else None
+            if st.q_packed:
+                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, packed=st.Qc, scale=st.Qs, err_w=wts.err, err_out=err)
+            else:
+                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, codes=st.Qc, scale=st.Qs, err_w=wts.err, err_out=err)
+            st.has_Q = True
+            return err
+        absmax = torch.zeros(B, dtype=torch.int32, device=Ws.device)  # |res| max as uint32 bits
         Lm = st.L[:, :, :Kdim]
         Rm = st.R[:, :Kdim, :]
         # res = W - L R  (alg.py:262; RESID epilogue also produces |res| max for the quantiser)

@@ -226,6 +226,20 @@ typedef struct cq_x3_args {
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
 
+/* Fused Q update.  Replaces alg.py:253-283 (maybe_update_Q / update_Q_non_data_aware:
+ * res = W - L@R, quantize_matrix) + quantization.py:244-269 (whole-matrix uniform quantise):
+ * res is recomputed per tile from the split-fp16 halves of L (m x r) and R^T (n x r,
+ * inv_scale[b] = 1 / (scale_L * scale_R)) and never written; two passes over W (absmax, then
+ * quantise).  r = 0 (no LR yet): res = W exactly, factor pointers may be NULL.  Outputs:
+ * packed offset-binary codes (bits 2/4) and/or int8/int16 codes, scale_out[b] =
+ * max(max|res|, eps), err_out[b] = sum_ij err_w[j] (deq - res)^2 (fp64; err_w NULL = 1). */
+size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch);
+int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
+                   const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
+                   const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,
+                   float* scale_out, const float* err_w, double* err_out, void* ws,
+                   size_t ws_bytes, void* stream);
+
 /* Chebyshev 3-term recurrence support and elementwise helpers. */
 /* out[b] = sum(x[b]^2 * w[j % ncols]) fp64 (w may be NULL) — denominators of alg.py:298 */
 int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel,

@@ -449,3 +449,52 @@ def test_pow2_scale_and_split(K):
     tl = torch.empty_like(th)
     K.transpose_split(X, out=Y, hi=th, lo=tl, scale=s)
     assert torch.equal(th, rh.transpose(1, 2)) and torch.equal(tl, rl.transpose(1, 2))
+
+
+@pytest.mark.parametrize("bits", [2, 4, 8, 16])
+def test_q_update_x3_without_lr_is_exact(K, bits):
+    """r = 0 (first Q update, alg.py:262 with no LR): res = W, so the fused kernel must match
+    the standalone whole-matrix quantiser bit for bit (codes, packed bytes, scale)."""
+    g = torch.Generator(device=DEV).manual_seed(bits)
+    W = (torch.randn(3, 200, 392, device=DEV, generator=g) * 0.02).half()
+    ref = K.quantize_uniform(W.float().view(3, -1), 200 * 392, bits, codes=True)
+    codes = torch.empty(3, 200 * 392, dtype=K.code_dtype(bits), device=DEV)
+    scale = torch.empty(3, device=DEV)
+    err = torch.empty(3, dtype=torch.float64, device=DEV)
+    K.q_update_x3(W, None, None, bits, codes=codes, scale=scale, err_out=err)
+    assert torch.equal(codes, ref["codes"].view(3, -1))
+    assert torch.equal(scale, ref["scale"].view(3))
+    if bits <= 4:
+        packed = torch.empty(3, 200 * 392 * bits // 8, dtype=torch.uint8, device=DEV)
+        K.q_update_x3(W, None, None, bits, packed=packed, scale=scale)
+        assert torch.equal(K.unpack_codes(packed, 200 * 392, bits).view(3, -1).to(codes.dtype), codes)
+    # the kernel's arithmetic: deq = (c / k) * s and d = deq - x in fp32, d^2 summed in fp64
+    deq = (codes.float() / float(2 ** (bits - 1) - 1)) * scale.view(3, 1)
+    d = deq - W.float().view(3, -1)
+    e_ref = (d * d).double().sum(1)
+    # torch fp32 division vs the IEEE one in-kernel: visible at 16 bits, where the error is tiny
+    assert torch.allclose(err, e_ref, rtol=1e-4 if bits == 16 else 1e-6, atol=0)
+
+
+def test_q_update_x3_with_lr_matches_fp64_residual(K):
+    """r = 64: codes of res = W - L R agree with those of the fp64 residual except at
+    rounding boundaries; scale to fp32 rounding; error to 1e-6 relative."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    B, m, n, r = 2, 300, 520, 64
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.02).half()
+    L = torch.linalg.qr(torch.randn(B, m, r, device=DEV, generator=g))[0].contiguous()
+    R = (torch.randn(B, r, n, device=DEV, generator=g) * 0.01).contiguous()
+    packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=DEV)
+    scale = torch.empty(B, device=DEV)
+    err = torch.empty(B, dtype=torch.float64, device=DEV)
+    w = torch.rand(n, device=DEV, generator=g) + 0.5
+    K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_w=w, err_out=err)
+    res = W.double() - L.double() @ R.double()
+    s64 = res.abs().amax((1, 2))
+    assert torch.allclose(scale.double(), s64, rtol=1e-6, atol=0)
+    c = K.unpack_codes(packed, m * n, 2).view(B, m, n).double()
+    c_ref = torch.round(res / scale.double().view(B, 1, 1))
+    assert (c != c_ref).double().mean().item() < 1e-3
+    deq = c * scale.double().view(B, 1, 1)
+    e_ref = (((deq - res) ** 2) * w.double()).sum((1, 2))
+    assert torch.allclose(err, e_ref, rtol=1e-4, atol=0)
