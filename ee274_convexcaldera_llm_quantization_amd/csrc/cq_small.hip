@@ -694,6 +694,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             od[u][r] = (x == 2 * k + 1) ? 1.f : 0.f;
         }
     __syncthreads();
+    const double skip_rel = fmax(1e-17, 0.01 * tol);
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
@@ -716,7 +717,10 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                 if (j < p) {
                     const double aij = a[pk(i, j)];
                     const double aii = a[pk(i, i)], ajj = a[pk(j, j)];
-                    if (fabs(aij) > 1e-300 && fabs(aij) > 1e-17 * sqrt(fabs(aii * ajj))) {
+                    // threshold Jacobi: elements below tol/100 of their diagonal scale are left
+                    // alone (their total stays under the off-norm tolerance), so the last sweeps
+                    // skip most pair-block updates
+                    if (fabs(aij) > 1e-300 && fabs(aij) > skip_rel * sqrt(fabs(aii * ajj))) {
                         const double th = (ajj - aii) / (2.0 * aij);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
                         c = 1.0 / sqrt(1.0 + t * t);
