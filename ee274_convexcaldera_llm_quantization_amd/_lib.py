@@ -57,6 +57,8 @@ class X3Args(ctypes.Structure):
         ("tri", c_int),
         ("b_blocked", c_int),
         ("active", c_vp),
+        ("a_blocked", c_int),
+        ("o_blocked", c_int),
     ]
 
 
@@ -90,9 +92,9 @@ _SIGS = {
     "cq_scale_rc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                             c_i64, c_vp, c_i64, c_vp]),
     "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "cq_transpose_split": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
+    "cq_transpose_split": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp, c_int, c_vp]),
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
-    "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp]),
+    "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
@@ -407,7 +409,8 @@ def sym_split_f16(G: torch.Tensor, x_scale: float, *, hi=None, lo=None, scale=No
     return hi, lo, scale, inv_scale
 
 
-def transpose_split(X: torch.Tensor, *, out=None, hi=None, lo=None, scale: float | torch.Tensor = 1.0):
+def transpose_split(X: torch.Tensor, *, out=None, hi=None, lo=None, scale: float | torch.Tensor = 1.0,
+                    blocked: bool = False):
     """X (B, r, c) fp32 contiguous -> X^T (B, c, r) fp32 (out) and/or its fp16 split (hi, lo)
     scaled by `scale` (a float, or a (B,) fp32 tensor of per-matrix scales)."""
     _require_hip(X)
@@ -415,7 +418,8 @@ def transpose_split(X: torch.Tensor, *, out=None, hi=None, lo=None, scale: float
     B, r, c = X.shape
     sv = scale if torch.is_tensor(scale) else None
     sf = 1.0 if sv is not None else float(scale)
-    _check(load().cq_transpose_split(_p(X), r, c, B, _p(out), _p(hi), _p(lo), sf, _p(sv), _stream(X.device)),
+    _check(load().cq_transpose_split(_p(X), r, c, B, _p(out), _p(hi), _p(lo), sf, _p(sv), int(bool(blocked)),
+                                     _stream(X.device)),
            "cq_transpose_split")
     return out, hi, lo
 
@@ -431,8 +435,9 @@ def pow2_scale(X: torch.Tensor, log2_target: int = 14, out=None):
     return out
 
 
-def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None):
-    """fp16 halves of X * scale (scale: float or (B,) tensor), same shape as X."""
+def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False):
+    """fp16 halves of X * scale (scale: float or (B,) tensor), same shape as X; blocked: the
+    K-blocked operand layout over X's last dimension (storage size unchanged)."""
     _require_hip(X)
     assert X.dtype == torch.float32 and X.is_contiguous()
     B = X.shape[0]
@@ -440,13 +445,15 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None):
     lo = torch.empty(X.shape, dtype=torch.float16, device=X.device) if lo is None else lo
     sv = scale if torch.is_tensor(scale) else None
     sf = 1.0 if sv is not None else float(scale)
-    _check(load().cq_split_f16(_p(X), X.numel() // B, B, _p(sv), sf, _p(hi), _p(lo), _stream(X.device)),
+    _check(load().cq_split_f16(_p(X), X.numel() // B, B, _p(sv), sf, _p(hi), _p(lo),
+                               X.shape[-1] if blocked else 0, _stream(X.device)),
            "cq_split_f16")
     return hi, lo
 
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
-            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None):
+            out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
+            a_blocked=False, o_blocked=False):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l."""
@@ -458,7 +465,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         assert t is None or t.is_contiguous()
     g = X3Args()
     g.M, g.N, g.K, g.batch = M, N, Kd, Bt
-    g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), Kd, M * Kd
+    g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (M if a_blocked else Kd), M * Kd
     g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), (N if b_blocked else Kd), N * Kd
     g.inv_scale = inv_scale.data_ptr()
     g.C, g.ldc, g.stride_c = C.data_ptr(), N, M * N
@@ -476,6 +483,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.tri = int(bool(tri))
     g.b_blocked = int(bool(b_blocked))
     g.active = active.data_ptr() if active is not None else None
+    g.a_blocked = int(bool(a_blocked))
+    g.o_blocked = int(bool(o_blocked))
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
     return C
 

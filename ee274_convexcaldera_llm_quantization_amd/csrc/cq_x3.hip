@@ -46,6 +46,8 @@ struct X3K {
     int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
     int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
     const int* active;  // per batch (NULL = all): inactive entries skip the product, C = D
+    int a_blocked;  // A halves K-blocked [K/32][lda rows][32] (lda = rows)
+    int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
     int64_t tiles_n, tiles_m;
 };
 
@@ -404,7 +406,8 @@ __device__ __forceinline__ void xw_plan(const X3K& a, int64_t m0, int64_t n0, in
         const int64_t lim = isA ? a.M : a.N;
         int64_t gr = (isA ? m0 : n0) + row;
         gr = gr < lim ? gr : lim - 1;
-        off[u] = (uint32_t)(isA ? gr * a.lda + c * 8 : a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8);
+        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * 32 + c * 8 : gr * a.lda + c * 8)
+                                : (a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8));
     }
 }
 
@@ -416,7 +419,7 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _F
         const bool isA = I < 24;
         const int part = isA ? (I >= 12) : (I >= 48);
         const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
-        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + k0
+        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
         __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
@@ -523,8 +526,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
                     const float hs = v * a.out_scale;
                     const _Float16 h = (_Float16)hs;
                     const _Float16 l = (_Float16)(hs - (float)h);
-                    a.Oh[b * a.so + row * a.ldo + col] = h;
-                    a.Ol[b * a.so + row * a.ldo + col] = l;
+                    const int64_t o = b * a.so + (a.o_blocked ? (col >> 5) * (a.M * 32) + row * 32 + (col & 31)
+                                                              : row * a.ldo + col);
+                    a.Oh[o] = h;
+                    a.Ol[o] = l;
                     ovf |= !(fabsf(hs) < 65504.f);
                 }
             }
@@ -707,6 +712,7 @@ __global__ void split_kernel(const float* __restrict__ X, int64_t n_per, const f
     const int64_t tot4 = batch * n_per / 4;
     for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < tot4; q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = q * 4;
+        const int64_t o = e;
         const float s = s_v ? s_v[e / n_per] : s_fixed;
         const float4 v = *reinterpret_cast<const float4*>(X + e);
         const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
@@ -716,8 +722,8 @@ __global__ void split_kernel(const float* __restrict__ X, int64_t n_per, const f
             h[u] = (_Float16)xs[u];
             l[u] = (_Float16)(xs[u] - (float)h[u]);
         }
-        *reinterpret_cast<uint2*>(hi + e) = *reinterpret_cast<const uint2*>(h);
-        *reinterpret_cast<uint2*>(lo + e) = *reinterpret_cast<const uint2*>(l);
+        *reinterpret_cast<uint2*>(hi + o) = *reinterpret_cast<const uint2*>(h);
+        *reinterpret_cast<uint2*>(lo + o) = *reinterpret_cast<const uint2*>(l);
     }
 }
 
@@ -786,12 +792,40 @@ __global__ void pow2_scale_kernel(float* __restrict__ s, int64_t batch, int log2
     s[b] = ldexpf(1.f, log2_target - e);
 }
 
+// K-blocked split (ncols % 32 == 0): element (row, col) of a rows x ncols matrix goes to
+// (col / 32) * rows * 32 + row * 32 + col % 32 — the K-blocked operand layout of cq_gemm_x3.
+// grid (rows / 4, batch): one row per wave, no integer division.
+__global__ __launch_bounds__(256) void split_blocked_kernel(const float* __restrict__ X, int64_t rows, int64_t ncols,
+                                                            const float* __restrict__ s_v, float s_fixed,
+                                                            _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+    const int64_t b = blockIdx.y;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float s = s_v ? s_v[b] : s_fixed;
+    const float* xr = X + b * rows * ncols + row * ncols;
+    _Float16* hb = hi + b * rows * ncols + row * 32;
+    _Float16* lb = lo + b * rows * ncols + row * 32;
+    for (int64_t c = 4 * (threadIdx.x & 63); c < ncols; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + c);
+        const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+        _Float16 h[4], l[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            h[u] = (_Float16)xs[u];
+            l[u] = (_Float16)(xs[u] - (float)h[u]);
+        }
+        const int64_t o = (c >> 5) * rows * 32 + (c & 31);
+        *reinterpret_cast<uint2*>(hb + o) = *reinterpret_cast<const uint2*>(h);
+        *reinterpret_cast<uint2*>(lb + o) = *reinterpret_cast<const uint2*>(l);
+    }
+}
+
 // Batched transpose Y = X^T (X rows x cols, row-major) through a 64 x 65 LDS tile, with an
 // optional fp16 split of Y (scale s).
 __global__ __launch_bounds__(256) void transpose_split_kernel(const float* __restrict__ X, int64_t rows, int64_t cols,
                                                               float* __restrict__ Y, _Float16* __restrict__ hi,
                                                               _Float16* __restrict__ lo, float s_fixed,
-                                                              const float* __restrict__ s_v) {
+                                                              const float* __restrict__ s_v, int blocked) {
     __shared__ float tile[64][65];
     const int64_t b = blockIdx.z;
     const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
@@ -812,8 +846,10 @@ __global__ __launch_bounds__(256) void transpose_split_kernel(const float* __res
             if (hi) {
                 const float xs = v * s;
                 const _Float16 h = (_Float16)xs;
-                hi[ob + orow * rows + ocol] = h;
-                lo[ob + orow * rows + ocol] = (_Float16)(xs - (float)h);
+                // Y is cols x rows: K-blocked halves put (orow, ocol) at (ocol/32)*cols*32 + orow*32 + ocol%32
+                const int64_t o = blocked ? ob + (ocol >> 5) * cols * 32 + orow * 32 + (ocol & 31) : ob + orow * rows + ocol;
+                hi[o] = h;
+                lo[o] = (_Float16)(xs - (float)h);
             }
         }
     }
@@ -861,24 +897,34 @@ int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target,
 }
 
 int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scale_v, float scale, uint16_t* hi,
-                 uint16_t* lo, void* stream) {
+                 uint16_t* lo, int64_t blocked_ncols, void* stream) {
     CQ_REQUIRE(X && hi && lo, "cq_split_f16: null pointer");
     CQ_REQUIRE(n_per > 0 && batch > 0 && n_per % 4 == 0, "cq_split_f16: n_per must be a positive multiple of 4");
+    CQ_REQUIRE(blocked_ncols == 0 || (blocked_ncols % 32 == 0 && n_per % blocked_ncols == 0),
+               "cq_split_f16: blocked layout needs ncols % 32 == 0 dividing n_per");
     const int64_t tot4 = batch * n_per / 4;
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(tot4, 256), 8192);
+    if (blocked_ncols) {
+        const int64_t rows = n_per / blocked_ncols;
+        CQ_REQUIRE(batch < 65536, "cq_split_f16: batch too large");
+        split_blocked_kernel<<<dim3((unsigned)ceil_div(rows, 4), (unsigned)batch), 256, 0, as_stream(stream)>>>(
+            X, rows, blocked_ncols, scale_v, scale, reinterpret_cast<_Float16*>(hi), reinterpret_cast<_Float16*>(lo));
+        return check_launch("cq_split_f16");
+    }
     split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, n_per, scale_v, scale, reinterpret_cast<_Float16*>(hi),
                                                       reinterpret_cast<_Float16*>(lo), batch);
     return check_launch("cq_split_f16");
 }
 
 int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch, float* Y, uint16_t* hi,
-                       uint16_t* lo, float scale, const float* scale_v, void* stream) {
+                       uint16_t* lo, float scale, const float* scale_v, int blocked, void* stream) {
+    CQ_REQUIRE(!blocked || rows % 32 == 0, "cq_transpose_split: blocked halves need rows % 32 == 0");
     CQ_REQUIRE(X && (Y || (hi && lo)), "cq_transpose_split: null pointer");
     CQ_REQUIRE(!hi == !lo, "cq_transpose_split: hi and lo go together");
     CQ_REQUIRE(rows > 0 && cols > 0 && batch > 0 && batch < 65536, "cq_transpose_split: bad shape");
     dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64), (unsigned)batch);
     transpose_split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, rows, cols, Y, reinterpret_cast<_Float16*>(hi),
-                                                                 reinterpret_cast<_Float16*>(lo), scale, scale_v);
+                                                                 reinterpret_cast<_Float16*>(lo), scale, scale_v, blocked);
     return check_launch("cq_transpose_split");
 }
 
@@ -903,7 +949,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     if (!ws || ws_bytes < cq_q_update_workspace(m, n, batch)) return set_error(CQ_EWORKSPACE, "cq_q_update_x3: workspace too small");
     QUK q;
     X3K& a = q.x;
-    memset(&a, 0, sizeof(a));
+    memset(&a, 0, sizeof(a));  // a_blocked = b_blocked = 0, no active mask
     // A operand R^T (n x r): tile rows run over W's columns; B operand L (m x r): tile
     // columns run over W's rows (see q_update_x3_kernel)
     a.M = n; a.N = m; a.K = r; a.batch = batch;
@@ -944,7 +990,9 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(g->K % X3_BK == 0, "cq_gemm_x3: K must be a multiple of 32");
     CQ_REQUIRE(g->lda % 8 == 0 && g->ldb % 8 == 0 && g->stride_a % 8 == 0 && g->stride_b % 8 == 0,
                "cq_gemm_x3: operand rows must be 16-byte aligned");
-    CQ_REQUIRE(g->lda >= g->K && g->ldb >= g->K && g->ldc >= g->N, "cq_gemm_x3: leading dimension too small");
+    CQ_REQUIRE((g->a_blocked ? g->lda >= g->M : g->lda >= g->K) && (g->b_blocked ? g->ldb >= g->N : g->ldb >= g->K) &&
+                   g->ldc >= g->N,
+               "cq_gemm_x3: leading dimension too small");
     CQ_REQUIRE(!g->out_h == !g->out_l, "cq_gemm_x3: out_h and out_l go together");
     CQ_REQUIRE(!g->out_h || (g->overflow && g->out_scale > 0.f), "cq_gemm_x3: split output needs overflow flags");
     CQ_REQUIRE(!g->beta_v || g->P, "cq_gemm_x3: beta_v needs P");
@@ -968,6 +1016,10 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.tri = g->tri;
     a.b_blocked = g->b_blocked;
     a.active = g->active;
+    a.a_blocked = g->a_blocked;
+    a.o_blocked = g->o_blocked;
+    CQ_REQUIRE(!g->o_blocked || g->N % 32 == 0, "cq_gemm_x3: blocked split output needs N % 32 == 0");
+    CQ_REQUIRE(!g->a_blocked || g->lda >= g->M, "cq_gemm_x3: blocked A needs lda = rows >= M");
     CQ_REQUIRE(!g->active || g->D, "cq_gemm_x3: active needs D (the pass-through value)");
     CQ_REQUIRE(!g->b_blocked || g->ldb >= g->N, "cq_gemm_x3: blocked B needs ldb = rows >= N");
     static const int variant = [] {
@@ -977,6 +1029,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         if (!e) return 2;
         return e[0] == 'r' ? 1 : e[0] == 'g' ? 0 : 2;
     }();
+    CQ_REQUIRE(variant == 2 || (!g->a_blocked && !g->o_blocked),
+               "cq_gemm_x3: blocked A / split output need the LDS-DMA 192x384 kernel");
     if (variant == 2) {
         a.tiles_n = ceil_div(g->N, XW_BN);
         a.tiles_m = ceil_div(g->M, XW_BM);

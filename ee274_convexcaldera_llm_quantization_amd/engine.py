@@ -387,6 +387,8 @@ class CalderaEngine:
                         min_err[b] = e[b]
                     if sel:
                         st.snapshot_into(best, sel)
+        if self.solver is not None:
+            self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         return self._finalize(best, st, W, Ws, gs, errors, wts)
 
     def _state_error(self, st, Ws, work, wts):

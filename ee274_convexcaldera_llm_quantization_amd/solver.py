@@ -158,6 +158,16 @@ class RankRSolver:
                 return b
         raise RuntimeError("solver buffer pool exhausted")
 
+    def release(self):
+        """Drop the large per-call work buffers (G and its halves, Y halves, blocks); the warm
+        start (X, theta) and the statistics stay."""
+        self._bufs = None
+        self._G = None
+        self._yh = self._yl = None
+        for name in ("_Gh", "_Gl", "_xt", "_xh", "_xl"):
+            if hasattr(self, name):
+                setattr(self, name, None)
+
     # ------------------------------------------------------------------ steps
     def _cholqr(self, X, *keep):
         out = self._free(X, *keep)
@@ -170,8 +180,9 @@ class RankRSolver:
         G = self._G
         Z = self._free(X, *keep)
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
-            K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE)
-            K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked)
+            K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
+            K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked,
+                      a_blocked=True)
             K.transpose_split(self._xt[0], out=Z)
         else:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
@@ -236,7 +247,8 @@ class RankRSolver:
         """Same recurrence on X^T with split-fp16 products (cq_gemm_x3); X is left intact."""
         deg = coef.shape[0]
         xt, xh, xl = self._xt, self._xh, self._xl
-        K.transpose_split(X, out=xt[0], hi=xh[0], lo=xl[0], scale=X3_SCALE)
+        # iterates' halves are K-blocked (each 32-deep step of a tile is one contiguous run)
+        K.transpose_split(X, out=xt[0], hi=xh[0], lo=xl[0], scale=X3_SCALE, blocked=True)
         fl = 2.0 * self.k * self.k * self.p * self.B
         # bytes a recurrence step moves: G halves (4 B/elem) + X^T halves + prev, cur in,
         # new out (fp32) + new halves out
@@ -246,7 +258,8 @@ class RankRSolver:
         ev = EVENT_PROBE.start(fl, nb, kn)
         K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
                   gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
-                  out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked, active=self._active)
+                  out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked, active=self._active,
+                  a_blocked=True, o_blocked=True)
         EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = 0, 1
@@ -257,7 +270,7 @@ class RankRSolver:
                       alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
                       out_h=None if last else xh[prev], out_l=None if last else xl[prev],
                       out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked,
-                      active=self._active)
+                      active=self._active, a_blocked=True, o_blocked=True)
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur = cur, prev
@@ -289,11 +302,12 @@ class RankRSolver:
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             K.pow2_scale(Y, 14, out=self._ys)
             if self.left:
-                K.split_f16(Y, self._ys, hi=self._yh, lo=self._yl)
+                K.split_f16(Y, self._ys, hi=self._yh, lo=self._yl, blocked=True)
             else:
-                K.transpose_split(Y, hi=self._yh, lo=self._yl, scale=self._ys)
+                K.transpose_split(Y, hi=self._yh, lo=self._yl, scale=self._ys, blocked=True)
             yinv = 1.0 / (self._ys * self._ys)
-            K.gemm_x3(self._yh, self._yl, self._yh, self._yl, yinv, self._G, tri=True)  # upper triangle
+            K.gemm_x3(self._yh, self._yl, self._yh, self._yl, yinv, self._G, tri=True,  # upper triangle
+                      a_blocked=True, b_blocked=True)
             self._g_upper_only = True
         elif self.left:
             K.gemm(Y, Y, tb=True, C=self._G, syrk=True)  # Y Y^T (upper tiles + mirror)

@@ -191,13 +191,16 @@ int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, i
 /* scale_out[b] = 2^(log2_target - e) with max|X[b]| in [2^(e-1), 2^e) (1 for all-zero X[b]). */
 int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target, float* scale_out,
                   void* stream);
-/* hi/lo[b] = split of X[b] (n_per values) scaled by scale_v[b] (or scale if scale_v NULL). */
+/* hi/lo[b] = split of X[b] (n_per values) scaled by scale_v[b] (or scale if scale_v NULL).
+ * blocked_ncols > 0: X[b] is (n_per / ncols) x ncols and the halves are written K-blocked
+ * (element (r, c) at (c / 32) * rows * 32 + r * 32 + c % 32; ncols % 32 == 0). */
 int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scale_v, float scale,
-                 uint16_t* hi, uint16_t* lo, void* stream);
+                 uint16_t* hi, uint16_t* lo, int64_t blocked_ncols, void* stream);
 /* Y[b] = X[b]^T (X rows x cols row-major -> Y cols x rows), and/or its split (scale_v[b], or
- * scale if scale_v is NULL). */
+ * scale if scale_v is NULL); blocked: halves K-blocked over Y's columns (rows % 32 == 0). */
 int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch, float* Y,
-                       uint16_t* hi, uint16_t* lo, float scale, const float* scale_v, void* stream);
+                       uint16_t* hi, uint16_t* lo, float scale, const float* scale_v, int blocked,
+                       void* stream);
 
 typedef struct cq_x3_args {
     int64_t M, N, K, batch;
@@ -222,6 +225,9 @@ typedef struct cq_x3_args {
     int b_blocked;                 /* B halves K-blocked (see cq_sym_split_f16); ldb = rows */
     const int* active;             /* [batch] or NULL: entries with active[b] == 0 skip the
                                       product and write C = D (and its split) unchanged */
+    int a_blocked;                 /* A halves K-blocked like b_blocked; lda = rows */
+    int o_blocked;                 /* out_h/out_l written K-blocked over C's columns (an A
+                                      operand of the next product); N % 32 == 0 */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

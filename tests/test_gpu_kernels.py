@@ -498,3 +498,46 @@ def test_q_update_x3_with_lr_matches_fp64_residual(K):
     deq = c * scale.double().view(B, 1, 1)
     e_ref = (((deq - res) ** 2) * w.double()).sum((1, 2))
     assert torch.allclose(err, e_ref, rtol=1e-4, atol=0)
+
+
+
+def _kblock(x):
+    """(B, R, K) row-major -> the K-blocked operand layout [K/32][R][32] (same storage size)."""
+    B, R, Kd = x.shape
+    return x.view(B, R, Kd // 32, 32).permute(0, 2, 1, 3).contiguous().view(B, R, Kd)
+
+
+def test_blocked_operand_layouts(K):
+    """split_f16 / transpose_split blocked outputs equal the K-blocked permutation of the
+    row-major halves; a product on blocked A and B equals the row-major product bit for bit,
+    and a blocked split output feeds the next product like a row-major one."""
+    g = torch.Generator(device=DEV).manual_seed(12)
+    Y = torch.randn(2, 224, 320, device=DEV, generator=g)
+    s = K.pow2_scale(Y, 14)
+    h, l = K.split_f16(Y, s)
+    hb, lb = K.split_f16(Y, s, blocked=True)
+    assert torch.equal(hb, _kblock(h)) and torch.equal(lb, _kblock(l))
+    X = torch.randn(2, 320, 96, device=DEV, generator=g)   # (k, p) -> X^T (p, k) halves
+    _, th, tl = K.transpose_split(X, hi=torch.empty(2, 96, 320, dtype=torch.float16, device=DEV),
+                                  lo=torch.empty(2, 96, 320, dtype=torch.float16, device=DEV), scale=64.0)
+    _, tbh, tbl = K.transpose_split(X, hi=torch.empty_like(th), lo=torch.empty_like(tl), scale=64.0, blocked=True)
+    assert torch.equal(tbh, _kblock(th)) and torch.equal(tbl, _kblock(tl))
+    inv = 1.0 / (s * s)
+    C1 = torch.empty(2, 224, 224, device=DEV)
+    C2 = torch.empty_like(C1)
+    K.gemm_x3(h, l, h, l, inv, C1)
+    K.gemm_x3(hb, lb, hb, lb, inv, C2, a_blocked=True, b_blocked=True)
+    assert torch.equal(C1, C2)
+    # blocked split output (C = X^T Y^T: 96 x 224, K = 320)
+    Yt = Y.transpose(1, 2).contiguous()          # (320, 224): B operand rows = 224
+    yth, ytl = K.split_f16(Y, s)                  # Y (224, 320) rows are K-contiguous for B
+    C3 = torch.empty(2, 96, 224, device=DEV)
+    oh = torch.empty(2, 96, 224, dtype=torch.float16, device=DEV)
+    ol = torch.empty_like(oh)
+    ohb, olb = torch.empty_like(oh), torch.empty_like(ol)
+    ovf = torch.zeros(2, dtype=torch.int32, device=DEV)
+    inv2 = 1.0 / (64.0 * s)
+    K.gemm_x3(th, tl, yth, ytl, inv2, C3, out_h=oh, out_l=ol, out_scale=4.0, overflow=ovf)
+    K.gemm_x3(tbh, tbl, yth, ytl, inv2, C3, out_h=ohb, out_l=olb, out_scale=4.0, overflow=ovf,
+              a_blocked=True, o_blocked=True)
+    assert torch.equal(ohb, _kblock(oh)) and torch.equal(olb, _kblock(ol))

@@ -43,6 +43,13 @@ for p in (192, 256, 384):
     bench(f"x3  + cheb epilogue + split p={p}", lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, P=Ct, D=Xt, alpha_v=a,
                                                                beta_v=b, gamma_v=c, out_h=Oh, out_l=Ol,
                                                                out_scale=xs, overflow=ovf, b_blocked=True), fl)
+    Xhb = Xh.view(B, p, k // 32, 32).permute(0, 2, 1, 3).contiguous().view(B, p, k)
+    Xlb = Xl.view(B, p, k // 32, 32).permute(0, 2, 1, 3).contiguous().view(B, p, k)
+    bench(f"x3  A and B K-blocked p={p}", lambda: K.gemm_x3(Xhb, Xlb, Gh, Gl, inv, Ct, b_blocked=True, a_blocked=True), fl)
+    Ctb = torch.empty_like(Ct)
+    K.gemm_x3(Xhb, Xlb, Gh, Gl, inv, Ctb, b_blocked=True, a_blocked=True)
+    K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, b_blocked=True)
+    print("   blocked-A result identical:", torch.equal(Ct, Ctb), flush=True)
     C = torch.empty(B, k, p, device=dev)
     bench(f"f32 G X ta  p={p}", lambda: K.gemm(G, X, ta=True, C=C), fl)
     K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, b_blocked=True)
