@@ -97,6 +97,10 @@ _SIGS = {
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
@@ -516,3 +520,27 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
     _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),
                               _p(packed), _p(scale), _p(err_w), _p(err_out), _p(ws), ws.numel(), _stream(dev)),
            "cq_q_update_x3")
+
+
+def absmax(X: torch.Tensor) -> torch.Tensor:
+    """(B,) fp32 max |X[b]| of a (B, ...) fp16/fp32 tensor."""
+    _require_hip(X)
+    X = X.contiguous()
+    B = X.shape[0]
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[X.dtype]
+    out = torch.empty(B, dtype=torch.float32, device=X.device)
+    _check(load().cq_absmax(dt, _p(X), X.numel() // B, B, _p(out), _stream(X.device)), "cq_absmax")
+    return out
+
+
+def residual_split(Ws, packed, qscale, bits, wmax, *, ycol=None, ycol_max=1.0, res=None, Y=None, hi=None, lo=None,
+                   thi=None, tlo=None, scale=None, sq=None):
+    """Fused LR-step residual (see include/caldera_hip.h cq_residual_split).  Ws (B, m, n)."""
+    _require_hip(Ws, packed, qscale, wmax, ycol, res, Y, hi, lo, thi, tlo, scale, sq)
+    B, m, n = Ws.shape
+    dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[Ws.dtype]
+    lib = load()
+    ws = workspace(lib.cq_residual_split_workspace(m, n, B), Ws.device) if sq is not None else None
+    _check(lib.cq_residual_split(dt, _p(Ws), _p(packed), _p(qscale), int(bits), _p(ycol), float(ycol_max), _p(wmax),
+                                 B, m, n, _p(res), _p(Y), _p(hi), _p(lo), _p(thi), _p(tlo), _p(scale), _p(sq), _p(ws),
+                                 0 if ws is None else ws.numel(), _stream(Ws.device)), "cq_residual_split")

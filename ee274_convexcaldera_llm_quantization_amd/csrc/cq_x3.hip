@@ -679,6 +679,158 @@ __global__ void q_update_finalize_kernel(const uint32_t* absmax, const double* p
     }
 }
 
+
+// ------------------------------------------------------------------ fused residual + split
+// One pass over W and the packed Q codes for the LR step (alg.py:124 res = W - Q, :211
+// Y = res * sqrt(h)): writes any of res (fp32), Y (fp32), the K-blocked split halves of Y
+// over its columns (A/B operand of Y Y^T) and over its rows (operand of U^T Y / Y^T Y), and
+// ||Y||^2 (fp64, deterministic per-tile partials).  The split scale is a per-matrix power of
+// two from the bound |Y| <= (max|W| + Q_scale) * max(ycol), so no absmax pass is needed.
+// Tile 32 rows x 64 columns per step, 256 threads (8 consecutive columns each).
+template <int DT, int BITS>
+__global__ __launch_bounds__(256) void residual_split_kernel(
+    const void* __restrict__ Ws, const uint8_t* __restrict__ qc, const float* __restrict__ qscale,
+    const float* __restrict__ ycol, const float* __restrict__ wmax, float ycmax, int64_t m, int64_t n,
+    float* __restrict__ res, float* __restrict__ Y, _Float16* __restrict__ hi, _Float16* __restrict__ lo,
+    _Float16* __restrict__ thi, _Float16* __restrict__ tlo, float* __restrict__ scale_out,
+    double* __restrict__ part) {
+    __shared__ float tile[64][33];
+    __shared__ double red[4];
+    constexpr float k = (float)((1 << (BITS - 1)) - 1);
+    const int64_t b = blockIdx.z;
+    const int64_t MN = m * n;
+    const float qs = qc ? qscale[b] : 0.f;
+    int e2 = 0;
+    {
+        const float bnd = (wmax[b] + qs) * ycmax;
+        if (bnd > 0.f && isfinite(bnd)) frexpf(bnd, &e2);
+    }
+    const float sc = ldexpf(1.f, 14 - e2);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && scale_out) scale_out[b] = sc;
+    const int t = threadIdx.x;
+    const int r = t >> 3, c8 = (t & 7) * 8;          // row in tile, first of 8 columns
+    const int64_t j0 = (int64_t)blockIdx.x * 64;
+    double acc = 0.0;
+    const int rows_per = (int)gridDim.y;
+    for (int64_t i0 = (int64_t)blockIdx.y * 32; i0 < m; i0 += (int64_t)rows_per * 32) {
+        const int64_t i = i0 + r, j = j0 + c8;
+        const int64_t e = b * MN + i * n + j;
+        float w[8];
+        if (DT == CQ_F16) {
+            const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Ws) + e);
+            const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[u] = (float)hv[u];
+        } else {
+            const float4 f0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Ws) + e);
+            const float4 f1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Ws) + e + 4);
+            w[0] = f0.x; w[1] = f0.y; w[2] = f0.z; w[3] = f0.w; w[4] = f1.x; w[5] = f1.y; w[6] = f1.z; w[7] = f1.w;
+        }
+        float q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = 0.f;
+        if (qc) {
+            const int64_t eq = e;  // element index (codes follow the row-major element order)
+            if (BITS == 2) {
+                const uint16_t two = *reinterpret_cast<const uint16_t*>(qc + eq / 4);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t byte = (u < 4) ? (two & 0xffu) : (two >> 8);
+                    const int sh = 6 - 2 * (u & 3);
+                    q[u] = dequant((float)((int)((byte >> sh) & 3u) - 1), k, qs);
+                }
+            } else if (BITS == 4) {
+                const uint32_t four = *reinterpret_cast<const uint32_t*>(qc + eq / 2);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t byte = (four >> (8 * (u >> 1))) & 0xffu;
+                    const uint32_t v = (u & 1) ? (byte & 15u) : (byte >> 4);
+                    q[u] = dequant((float)((int)v - 7), k, qs);
+                }
+            } else if (BITS == 8) {
+                const int8_t* cp = reinterpret_cast<const int8_t*>(qc) + eq;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = dequant((float)cp[u], k, qs);
+            } else {
+                const int16_t* cp = reinterpret_cast<const int16_t*>(qc) + eq;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = dequant((float)cp[u], k, qs);
+            }
+        }
+        float rv[8], yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = w[u] - q[u];
+            yv[u] = ycol ? rv[u] * ycol[j + u] : rv[u];
+            acc += (double)yv[u] * (double)yv[u];
+        }
+        if (res) {
+            *reinterpret_cast<float4*>(res + e) = make_float4(rv[0], rv[1], rv[2], rv[3]);
+            *reinterpret_cast<float4*>(res + e + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
+        }
+        if (Y) {
+            *reinterpret_cast<float4*>(Y + e) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+            *reinterpret_cast<float4*>(Y + e + 4) = make_float4(yv[4], yv[5], yv[6], yv[7]);
+        }
+        if (hi) {  // blocked over columns: (j / 32) * m * 32 + i * 32 + j % 32
+            _Float16 h8[8], l8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float xs = yv[u] * sc;
+                h8[u] = (_Float16)xs;
+                l8[u] = (_Float16)(xs - (float)h8[u]);
+            }
+            const int64_t o = b * MN + (j >> 5) * m * 32 + i * 32 + (j & 31);
+            *reinterpret_cast<uint4*>(hi + o) = *reinterpret_cast<const uint4*>(h8);
+            *reinterpret_cast<uint4*>(lo + o) = *reinterpret_cast<const uint4*>(l8);
+        }
+        if (thi) {  // blocked over rows (Y^T as a row-major n x m operand): (i / 32) * n * 32 + j * 32 + i % 32
+#pragma unroll
+            for (int u = 0; u < 8; ++u) tile[c8 + u][r] = yv[u] * sc;
+            __syncthreads();
+            const int jc = t >> 2, r8 = (t & 3) * 8;   // column of the tile, 8 consecutive rows
+            _Float16 h8[8], l8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float xs = tile[jc][r8 + u];
+                h8[u] = (_Float16)xs;
+                l8[u] = (_Float16)(xs - (float)h8[u]);
+            }
+            const int64_t o = b * MN + (i0 >> 5) * n * 32 + (j0 + jc) * 32 + r8;
+            *reinterpret_cast<uint4*>(thi + o) = *reinterpret_cast<const uint4*>(h8);
+            *reinterpret_cast<uint4*>(tlo + o) = *reinterpret_cast<const uint4*>(l8);
+            __syncthreads();
+        }
+    }
+    if (part) {
+        acc = wave_sum(acc);
+        if ((t & 63) == 0) red[t >> 6] = acc;
+        __syncthreads();
+        if (t == 0) part[(b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    }
+}
+
+__global__ void sum_tile_parts_kernel(const double* __restrict__ part, int64_t nparts, double* __restrict__ out) {
+    const int64_t b = blockIdx.x;
+    double s = 0.0;
+    for (int64_t t = threadIdx.x; t < nparts; t += 64) s += part[b * nparts + t];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[b] = s;
+}
+
+template <int DT>
+__global__ void absmax_dt_kernel(const void* __restrict__ X, int64_t n_per, uint32_t* __restrict__ out) {
+    const int64_t b = blockIdx.y;
+    uint32_t mx = 0;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n_per; q += (int64_t)gridDim.x * blockDim.x) {
+        const float v = DT == CQ_F16 ? (float)reinterpret_cast<const _Float16*>(X)[b * n_per + q]
+                                     : reinterpret_cast<const float*>(X)[b * n_per + q];
+        mx = max(mx, abs_bits(v));
+    }
+    mx = wave_max_u32(mx);
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(out + b, mx);
+}
+
 // ------------------------------------------------------------------ split / transpose helpers
 
 // Per-batch power-of-two scale s = 2^(14 - ceil(log2 max_i G_ii)) for a PSD G (|G_ij| <=
@@ -981,6 +1133,54 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
 #undef CQ_QU
     q_update_finalize_kernel<<<(unsigned)batch, 64, 0, s>>>(q.absmax, q.part, tiles, batch, eps, scale_out, err_out);
     return check_launch("cq_q_update_x3");
+}
+
+
+int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out, void* stream) {
+    CQ_REQUIRE(X && out && n_per > 0 && batch > 0 && batch < 65536, "cq_absmax: bad args");
+    CQ_REQUIRE(dtype == CQ_F16 || dtype == CQ_F32, "cq_absmax: dtype must be f16/f32");
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(out, 0, batch * sizeof(float), s) != hipSuccess) return set_error(CQ_EHIP, "cq_absmax: memset");
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_per, 256), std::max<int64_t>(1, 4096 / batch)));
+    if (dtype == CQ_F16) absmax_dt_kernel<CQ_F16><<<dim3(gx, (unsigned)batch), 256, 0, s>>>(X, n_per, reinterpret_cast<uint32_t*>(out));
+    else absmax_dt_kernel<CQ_F32><<<dim3(gx, (unsigned)batch), 256, 0, s>>>(X, n_per, reinterpret_cast<uint32_t*>(out));
+    return check_launch("cq_absmax");  // max |x| bits are the float's bits: out reads as float
+}
+
+size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch) {
+    const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(m / 32, 16));
+    return (size_t)batch * gy * ceil_div(n, 64) * sizeof(double);
+}
+
+int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,
+                      const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m, int64_t n,
+                      float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo, uint16_t* thi, uint16_t* tlo,
+                      float* scale_out, double* sq_out, void* ws, size_t ws_bytes, void* stream) {
+    CQ_REQUIRE(Ws && wmax && batch > 0 && batch < 65536 && m > 0 && n > 0, "cq_residual_split: bad args");
+    CQ_REQUIRE(m % 32 == 0 && n % 64 == 0, "cq_residual_split: m % 32 and n % 64 must be 0");
+    CQ_REQUIRE(!packed || qscale, "cq_residual_split: scale required with codes");
+    CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16, "Bit-width not supported!");
+    CQ_REQUIRE(!hi == !lo && !thi == !tlo, "cq_residual_split: halves go in pairs");
+    CQ_REQUIRE((!hi && !thi) || scale_out, "cq_residual_split: halves need scale_out");
+    CQ_REQUIRE(!sq_out || (ws && ws_bytes >= cq_residual_split_workspace(m, n, batch)), "cq_residual_split: workspace too small");
+    const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(m / 32, 16));
+    dim3 grid((unsigned)(n / 64), (unsigned)gy, (unsigned)batch);
+    hipStream_t s = as_stream(stream);
+    double* part = sq_out ? reinterpret_cast<double*>(ws) : nullptr;
+    auto h = [](uint16_t* p) { return reinterpret_cast<_Float16*>(p); };
+#define CQ_RS(DT, B) residual_split_kernel<DT, B><<<grid, 256, 0, s>>>(Ws, packed, qscale, ycol, wmax, ycol_max, m, n, \
+        res_out, Y_out, h(hi), h(lo), h(thi), h(tlo), scale_out, part)
+    const int bsel = packed ? bits : 2;
+    if (dtype == CQ_F16) {
+        switch (bsel) { case 2: CQ_RS(CQ_F16, 2); break; case 4: CQ_RS(CQ_F16, 4); break;
+                        case 8: CQ_RS(CQ_F16, 8); break; default: CQ_RS(CQ_F16, 16); }
+    } else {
+        switch (bsel) { case 2: CQ_RS(CQ_F32, 2); break; case 4: CQ_RS(CQ_F32, 4); break;
+                        case 8: CQ_RS(CQ_F32, 8); break; default: CQ_RS(CQ_F32, 16); }
+    }
+#undef CQ_RS
+    if (sq_out) sum_tile_parts_kernel<<<(unsigned)batch, 64, 0, s>>>(part, gy * (n / 64), sq_out);
+    return check_launch("cq_residual_split");
 }
 
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {

@@ -80,6 +80,7 @@ class _Weights:
         if not p.activation_aware_LR:
             self.err = h
             self.ycol = None
+            self.ycol_max = 1.0
             self.rinv = None
             self.lplr = h * h
             self.identity = False
@@ -97,6 +98,7 @@ class _Weights:
         self.err = herr
         sq = torch.sqrt(lam)
         self.ycol = None if self.identity else sq
+        self.ycol_max = 1.0 if self.identity else float(sq.max().item())
         self.rinv = None if self.identity else 1.0 / sq
         self.lplr = None if self.identity else lam  # ||Y - L (R*ycol)||^2 uses unit weights
 
@@ -204,15 +206,30 @@ class CalderaEngine:
         dev = Ws.device
         quantized = p.L_bits < 16 or p.R_bits < 16
         weighted = p.activation_aware_LR and wts.ycol is not None
-        K.build_residual(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, p.Q_bits,
-                         wts.ycol, Y=Y if weighted else None, res=res)
-        Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
-        Y = Ysrc
         if self.solver is None:
             self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
                                       filter_precision=self.filter_precision, **self.solver_kwargs)
         sv = self.solver
-        vecs, theta = yield from sv.solve_iter(Ysrc)
+        y_split = None
+        ysq = None
+        if sv.x3 and not sv.direct and m % 32 == 0 and n % 64 == 0 and st.q_packed:
+            # one pass: res / Y (fp32), the solver's Gram operand halves and ||Y||^2
+            if self._yh is None:
+                self._yh = torch.empty((B, m, n), dtype=torch.float16, device=dev)
+                self._yl = torch.empty_like(self._yh)
+                self._ys = torch.empty(B, dtype=torch.float32, device=dev)
+            ysq = torch.empty(B, dtype=torch.float64, device=dev)
+            halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)
+            K.residual_split(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, p.Q_bits, self._wmax,
+                             ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
+                             res=res, Y=Y if weighted else None, scale=self._ys, sq=ysq, **halves)
+            y_split = (self._yh, self._yl, self._ys)
+        else:
+            K.build_residual(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, p.Q_bits,
+                             wts.ycol, Y=Y if weighted else None, res=res)
+        Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
+        Y = Ysrc
+        vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split)
         r = sv.r
         S = torch.sqrt(theta.clamp_min(0.0))  # singular values (fp64)
         S32 = S.float()
@@ -255,8 +272,8 @@ class CalderaEngine:
             # weights, so the weighted residual is (I - U U^T) Y and, by Pythagoras,
             # sum_j h_j (res - L R)_ij^2 = ||Y||^2 - ||U^T Y||^2 = ||Y||^2 - sum_j h_j R_ij^2
             # (two fp64 reductions instead of an m x n x r product; U orthonormal to ~1e-7)
-            return (K.weighted_sqsum(Ysrc, None, n) -
-                    K.weighted_sqsum(R, wts.err if wts.ycol is not None else None, n))
+            ysq = K.weighted_sqsum(Ysrc, None, n) if ysq is None else ysq
+            return ysq - K.weighted_sqsum(R, wts.err if wts.ycol is not None else None, n)
         err = torch.empty(B, dtype=torch.float64, device=dev)
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
@@ -350,6 +367,8 @@ class CalderaEngine:
             raise NotImplementedError("caldera-mi355x: W.shape[1] must be a multiple of 4")
         gs, Ws = K.rms_scale(W, scale_W)
         wts = _Weights(h, n, p, dev)
+        self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
+        self._yh = self._yl = self._ys = None
         den = K.weighted_sqsum(Ws, wts.err, n)
         r = p.rank
         st = BatchState(B, m, n, r, p, dev)
@@ -389,6 +408,7 @@ class CalderaEngine:
                         st.snapshot_into(best, sel)
         if self.solver is not None:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
+        self._yh = self._yl = None
         return self._finalize(best, st, W, Ws, gs, errors, wts)
 
     def _state_error(self, st, Ws, work, wts):

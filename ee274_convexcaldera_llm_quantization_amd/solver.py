@@ -283,8 +283,10 @@ class RankRSolver:
         """Y (B, m, n) fp32 -> (vecs (B, k, r), theta (B, r) fp64 eigenvalues of G, descending)."""
         return run_to_end(self.solve_iter(Y, warm))
 
-    def solve_iter(self, Y: torch.Tensor, warm: bool = True):
-        """Generator form of solve(): yields before each host synchronisation (overlap.py)."""
+    def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None):
+        """Generator form of solve(): yields before each host synchronisation (overlap.py).
+        y_split: optional (hi, lo, scale) K-blocked split-fp16 halves of the Gram operand (Y
+        for m <= n, Y^T otherwise) already produced by the caller (cq_residual_split)."""
         B, k, p = self.B, self.k, self.p
         dev = Y.device
         self.stats.calls += 1
@@ -296,17 +298,21 @@ class RankRSolver:
         self._g_upper_only = False
         if self.x3 and (self.n if self.left else self.m) % 32 == 0:
             # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two
-            if self._yh is None:
-                self._yh = torch.empty((B, k, Y.shape[1] + Y.shape[2] - k), dtype=torch.float16, device=dev)
-                self._yl = torch.empty_like(self._yh)
-                self._ys = torch.empty(B, dtype=torch.float32, device=dev)
-            K.pow2_scale(Y, 14, out=self._ys)
-            if self.left:
-                K.split_f16(Y, self._ys, hi=self._yh, lo=self._yl, blocked=True)
+            if y_split is not None:
+                yh, yl, ys = y_split
             else:
-                K.transpose_split(Y, hi=self._yh, lo=self._yl, scale=self._ys, blocked=True)
-            yinv = 1.0 / (self._ys * self._ys)
-            K.gemm_x3(self._yh, self._yl, self._yh, self._yl, yinv, self._G, tri=True,  # upper triangle
+                if self._yh is None:
+                    self._yh = torch.empty((B, k, Y.shape[1] + Y.shape[2] - k), dtype=torch.float16, device=dev)
+                    self._yl = torch.empty_like(self._yh)
+                    self._ys = torch.empty(B, dtype=torch.float32, device=dev)
+                yh, yl, ys = self._yh, self._yl, self._ys
+                K.pow2_scale(Y, 14, out=ys)
+                if self.left:
+                    K.split_f16(Y, ys, hi=yh, lo=yl, blocked=True)
+                else:
+                    K.transpose_split(Y, hi=yh, lo=yl, scale=ys, blocked=True)
+            yinv = 1.0 / (ys * ys)
+            K.gemm_x3(yh, yl, yh, yl, yinv, self._G, tri=True,  # upper triangle
                       a_blocked=True, b_blocked=True)
             self._g_upper_only = True
         elif self.left:

@@ -232,6 +232,23 @@ typedef struct cq_x3_args {
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
 
+/* out[b] = max |X[b]| (n_per values, fp16 or fp32), NaN sorting above inf. */
+int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out, void* stream);
+
+/* Fused residual for the LR step.  Replaces alg.py:124 (residual = W - Q) and :211
+ * (Y = residual @ H_sqrt for diagonal H), plus the operand preparation of the solver: one
+ * pass over W and the packed codes writes any of res (fp32), Y = res * ycol (fp32), the
+ * K-blocked split halves of Y over its columns (hi/lo, layout of cq_split_f16 blocked) and
+ * over its rows (thi/tlo: Y^T as an n x m operand, blocked), and sq_out[b] = ||Y||_F^2
+ * (fp64).  The halves' scale (scale_out[b]) is the power of two for the bound
+ * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|.  m % 32 == 0, n % 64 == 0. */
+size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch);
+int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,
+                      const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m,
+                      int64_t n, float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo,
+                      uint16_t* thi, uint16_t* tlo, float* scale_out, double* sq_out, void* ws,
+                      size_t ws_bytes, void* stream);
+
 /* Fused Q update.  Replaces alg.py:253-283 (maybe_update_Q / update_Q_non_data_aware:
  * res = W - L@R, quantize_matrix) + quantization.py:244-269 (whole-matrix uniform quantise):
  * res is recomputed per tile from the split-fp16 halves of L (m x r) and R^T (n x r,

@@ -541,3 +541,43 @@ def test_blocked_operand_layouts(K):
     K.gemm_x3(tbh, tbl, yth, ytl, inv2, C3, out_h=ohb, out_l=olb, out_scale=4.0, overflow=ovf,
               a_blocked=True, o_blocked=True)
     assert torch.equal(ohb, _kblock(oh)) and torch.equal(olb, _kblock(ol))
+
+
+@pytest.mark.parametrize("bits,weighted", [(2, False), (4, True), (8, False)])
+def test_residual_split_matches_unfused(K, bits, weighted):
+    """cq_residual_split == build_residual + split (both blocked layouts) at the kernel's
+    power-of-two scale, which bounds max|Y|; ||Y||^2 to fp64 rounding."""
+    g = torch.Generator(device=DEV).manual_seed(bits)
+    B, m, n = 2, 96, 320
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.5).half()
+    q = K.quantize_uniform(W.float().view(B, -1) * 0.9, m * n, bits, codes=True)
+    if bits <= 4:
+        codes = K.quantize_uniform(W.float().view(B, -1) * 0.9, m * n, bits, packed=True)["packed"]
+    else:
+        codes = q["codes"].view(B, -1).contiguous()
+    qs = q["scale"].view(B).contiguous()
+    ycol = (torch.rand(n, device=DEV, generator=g) + 0.5) if weighted else None
+    wmax = K.absmax(W)
+    assert torch.equal(wmax, W.float().abs().amax((1, 2)))
+    res_ref = torch.empty(B, m, n, device=DEV)
+    Y_ref = torch.empty(B, m, n, device=DEV) if weighted else None
+    K.build_residual(W, codes, qs, bits, ycol, Y=Y_ref, res=res_ref)
+    Ysrc = Y_ref if weighted else res_ref
+    res = torch.empty_like(res_ref)
+    Y = torch.empty_like(res_ref) if weighted else None
+    hi = torch.empty(B, m, n, dtype=torch.float16, device=DEV)
+    lo, thi, tlo = torch.empty_like(hi), torch.empty_like(hi), torch.empty_like(hi)
+    sc = torch.empty(B, device=DEV)
+    sq = torch.empty(B, dtype=torch.float64, device=DEV)
+    K.residual_split(W, codes, qs, bits, wmax, ycol=ycol, ycol_max=float(ycol.max()) if weighted else 1.0,
+                     res=res, Y=Y, hi=hi, lo=lo, thi=thi, tlo=tlo, scale=sc, sq=sq)
+    assert torch.equal(res, res_ref)
+    if weighted:
+        assert torch.equal(Y, Y_ref)
+    assert (Ysrc.abs().amax((1, 2)) * sc < 2.0 ** 14).all()
+    h_ref, l_ref = K.split_f16(Ysrc.contiguous(), sc, blocked=True)
+    assert torch.equal(hi, h_ref) and torch.equal(lo, l_ref)
+    th_ref, tl_ref = K.split_f16(Ysrc.transpose(1, 2).contiguous(), sc, blocked=True)
+    # the transposed halves are (B, n, m) operands stored in (B, m, n)-shaped buffers
+    assert torch.equal(thi.view(B, n, m), th_ref) and torch.equal(tlo.view(B, n, m), tl_ref)
+    assert torch.allclose(sq, (Ysrc.double() ** 2).sum((1, 2)), rtol=1e-12, atol=0)
