@@ -73,6 +73,15 @@ _SIGS = {
     "cq_quantize_uniform_known_max": (c_int, [c_vp, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_unpack_codes": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "cq_quantize_nf_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_quantize_nf": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
+                               c_vp, c_size, c_vp]),
+    "cq_dequant_nf": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "cq_bbint_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_bbint_stats": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_bbint_emit": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_vp, c_vp, c_size, c_vp]),
+    "cq_dequant_bbint": (c_int, [c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cq_dequant_uniform": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_build_residual": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp,
                                   c_vp, c_vp]),
@@ -248,6 +257,82 @@ def unpack_codes(packed: torch.Tensor, numel: int, bits: int) -> torch.Tensor:
     _check(load().cq_unpack_codes(_p(packed), B, numel, bits, _p(codes), _stream(packed.device)),
            "cq_unpack_codes")
     return codes
+
+
+def quantize_nf(x: torch.Tensor, block_size: int, bits: int, eps: float = 1e-8, *, idx=True, deq=True,
+                err_w=None, err_ncols=1, err_out=None):
+    """NF4 / NF2 (quantization.py:39-91, :270-279).  x (B, numel) fp32 contiguous ->
+    dict(idx (B, numel) uint8, deq (B, numel) fp32, scale (B, numel // block_size) fp32)."""
+    _require_hip(x, err_w, err_out)
+    assert x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 2
+    B, numel = x.shape
+    dev = x.device
+    out = {"idx": torch.empty((B, numel), dtype=torch.uint8, device=dev) if idx else None,
+           "deq": torch.empty((B, numel), dtype=torch.float32, device=dev) if deq else None,
+           "scale": torch.empty((B, numel // block_size), dtype=torch.float32, device=dev)}
+    lib = load()
+    ws = workspace(lib.cq_quantize_nf_workspace(B, numel, block_size), dev)
+    _check(lib.cq_quantize_nf(_p(x), B, numel, block_size, bits, eps, _p(out["idx"]), _p(out["deq"]),
+                              _p(out["scale"]), _p(err_w), err_ncols, _p(err_out), _p(ws), ws.numel(),
+                              _stream(dev)), "cq_quantize_nf")
+    return out
+
+
+def dequantize_nf(idx: torch.Tensor, scale: torch.Tensor, bits: int) -> torch.Tensor:
+    """level[idx] * scale[blk] (quantization.py:87-91); idx uint8, scale (nblocks,) fp32."""
+    _require_hip(idx, scale)
+    total = idx.numel()
+    out = torch.empty(total, dtype=torch.float32, device=idx.device)
+    _check(load().cq_dequant_nf(_p(idx), _p(scale), total, total // scale.numel(), bits, _p(out),
+                                _stream(idx.device)), "cq_dequant_nf")
+    return out
+
+
+def quantize_bbint(x: torch.Tensor, block_size: int, bits: int, eps: float = 1e-8, *, packed=True, deq=True,
+                   outliers=True, err_w=None, err_ncols=1, err_out=None):
+    """bbint4 / bbint2 (quantization.py:107-243).  x (B, numel) fp32 contiguous -> dict(packed
+    (B, numel*bits/8) uint8, deq (B, numel), bmin / bscale (B, nblk), n_out [B] (host ints),
+    vals (sum n_out,) fp32, idx (sum n_out, 2) int64 — matrix b's rows follow matrix b-1's).
+    One host synchronisation (the outlier count sizes the list)."""
+    _require_hip(x, err_w, err_out)
+    assert x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 2
+    B, numel = x.shape
+    dev = x.device
+    nblk = numel // block_size
+    lib = load()
+    nws = lib.cq_bbint_workspace(B, numel, block_size)
+    if nws == 0:
+        raise ValueError(f"bbint: numel {numel} is not divisible by block size {block_size}")
+    ws = workspace(nws, dev)
+    bmin = torch.empty((B, nblk), dtype=torch.float32, device=dev)
+    bscale = torch.empty((B, nblk), dtype=torch.float32, device=dev)
+    n_out = torch.empty(B, dtype=torch.int64, device=dev)
+    st = _stream(dev)
+    _check(lib.cq_bbint_stats(_p(x), B, numel, block_size, bits, eps, _p(bmin), _p(bscale), _p(n_out), _p(ws),
+                              ws.numel(), st), "cq_bbint_stats")
+    counts = [int(v) for v in n_out.tolist()] if outliers else [0] * B
+    tot = sum(counts)
+    vals = torch.empty(tot, dtype=torch.float32, device=dev) if outliers else None
+    oidx = torch.empty((tot, 2), dtype=torch.int64, device=dev) if outliers else None
+    pk = torch.empty((B, numel * bits // 8), dtype=torch.uint8, device=dev) if packed else None
+    dq = torch.empty((B, numel), dtype=torch.float32, device=dev) if deq else None
+    _check(lib.cq_bbint_emit(_p(x), B, numel, block_size, bits, _p(bmin), _p(bscale), _p(pk), _p(dq),
+                             _p(vals) if tot else None, _p(oidx) if tot else None, _p(err_w), err_ncols,
+                             _p(err_out), _p(ws), ws.numel(), st), "cq_bbint_emit")
+    return {"packed": pk, "deq": dq, "bmin": bmin, "bscale": bscale, "n_out": counts, "vals": vals, "idx": oidx}
+
+
+def dequantize_bbint(packed: torch.Tensor, bits: int, bmin: torch.Tensor, bscale: torch.Tensor,
+                     vals: torch.Tensor | None, idx: torch.Tensor | None, block_size: int) -> torch.Tensor:
+    """u * scale + min per block, outliers scattered back (quantization.py:157-172, :224-243)."""
+    _require_hip(packed, bmin, bscale, vals, idx)
+    total = packed.numel() * 8 // bits
+    out = torch.empty(total, dtype=torch.float32, device=packed.device)
+    k = 0 if vals is None else vals.numel()
+    _check(load().cq_dequant_bbint(_p(packed), bits, _p(bmin), _p(bscale), total, block_size,
+                                   _p(vals) if k else None, _p(idx.contiguous()) if k else None, k, _p(out),
+                                   _stream(packed.device)), "cq_dequant_bbint")
+    return out
 
 
 def build_residual(Ws, qcodes, qscale, bits, ycol, Y=None, res=None):

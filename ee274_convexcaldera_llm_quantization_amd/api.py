@@ -14,7 +14,8 @@ from .overlap import run_interleaved
 
 
 def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
-    """Return diag(H) if H is diagonal, else raise (dense H is not on the MI355X path yet)."""
+    """diag(H) when H is a diagonal matrix (what main.py:163-165 passes: diag_embed of the
+    per-channel Hessian) or already a 1-D diagonal; otherwise H itself (dense path)."""
     if H.dim() == 1:
         if H.shape[0] != n:
             raise ValueError(f"H diagonal has length {H.shape[0]}, expected {n}")
@@ -24,8 +25,7 @@ def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
     d = torch.diagonal(H)
     off = torch.count_nonzero(H) - torch.count_nonzero(d)
     if int(off.item()) != 0:
-        raise NotImplementedError("caldera-mi355x: only diagonal H (None, identity or diag_embed(h), "
-                                  "as every reference caller passes) is supported on MI355X")
+        return H.contiguous()
     return d.contiguous()
 
 
@@ -63,7 +63,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
     if W.dtype not in (torch.float16, torch.float32):
         W = W.float()
     B, m, n = W.shape
-    h = None if H is None else _diag_of(H.to(comp).float(), n)
+    h = None if H is None else _diag_of(H.to(comp).float(), n)  # (n,) diagonal or (n, n) dense
     params = EngineParams.from_caldera_params(quant_params)
     if streams is None:
         streams = 1

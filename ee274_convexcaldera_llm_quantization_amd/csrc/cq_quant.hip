@@ -329,10 +329,10 @@ __global__ __launch_bounds__(kThreads) void build_residual_kernel(
     const void* __restrict__ Ws, const uint8_t* __restrict__ qc, const float* __restrict__ qscale,
     const float* __restrict__ ycol, int64_t m, int64_t n, float* __restrict__ Y,
     float* __restrict__ res) {
-    constexpr float k = (float)((1 << (BITS - 1)) - 1);
+    constexpr float k = BITS == 32 ? 1.f : (float)((1 << (BITS - 1)) - 1);
     const int64_t b = blockIdx.y;
     const int64_t numel = m * n;
-    const float s = qc ? qscale[b] : 0.f;
+    const float s = (qc && qscale) ? qscale[b] : 0.f;
     const int64_t ngroups = numel / 4;  // n % 4 == 0 guaranteed by caller
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     for (int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x; g < ngroups; g += stride) {
@@ -362,6 +362,9 @@ __global__ __launch_bounds__(kThreads) void build_residual_kernel(
                 q[1] = dequant((float)((int)(v0 & 15u) - 7), k, s);
                 q[2] = dequant((float)((int)(v1 >> 4) - 7), k, s);
                 q[3] = dequant((float)((int)(v1 & 15u) - 7), k, s);
+            } else if (BITS == 32) {  // dense fp32 Q (codebook methods)
+                const float4 f = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(qc) + b * numel)[g];
+                q[0] = f.x; q[1] = f.y; q[2] = f.z; q[3] = f.w;
             } else if (BITS == 8) {
                 const char4 c = reinterpret_cast<const char4*>(qc + b * numel)[g];
                 q[0] = dequant((float)c.x, k, s); q[1] = dequant((float)c.y, k, s);
@@ -585,8 +588,8 @@ int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const fl
                       float* res_out, void* stream) {
     CQ_REQUIRE(Ws && batch > 0 && m > 0 && n > 0 && (Y || res_out), "cq_build_residual: bad args");
     CQ_REQUIRE(n % 4 == 0, "cq_build_residual: n %% 4 != 0");
-    CQ_REQUIRE(!packed || scale, "cq_build_residual: scale required with codes");
-    CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16, "Bit-width not supported!");
+    CQ_REQUIRE(!packed || scale || bits == 32, "cq_build_residual: scale required with codes");
+    CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16 || bits == 32, "Bit-width not supported!");
     const int g = grid_for(m * n, batch);
     dim3 grid(g, batch);
     hipStream_t s = as_stream(stream);
@@ -594,10 +597,10 @@ int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const fl
     const int bsel = packed ? bits : 2;
     if (dtype == CQ_F16) {
         switch (bsel) { case 2: CQ_BR(CQ_F16, 2); break; case 4: CQ_BR(CQ_F16, 4); break;
-                        case 8: CQ_BR(CQ_F16, 8); break; default: CQ_BR(CQ_F16, 16); }
+                        case 8: CQ_BR(CQ_F16, 8); break; case 32: CQ_BR(CQ_F16, 32); break; default: CQ_BR(CQ_F16, 16); }
     } else {
         switch (bsel) { case 2: CQ_BR(CQ_F32, 2); break; case 4: CQ_BR(CQ_F32, 4); break;
-                        case 8: CQ_BR(CQ_F32, 8); break; default: CQ_BR(CQ_F32, 16); }
+                        case 8: CQ_BR(CQ_F32, 8); break; case 32: CQ_BR(CQ_F32, 32); break; default: CQ_BR(CQ_F32, 16); }
     }
 #undef CQ_BR
     return check_launch("cq_build_residual");

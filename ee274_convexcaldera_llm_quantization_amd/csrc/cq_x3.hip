@@ -696,7 +696,7 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
     double* __restrict__ part) {
     __shared__ float tile[64][33];
     __shared__ double red[4];
-    constexpr float k = (float)((1 << (BITS - 1)) - 1);
+    constexpr float k = BITS == 32 ? 1.f : (float)((1 << (BITS - 1)) - 1);
     const int64_t b = blockIdx.z;
     const int64_t MN = m * n;
     const float qs = qc ? qscale[b] : 0.f;
@@ -751,6 +751,10 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
                 const int8_t* cp = reinterpret_cast<const int8_t*>(qc) + eq;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) q[u] = dequant((float)cp[u], k, qs);
+            } else if (BITS == 32) {  // dense fp32 Q (codebook methods); qscale = bound on |Q|
+                const float4 f0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(qc) + eq);
+                const float4 f1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(qc) + eq + 4);
+                q[0] = f0.x; q[1] = f0.y; q[2] = f0.z; q[3] = f0.w; q[4] = f1.x; q[5] = f1.y; q[6] = f1.z; q[7] = f1.w;
             } else {
                 const int16_t* cp = reinterpret_cast<const int16_t*>(qc) + eq;
 #pragma unroll
@@ -1159,7 +1163,7 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     CQ_REQUIRE(Ws && wmax && batch > 0 && batch < 65536 && m > 0 && n > 0, "cq_residual_split: bad args");
     CQ_REQUIRE(m % 32 == 0 && n % 64 == 0, "cq_residual_split: m % 32 and n % 64 must be 0");
     CQ_REQUIRE(!packed || qscale, "cq_residual_split: scale required with codes");
-    CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16, "Bit-width not supported!");
+    CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16 || bits == 32, "Bit-width not supported!");
     CQ_REQUIRE(!hi == !lo && !thi == !tlo, "cq_residual_split: halves go in pairs");
     CQ_REQUIRE((!hi && !thi) || scale_out, "cq_residual_split: halves need scale_out");
     CQ_REQUIRE(!sq_out || (ws && ws_bytes >= cq_residual_split_workspace(m, n, batch)), "cq_residual_split: workspace too small");
@@ -1173,10 +1177,10 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     const int bsel = packed ? bits : 2;
     if (dtype == CQ_F16) {
         switch (bsel) { case 2: CQ_RS(CQ_F16, 2); break; case 4: CQ_RS(CQ_F16, 4); break;
-                        case 8: CQ_RS(CQ_F16, 8); break; default: CQ_RS(CQ_F16, 16); }
+                        case 8: CQ_RS(CQ_F16, 8); break; case 32: CQ_RS(CQ_F16, 32); break; default: CQ_RS(CQ_F16, 16); }
     } else {
         switch (bsel) { case 2: CQ_RS(CQ_F32, 2); break; case 4: CQ_RS(CQ_F32, 4); break;
-                        case 8: CQ_RS(CQ_F32, 8); break; default: CQ_RS(CQ_F32, 16); }
+                        case 8: CQ_RS(CQ_F32, 8); break; case 32: CQ_RS(CQ_F32, 32); break; default: CQ_RS(CQ_F32, 16); }
     }
 #undef CQ_RS
     if (sq_out) sum_tile_parts_kernel<<<(unsigned)batch, 64, 0, s>>>(part, gy * (n / 64), sq_out);

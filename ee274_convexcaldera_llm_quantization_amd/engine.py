@@ -24,8 +24,9 @@ from dataclasses import dataclass, field
 import torch
 
 from . import _lib as K
+from . import qlog
 from .overlap import run_to_end
-from .solver import RankRSolver
+from .solver import RandSVD, RankRSolver
 
 
 @dataclass
@@ -72,8 +73,13 @@ class _Weights:
     lplr  : weights of ||(res - L R) H_sqrt||^2 (alg.py:182): ycol^2 (aware) / h^2 (not)
     """
 
+    dense = False
+
     def __init__(self, h: torch.Tensor | None, n: int, p: EngineParams, dev):
         f32 = torch.float32
+        if h is not None and h.dim() == 2:
+            self._init_dense(h.to(device=dev, dtype=f32), n, p, dev)
+            return
         if h is None:
             h = torch.ones(n, dtype=f32, device=dev)
         h = h.to(device=dev, dtype=f32)
@@ -103,12 +109,62 @@ class _Weights:
         self.lplr = None if self.identity else lam  # ||Y - L (R*ycol)||^2 uses unit weights
 
 
+    def _init_dense(self, H, n, p: EngineParams, dev):
+        """Non-diagonal H (alg.py:44-68).  H's eigendecomposition is a one-off setup step
+        (torch.linalg.eigh on the device, i.e. rocSOLVER; the reference calls
+        torch.linalg.eigh too); everything per iteration is GEMMs in libcaldera_hip.so:
+
+        data-aware: Hs = (H + H^T)/2 = V diag(lam) V^T, lam shifted by sigma_reg - lam_min
+          when lam_min < sigma_reg (:59-64).  H_sqrt V = V diag(sqrt lam) =: Vs, so
+          Y = res @ H_sqrt @ V = res @ Vs (:211), R = R~ diag(1/sqrt lam) V^T = R~ @ Vinv^T
+          with Vinv = V diag(1/sqrt lam) (:219-225), (R H_sqrt)(R H_sqrt)^T = (R Vs)(R Vs)^T
+          for the LPLR normal equations (:162-169) and ||X H_sqrt||^2 = ||X Vs||^2 (:182).
+        not data-aware: H_sqrt = H itself (:47-49); the LPLR error ||X H||^2 uses H as given.
+        error (:286-302): tr(E H E^T) = sum_k lam_k ||E v_k||^2 over the eigenpairs of the
+          symmetrised H (shifted for data-aware, as the reference reassigns H)."""
+        self.dense = True
+        self.identity = False
+        self.ycol = self.rinv = self.lplr = None
+        self.err = None
+        self.ycol_max = 1.0
+        Hs = (H + H.t()) * 0.5
+        lam, V = torch.linalg.eigh(Hs)
+        V = V.contiguous()
+        if p.activation_aware_LR:
+            lmin = lam.min()
+            if float(lmin.item()) < p.sigma_reg:
+                lam = lam + (torch.tensor(p.sigma_reg, dtype=lam.dtype, device=dev) - lmin)
+            sq = torch.sqrt(lam)
+            self.Vs = K.scale_rc(V, colscale=sq)[0]
+            self.Vinv = K.scale_rc(V, colscale=1.0 / sq)[0]
+            self.H_lplr = None
+        else:
+            self.Vs = self.Vinv = None
+            self.H_lplr = H.contiguous()
+        self.Ve, self.lam_e = V.contiguous(), lam.contiguous()
+
+    def dense_err(self, E: torch.Tensor, tmp: torch.Tensor) -> torch.Tensor:
+        """tr(E H E^T) per matrix = sum_k lam_k ||E v_k||^2 (E (B, m, n) fp32; tmp same shape)."""
+        K.gemm(E, self.Ve, C=tmp)
+        return K.weighted_sqsum(tmp, self.lam_e, self.lam_e.numel())
+
+
 class BatchState:
+    """Per-batch decomposition state.  Uniform Q lives as packed codes + one scale per
+    matrix (dequantised on the fly); the codebook methods (nf4/nf2/bbint) keep their dense
+    fp32 Q (`Qd`, with a bound `Qbound` on |Q|) and per-matrix (codes, params) items in the
+    reference's return layout.  Codebook L/R idxs/scales are per-matrix lists likewise."""
+
     def __init__(self, B, m, n, r, p: EngineParams, dev):
         self.B, self.m, self.n, self.r = B, m, n, r
         f32 = torch.float32
         numel = m * n
-        self.q_packed = p.Q_bits <= 4 and numel % 4 == 0
+        self.dense_q = p.method_Q != "uniform"
+        self.Qd = self.Qbound = None
+        self.q_items = [None] * B
+        self.q_packed = p.Q_bits <= 4 and numel % 4 == 0 and not self.dense_q
+        if self.dense_q:
+            numel = 1  # the uniform code buffers are unused
         self.qcode_numel = numel * p.Q_bits // 8 if self.q_packed else numel
         qdt = torch.uint8 if self.q_packed else K.code_dtype(p.Q_bits)
         self.Qc = torch.zeros((B, self.qcode_numel), dtype=qdt, device=dev)  # codes (Q=0: see has_Q)
@@ -126,13 +182,27 @@ class BatchState:
         if dst.L.shape != self.L.shape:
             dst.L = torch.zeros_like(self.L)
             dst.R = torch.zeros_like(self.R)
-        if self.L_idxs is not None and (dst.L_idxs is None or dst.L_idxs.shape != self.L_idxs.shape):
+        if torch.is_tensor(self.L_idxs) and (dst.L_idxs is None or dst.L_idxs.shape != self.L_idxs.shape):
             dst.L_idxs = torch.zeros_like(self.L_idxs)
             dst.R_idxs = torch.zeros_like(self.R_idxs)
             dst.L_scale = torch.zeros_like(self.L_scale)
             dst.R_scale = torch.zeros_like(self.R_scale)
         pairs = [(dst.Qc, self.Qc), (dst.Qs, self.Qs), (dst.L, self.L), (dst.R, self.R)]
-        if self.L_idxs is not None:
+        if self.dense_q and self.has_Q:
+            # codebook Q: every Q update allocates fresh tensors, so the snapshot keeps views
+            if dst.Qd is None:
+                dst.Qd = [None] * B
+            for b in sel:
+                dst.Qd[b] = self.Qd[b]
+                dst.q_items[b] = self.q_items[b]
+        if isinstance(self.L_idxs, list):
+            if not isinstance(dst.L_idxs, list):
+                dst.L_idxs, dst.R_idxs = [None] * B, [None] * B
+                dst.L_scale, dst.R_scale = [None] * B, [None] * B
+            for b in sel:
+                dst.L_idxs[b], dst.R_idxs[b] = self.L_idxs[b], self.R_idxs[b]
+                dst.L_scale[b], dst.R_scale[b] = self.L_scale[b], self.R_scale[b]
+        elif self.L_idxs is not None:
             pairs += [(dst.L_idxs, self.L_idxs), (dst.R_idxs, self.R_idxs),
                       (dst.L_scale, self.L_scale), (dst.R_scale, self.R_scale)]
         if len(sel) == B:
@@ -161,10 +231,8 @@ class CalderaEngine:
         self.timings = {}
         self.solver = None
         for meth in (params.method_Q, params.method_LR):
-            if meth != "uniform":
-                raise NotImplementedError(f"quantizer method '{meth}' is not yet available on MI355X")
-        if params.rand_svd:
-            raise NotImplementedError("rand_svd=True is not yet available on MI355X")
+            if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
+                raise NotImplementedError(f"Quantization method '{meth}' not supported yet.")
 
     # ------------------------------------------------------------------ pieces
     def _q_update(self, st: BatchState, Ws, res_buf, wts: _Weights, den):
@@ -172,6 +240,8 @@ class CalderaEngine:
         p = self.p
         B, m, n = st.B, st.m, st.n
         Kdim = st.L.shape[-1] if (p.compute_low_rank_factors and st.has_LR) else 0
+        if st.dense_q:
+            return self._q_update_codebook(st, Ws, res_buf, wts, Kdim)
         if Kdim % 32 == 0:
             # fused: res = W - L R recomputed per tile on split-fp16 products, never stored
             err = torch.empty(B, dtype=torch.float64, device=Ws.device)
@@ -199,20 +269,73 @@ class CalderaEngine:
         st.has_Q = True
         return err
 
+    def _q_update_codebook(self, st: BatchState, Ws, res_buf, wts: _Weights, Kdim):
+        """Q update with a codebook quantiser (nf4/nf2/bbint4/bbint2): res = W - L R
+        (alg.py:262) into the fp32 work buffer, then the whole-matrix quantiser
+        (alg.py:245-250) with the error sum_j h_j (deq - res)^2 fused."""
+        p = self.p
+        B, m, n = st.B, st.m, st.n
+        dev = Ws.device
+        if Kdim:
+            absmax = torch.zeros(B, dtype=torch.int32, device=dev)
+            K.gemm(st.L, st.R, C=res_buf, D=Ws, epi=K.EPI_RESID, absmax=absmax, batch=B)
+        else:
+            K.build_residual(Ws, None, None, 2, None, res=res_buf)
+        x = res_buf.view(B, m * n)
+        err = torch.empty(B, dtype=torch.float64, device=dev)
+        items, deq = self._quantize_whole(x, p.method_Q, p.Q_bits, err_w=wts.err, err_ncols=n, err_out=err)
+        st.Qd = deq.view(B, m, n)
+        st.Qbound = K.absmax(st.Qd)
+        st.q_items = items
+        st.has_Q = True
+        return err
+
+    def _quantize_whole(self, x, method, bits, **err):
+        """quantize_matrix (alg.py:245-250) of B matrices x (B, numel) with a codebook method:
+        returns ([(A_idxs (1, ...), params)] per matrix in the reference's layout, deq (B, numel))."""
+        B, numel = x.shape
+        if method in ("nf4", "nf2"):
+            out = K.quantize_nf(x, numel, qlog.code_bits(method, bits), **err)
+            return [(out["idx"][b].view(1, -1), out["scale"][b].view(1, 1)) for b in range(B)], out["deq"]
+        cb = qlog.code_bits(method, bits)
+        if numel % (8 // cb):
+            raise RuntimeError(f"{method}: {numel} elements do not pack {8 // cb} codes per byte")
+        out = K.quantize_bbint(x, numel, cb, **err)
+        items, off = [], 0
+        for b in range(B):
+            k = out["n_out"][b]
+            qlog.log_outliers(id(self) + b, k)  # one reference quantizer call per matrix
+            items.append((out["packed"][b].view(1, -1),
+                          (out["bmin"][b].view(1, 1), out["bscale"][b].view(1, 1), out["vals"][off:off + k],
+                           out["idx"][off:off + k])))
+            off += k
+        return items, out["deq"]
+
     def _lr_update(self, st: BatchState, Ws, Y, res, wts: _Weights, den):
         """maybe_update_LR / update_LR / LR_init (alg.py:115-235) + error (:286-302)."""
         p = self.p
         B, m, n = st.B, st.m, st.n
         dev = Ws.device
         quantized = p.L_bits < 16 or p.R_bits < 16
-        weighted = p.activation_aware_LR and wts.ycol is not None
+        weighted = p.activation_aware_LR and (wts.ycol is not None or wts.dense)
+        if self.solver is None and p.rand_svd:  # torch.svd_lowrank branch (alg.py:213-216, :228-231)
+            self.solver = RandSVD(B, m, n, p.rank, dev)
         if self.solver is None:
             self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
                                       filter_precision=self.filter_precision, **self.solver_kwargs)
         sv = self.solver
         y_split = None
         ysq = None
-        if sv.x3 and not sv.direct and m % 32 == 0 and n % 64 == 0 and st.q_packed:
+        if st.dense_q and st.has_Q:
+            qsrc, qsc, qbits = st.Qd, st.Qbound, 32
+        else:
+            qsrc, qsc, qbits = (st.Qc, st.Qs, p.Q_bits) if st.has_Q else (None, None, p.Q_bits)
+        if wts.dense:
+            # res = W - Q; data-aware Y = res @ H_sqrt @ V = res @ Vs (alg.py:211)
+            K.build_residual(Ws, qsrc, qsc, qbits, None, res=res)
+            if weighted:
+                K.gemm(res, wts.Vs, C=Y)
+        elif sv.x3 and not sv.direct and m % 32 == 0 and n % 64 == 0 and (st.q_packed or st.dense_q):
             # one pass: res / Y (fp32), the solver's Gram operand halves and ||Y||^2
             if self._yh is None:
                 self._yh = torch.empty((B, m, n), dtype=torch.float16, device=dev)
@@ -220,16 +343,16 @@ class CalderaEngine:
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
             halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)
-            K.residual_split(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, p.Q_bits, self._wmax,
+            K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
                              ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
                              res=res, Y=Y if weighted else None, scale=self._ys, sq=ysq, **halves)
             y_split = (self._yh, self._yl, self._ys)
         else:
-            K.build_residual(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, p.Q_bits,
-                             wts.ycol, Y=Y if weighted else None, res=res)
+            K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
         Y = Ysrc
         vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split)
+        rand = isinstance(sv, RandSVD)
         r = sv.r
         S = torch.sqrt(theta.clamp_min(0.0))  # singular values (fp64)
         S32 = S.float()
@@ -240,14 +363,22 @@ class CalderaEngine:
             U = vecs  # (B, m, r) view, ld p
             if p.activation_aware_LR:
                 L.copy_(U)
-                # R = (U^T Y) diag(1/sqrt(lam))   (alg.py:219-225)
-                K.gemm(U, Ysrc, ta=True, C=R)
+                # R = (U^T Y) diag(1/sqrt(lam))   (alg.py:219-225); randomized: S Vh as returned
+                if rand:
+                    R.copy_(sv.SVh)
+                else:
+                    K.gemm(U, Ysrc, ta=True, C=R)
                 if wts.rinv is not None:
                     K.scale_rc(R, colscale=wts.rinv, out=R)
+                elif wts.dense:  # R = R~ diag(1/sqrt lam) V^T
+                    R = K.gemm(R.clone(), wts.Vinv, tb=True, C=R)
             else:
                 sq = torch.sqrt(S32)
                 K.scale_rc(U, colscale=sq, out=L)  # L = U sqrt(S)
-                K.gemm(U, Ysrc, ta=True, C=R)      # S Vh
+                if rand:
+                    R.copy_(sv.SVh)
+                else:
+                    K.gemm(U, Ysrc, ta=True, C=R)  # S Vh
                 rs = torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30))
                 K.scale_rc(R, rowscale=rs, out=R)  # R = sqrt(S) Vh
         else:
@@ -257,6 +388,8 @@ class CalderaEngine:
                 K.gemm(Ysrc, V, C=L)                 # Y V
                 K.scale_rc(L, colscale=inv, out=L)   # U = Y V / S
                 K.scale_rc(V, trans=True, rowscale=S32, colscale=wts.rinv, out=R)  # S V^T diag(rinv)
+                if wts.dense:
+                    R = K.gemm(R.clone(), wts.Vinv, tb=True, C=R)
             else:
                 sq = torch.sqrt(S32)
                 K.gemm(Ysrc, V, C=L)
@@ -267,7 +400,9 @@ class CalderaEngine:
         st.L, st.R = L, R
         st.has_LR = True
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
-        if sv.left and p.activation_aware_LR and not quantized:
+        if wts.dense:
+            return self._state_error(st, Ws, res, wts)
+        if sv.left and p.activation_aware_LR and not quantized and not rand:
             # L = U (orthonormal columns), L R = U U^T Y diag(1/sqrt(h)) with h the error
             # weights, so the weighted residual is (I - U U^T) Y and, by Pythagoras,
             # sum_j h_j (res - L R)_ij^2 = ||Y||^2 - ||U^T Y||^2 = ||Y||^2 - sum_j h_j R_ij^2
@@ -293,6 +428,9 @@ class CalderaEngine:
         aware = p.activation_aware_LR
         R = R0
         best_err = torch.full((B,), float("inf"), dtype=torch.float64, device=dev)
+        cb = p.method_LR != "uniform"
+        best_items = [None] * B
+        resH = None
         best = dict(L=torch.zeros((B, m, r), device=dev), R=torch.zeros((B, r, n), device=dev),
                     Lc=torch.zeros((B, m * r), dtype=K.code_dtype(p.L_bits), device=dev),
                     Rc=torch.zeros((B, r * n), dtype=K.code_dtype(p.R_bits), device=dev),
@@ -305,29 +443,50 @@ class CalderaEngine:
         err = torch.empty(B, dtype=torch.float64, device=dev)
         for _ in range(p.lplr_iters):
             # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T = (Y Rw^T)(Rw Rw^T)^{-1}   (alg.py:162-169)
-            Rw = K.scale_rc(R, colscale=wts.ycol) if (aware and wts.ycol is not None) else R
+            if aware and wts.dense:
+                Rw = K.gemm(R, wts.Vs, C=torch.empty_like(R))  # R H_sqrt V
+            else:
+                Rw = K.scale_rc(R, colscale=wts.ycol) if (aware and wts.ycol is not None) else R
             Bm = K.gemm(Ysrc, Rw, tb=True, C=tmp_mr)            # m x r
             Mr = K.gram_f64(Rw, Rw, ta=True, tb=True)          # r x r
             Wr, info = self._solve_normal(Mr)
             T1 = K.gemm(Bm, Wr, C=torch.empty_like(tmp_mr))     # (Y Rw^T) Wr
             K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
-            # --- quantise L^T as one block (alg.py:171-172); codes kept in L layout
-            qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
-            L = qL["deq"].view(B, m, r)
+            # --- quantise L^T as one block (alg.py:171-172)
+            if cb:
+                Lt = K.transpose_split(L, out=torch.empty((B, r, m), dtype=torch.float32, device=dev))[0]
+                itemsL, deqLt = self._quantize_whole(Lt.view(B, r * m), p.method_LR, p.L_bits)
+                L = K.transpose_split(deqLt.view(B, r, m), out=torch.empty((B, m, r), dtype=torch.float32,
+                                                                            device=dev))[0]
+            else:  # uniform: codes kept in L layout (absmax is order-free), reordered when kept
+                qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
+                L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
             Ml = K.gram_f64(L, L)                              # r x r
             Wl, info2 = self._solve_normal(Ml)
             Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
             T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
             K.gemm(Wl, T2, C=Rn)
-            qR = K.quantize_uniform(Rn.view(B, r * n), r * n, p.R_bits, codes=True, deq=True)
-            R = qR["deq"].view(B, r, n)
+            if cb:
+                itemsR, deqR = self._quantize_whole(Rn.view(B, r * n), p.method_LR, p.R_bits)
+                R = deqR.view(B, r, n)
+            else:
+                qR = K.quantize_uniform(Rn.view(B, r * n), r * n, p.R_bits, codes=True, deq=True)
+                R = qR["deq"].view(B, r, n)
             # --- error ||(res - L R) H_sqrt||_F  (alg.py:182)
             if aware:
-                Rw2 = K.scale_rc(R, colscale=wts.ycol) if wts.ycol is not None else R
+                if wts.dense:
+                    Rw2 = K.gemm(R, wts.Vs, C=torch.empty_like(R))
+                else:
+                    Rw2 = K.scale_rc(R, colscale=wts.ycol) if wts.ycol is not None else R
                 K.gemm(L, Rw2, D=Y, epi=K.EPI_WERR, err_out=err)
             else:
-                K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.lplr, err_out=err)
+                if wts.dense:  # ||(res - L R) H||^2 with H_sqrt = H (alg.py:47-49, :182)
+                    if resH is None:
+                        resH = K.gemm(res, wts.H_lplr, C=torch.empty_like(res))
+                    K.gemm(L, K.gemm(R, wts.H_lplr, C=torch.empty_like(R)), D=resH, epi=K.EPI_WERR, err_out=err)
+                else:
+                    K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.lplr, err_out=err)
             e32 = torch.sqrt(err).float().double()  # torch.linalg.matrix_norm in fp32
             better = e32 < best_err
             yield
@@ -336,13 +495,23 @@ class CalderaEngine:
             for b in sel:
                 best["L"][b].copy_(L[b])
                 best["R"][b].copy_(R[b])
+                if cb:
+                    best_items[b] = (itemsL[b], itemsR[b])
+                    best_err[b] = e32[b]
+                    continue
                 best["Lc"][b].copy_(qL["codes"][b].view(m, r).t().reshape(-1))  # L^T order
                 best["Rc"][b].copy_(qR["codes"][b])
                 best["Ls"][b] = qL["scale"][b, 0]
                 best["Rs"][b] = qR["scale"][b, 0]
                 best_err[b] = e32[b]
-        st.L_idxs, st.R_idxs = best["Lc"], best["Rc"]
-        st.L_scale, st.R_scale = best["Ls"], best["Rs"]
+        if cb:
+            st.L_idxs = [it[0][0] if it else None for it in best_items]
+            st.L_scale = [it[0][1] if it else None for it in best_items]
+            st.R_idxs = [it[1][0] if it else None for it in best_items]
+            st.R_scale = [it[1][1] if it else None for it in best_items]
+        else:
+            st.L_idxs, st.R_idxs = best["Lc"], best["Rc"]
+            st.L_scale, st.R_scale = best["Ls"], best["Rs"]
         return best["L"], best["R"]
 
     # ------------------------------------------------------------------ driver
@@ -365,11 +534,23 @@ class CalderaEngine:
             W = W.float()
         if n % 4:
             raise NotImplementedError("caldera-mi355x: W.shape[1] must be a multiple of 4")
+        if p.compute_quantized_component and "Q" in p.update_order:
+            qlog.check_method_bits(p.method_Q, p.Q_bits)  # get_quant_info (alg.py:238-242)
+        if p.compute_low_rank_factors and "LR" in p.update_order and (p.L_bits < 16 or p.R_bits < 16):
+            qlog.check_method_bits(p.method_LR, p.L_bits)
+            qlog.check_method_bits(p.method_LR, p.R_bits)
         gs, Ws = K.rms_scale(W, scale_W)
         wts = _Weights(h, n, p, dev)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
         self._yh = self._yl = self._ys = None
-        den = K.weighted_sqsum(Ws, wts.err, n)
+        if wts.dense:  # den = tr(W H W^T) (alg.py:298)
+            self._etmp = torch.empty((B, m, n), dtype=torch.float32, device=dev)
+            wf = torch.empty((B, m, n), dtype=torch.float32, device=dev)
+            K.build_residual(Ws, None, None, 2, None, res=wf)
+            den = wts.dense_err(wf, self._etmp)
+            del wf
+        else:
+            den = K.weighted_sqsum(Ws, wts.err, n)
         r = p.rank
         st = BatchState(B, m, n, r, p, dev)
         best = BatchState(B, m, n, r, p, dev)
@@ -392,6 +573,8 @@ class CalderaEngine:
                     num = yield from self._lr_update(st, Ws, work, res, wts, den)
                 elif mtx == "Q" and p.compute_quantized_component:
                     num = self._q_update(st, Ws, work, wts, den)
+                    if wts.dense:
+                        num = self._state_error(st, Ws, work, wts)
                 updated[mtx] = True
                 if num is None:  # no update: error of the unchanged state
                     num = self._state_error(st, Ws, work, wts)
@@ -413,8 +596,16 @@ class CalderaEngine:
 
     def _state_error(self, st, Ws, work, wts):
         B, m, n = st.B, st.m, st.n
-        K.build_residual(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, self.p.Q_bits,
-                         None, res=work)
+        if st.dense_q and st.has_Q:
+            K.build_residual(Ws, st.Qd, None, 32, None, res=work)
+        else:
+            K.build_residual(Ws, st.Qc if st.has_Q else None, st.Qs if st.has_Q else None, self.p.Q_bits,
+                             None, res=work)
+        if wts.dense:  # E = W - Q - L R, then tr(E H E^T)
+            if st.has_LR:
+                K.gemm(st.L, st.R, C=work, D=work, epi=K.EPI_RESID,
+                       absmax=torch.zeros(B, dtype=torch.int32, device=Ws.device))
+            return wts.dense_err(work, self._etmp)
         err = torch.empty(B, dtype=torch.float64, device=Ws.device)
         K.gemm(st.L, st.R, D=work, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
@@ -433,7 +624,10 @@ class CalderaEngine:
                             for b in range(B)]
         for b in range(B):
             d = {}
-            if best.flag_Q[b]:
+            if best.flag_Q[b] and best.dense_q:
+                d["Q"] = best.Qd[b].clone()
+                d["Q_idxs"], d["Q_scale"] = best.q_items[b]
+            elif best.flag_Q[b]:
                 qc = best.Qc[b:b + 1]
                 codes = K.unpack_codes(qc, m * n, p.Q_bits) if best.q_packed else qc.clone()
                 # dequantize_block (quantization.py:103-105) on the reference int codes
@@ -446,7 +640,10 @@ class CalderaEngine:
                 d["Q_scale"] = 1
             d["L"] = best.L[b].clone()
             d["R"] = best.R[b].clone()
-            if best.L_idxs is not None and best.flag_LR[b]:
+            if isinstance(best.L_idxs, list) and best.flag_LR[b] and best.L_idxs[b] is not None:
+                d["L_idxs"], d["R_idxs"] = best.L_idxs[b], best.R_idxs[b]
+                d["L_scale"], d["R_scale"] = best.L_scale[b], best.R_scale[b]
+            elif torch.is_tensor(best.L_idxs) and best.flag_LR[b]:
                 d["L_idxs"] = best.L_idxs[b].view(1, -1).clone()
                 d["R_idxs"] = best.R_idxs[b].view(1, -1).clone()
                 d["L_scale"] = best.L_scale[b].view(1, 1).clone()

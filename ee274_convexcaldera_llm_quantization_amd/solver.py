@@ -392,3 +392,84 @@ class RankRSolver:
         self.theta = theta.clone()
         self._ends = ends
         return self.X[:, :, : self.r], theta[:, : self.r]
+
+
+class RandSVD:
+    """`torch.svd_lowrank(Y, q, niter=2)` of LR_init's rand_svd branch (alg.py:213-216,
+    :228-231; q = min(2 rank, min(m, n))), restated on the HIP kernels for a batch in
+    lockstep: Halko et al. Algorithm 5 with the same structure as torch/_lowrank.py — a
+    Gaussian sketch, `niter` power iterations re-orthonormalised after every product, a
+    wide Y (m < n) processed as Y^T — with CholQR2 (fp64 Gram + symmetric
+    elimination) in place of Householder QR (same subspaces) and the small SVD through the
+    Jacobi eigensolver of the q x q Gram.  The sketch is random, as in the reference, so
+    results agree with it statistically, not bitwise (oracle/caldera_oracle.py:svd_lowrank is
+    pinned to torch.svd_lowrank on a shared sketch, tests/test_oracle_golden.py).
+
+    solve_iter returns (U (B, m, r), theta = S^2 (B, r)) and sets `self.SVh` = diag(S) Vh
+    restricted to the top r (B, r, n): LR_init's R before the H scaling.  As in torch the
+    transposed variant's S Vh carries the projection onto the sketch (A Q Q^T), so R is not
+    re-fitted as U^T Y."""
+
+    left = True
+    direct = False
+    x3 = False
+
+    def __init__(self, B: int, m: int, n: int, r: int, device, *, niter: int = 2, seed: int = 0x5EED):
+        self.B, self.m, self.n = B, m, n
+        self.k = min(m, n)
+        self.r = min(r, self.k)
+        self.q = min(2 * r, self.k)
+        self.niter = niter
+        self.device = device
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(seed)
+        self.stats = SolverStats()
+        self.SVh = None
+
+    def release(self):
+        self.SVh = None
+
+    @staticmethod
+    def _orth(X):
+        for _ in range(2):  # CholQR2
+            M = K.gram_f64(X, X)
+            Wt32, _, _ = K.spd_whiten(M)
+            X = K.gemm(X, Wt32, C=torch.empty_like(X))
+        return X
+
+    def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None):
+        B, m, n, q, r = self.B, self.m, self.n, self.q, self.r
+        dev = Y.device
+        f32 = torch.float32
+        self.stats.calls += 1
+        transposed = m < n  # torch: "assume that A is tall", a wide A is processed as A^T
+        if transposed:  # basis of range(Y^T): Q (n x q)
+            R0 = torch.randn((B, m, q), generator=self.gen, device=dev, dtype=f32)
+            Qb = self._orth(K.gemm(Y, R0, ta=True, C=torch.empty((B, n, q), dtype=f32, device=dev)))
+            for _ in range(self.niter):
+                Qm = self._orth(K.gemm(Y, Qb, C=torch.empty((B, m, q), dtype=f32, device=dev)))
+                Qb = self._orth(K.gemm(Y, Qm, ta=True, C=torch.empty((B, n, q), dtype=f32, device=dev)))
+            Bt = K.gemm(Y, Qb, C=torch.empty((B, m, q), dtype=f32, device=dev))      # A Q
+            T = K.gram_f64(Bt, Bt)                                                   # (A Q)^T (A Q)
+            theta, Vb, _, _ = K.jacobi_eigh(T, tol=1e-12)
+            S = torch.sqrt(theta[:, :r].clamp_min(0.0)).float()
+            U = K.gemm(Bt, Vb[:, :, :r], C=torch.empty((B, m, r), dtype=f32, device=dev))
+            inv = torch.where(S > 0, 1.0 / S.clamp_min(1e-30), torch.zeros_like(S))
+            K.scale_rc(U, colscale=inv, out=U)                                       # U = A Q Vb / S
+            V = K.gemm(Qb, Vb[:, :, :r], C=torch.empty((B, n, r), dtype=f32, device=dev))  # Q Vb
+            self.SVh = K.scale_rc(V, trans=True, rowscale=S)                         # S V^T
+        else:  # basis of range(Y): Q (m x q)
+            R0 = torch.randn((B, n, q), generator=self.gen, device=dev, dtype=f32)
+            Qm = self._orth(K.gemm(Y, R0, C=torch.empty((B, m, q), dtype=f32, device=dev)))
+            for _ in range(self.niter):
+                Qb = self._orth(K.gemm(Y, Qm, ta=True, C=torch.empty((B, n, q), dtype=f32, device=dev)))
+                Qm = self._orth(K.gemm(Y, Qb, C=torch.empty((B, m, q), dtype=f32, device=dev)))
+            Bm = K.gemm(Qm, Y, ta=True, C=torch.empty((B, q, n), dtype=f32, device=dev))  # Q^T A
+            T = K.gram_f64(Bm, Bm, ta=True, tb=True)                                # B B^T
+            theta, Ub, _, _ = K.jacobi_eigh(T, tol=1e-12)
+            U = K.gemm(Qm, Ub[:, :, :r], C=torch.empty((B, m, r), dtype=f32, device=dev))
+            self.SVh = K.gemm(Ub[:, :, :r], Bm, ta=True, C=torch.empty((B, r, n), dtype=f32, device=dev))
+        self.stats.outer += 1
+        if False:
+            yield
+        return U, theta[:, :r]

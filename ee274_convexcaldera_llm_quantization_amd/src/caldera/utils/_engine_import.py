@@ -14,3 +14,4 @@ except ImportError:  # imported through the reference-style path: add the repo r
 
 kernels = importlib.import_module(_PKG + "._lib")
 api = importlib.import_module(_PKG + ".api")
+qlog = importlib.import_module(_PKG + ".qlog")

@@ -13,6 +13,7 @@ from typing import List
 import torch
 
 from ._engine_import import kernels as _K
+from ._engine_import import qlog as _qlog
 
 _BITWIDTHS = [2, 4, 8, 16]
 _QUANTIZER_METHODS = ["uniform", "nf4", "nf2", "bbint4", "bbint2"]
@@ -34,9 +35,15 @@ def _to_device(t: torch.Tensor):
     return t.to(torch.device("cuda", torch.cuda.current_device())), t.device
 
 
+def bbint_bits(method: str) -> int:
+    """Packing width of a bbint method (quantization.py:151 two codes per byte, :218-221 four)."""
+    return 4 if method == "bbint4" else 2
+
+
 class LowMemoryQuantizer(AbstractQuantizer):
-    """quantization.py:18-307.  Methods: uniform (HIP); nf4/nf2/bbint4/bbint2 validated
-    exactly as the reference, computed on MI355X in a later round."""
+    """quantization.py:18-307.  Every method (uniform, nf4, nf2, bbint4, bbint2) runs in
+    libcaldera_hip.so on the HIP device; codes, scales and parameter tuples have the
+    reference's shapes and dtypes."""
 
     def __init__(self, num_bits: int = 2, method: str = "uniform", block_size: int = 64):
         self.num_bits = num_bits
@@ -63,24 +70,49 @@ class LowMemoryQuantizer(AbstractQuantizer):
                 f"Weight with shape {weight.shape[0]} x {weight.shape[1]} "
                 f"is not divisible by block size {self.block_size}"
             )
-        if self.method != "uniform":
-            raise NotImplementedError(f"method '{self.method}' is not yet implemented on MI355X")
         x, home = _to_device(weight)
         # reduced-precision inputs are promoted by the reference (maximum with an fp32 eps)
         x = x.detach().to(torch.float32).contiguous().view(1, total)
-        out = _K.quantize_uniform(x, self.block_size, self.num_bits, epsilon, codes=True, deq=False)
-        codes = out["codes"].view(-1, self.block_size)
-        scale = out["scale"].view(-1, 1)
-        if home is not None:
-            codes, scale = codes.to(home), scale.to(home)
-        return codes, scale, weight.shape
+        bs = self.block_size
+
+        def back(t):
+            return t.to(home) if home is not None else t
+
+        if self.method == "uniform":
+            out = _K.quantize_uniform(x, bs, self.num_bits, epsilon, codes=True, deq=False)
+            return back(out["codes"].view(-1, bs)), back(out["scale"].view(-1, 1)), weight.shape
+        if self.method in ("nf4", "nf2"):
+            out = _K.quantize_nf(x, bs, 4 if self.method == "nf4" else 2, epsilon, idx=True, deq=False)
+            return back(out["idx"].view(-1, bs)), back(out["scale"].view(-1, 1)), weight.shape
+        bits = bbint_bits(self.method)
+        if bs % (8 // bits):
+            raise RuntimeError(f"{self.method}: block size {bs} is not a multiple of {8 // bits} "
+                               f"(the reference's strided packing fails on this shape)")
+        out = _K.quantize_bbint(x, bs, bits, epsilon, packed=True, deq=False)
+        _qlog.log_outliers(id(self), out["n_out"][0])
+        params = (back(out["bmin"].view(-1, 1)), back(out["bscale"].view(-1, 1)), back(out["vals"]),
+                  back(out["idx"]))
+        return back(out["packed"].view(-1, bs * bits // 8)), params, weight.shape
 
     def dequantize_block(self, weight_quant: torch.Tensor, weight_params, weight_shape: List[int]):
-        if self.method != "uniform":
-            raise NotImplementedError(f"method '{self.method}' is not yet implemented on MI355X")
         c, home = _to_device(weight_quant)
-        s, _ = _to_device(weight_params)
-        out = _K.dequantize_uniform(c.contiguous(), s.contiguous().float(), self.num_bits)
+        c = c.contiguous()
+        if self.method == "uniform":
+            s, _ = _to_device(weight_params)
+            out = _K.dequantize_uniform(c, s.contiguous().float(), self.num_bits)
+        elif self.method in ("nf4", "nf2"):
+            s, _ = _to_device(weight_params)
+            out = _K.dequantize_nf(c.to(torch.uint8), s.contiguous().float(), 4 if self.method == "nf4" else 2)
+        elif self.method in ("bbint4", "bbint2"):
+            bits = bbint_bits(self.method)
+            bmin, bscale, vals, idx = (_to_device(t)[0] for t in weight_params)
+            nblk = bmin.numel()
+            bs = c.numel() * 8 // bits // nblk
+            out = _K.dequantize_bbint(c.to(torch.uint8), bits, bmin.contiguous().float(),
+                                      bscale.contiguous().float(), vals.contiguous().float(),
+                                      idx.contiguous(), bs)
+        else:
+            raise NotImplementedError(f"Dequantization method '{self.method}' not implemented.")
         out = out.view(-1).reshape(weight_shape)
         return out.to(home) if home is not None else out
 

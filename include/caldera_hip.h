@@ -93,12 +93,54 @@ int cq_unpack_codes(const uint8_t* packed, int64_t batch, int64_t numel, int bit
                     int8_t* codes, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * NF4 / NF2 codebook quantiser.  Replaces RCR/src/caldera/utils/quantization.py:39-91
+ * (levels, thresholds (l_i + l_{i+1}) / 2, _quantize_nf, _dequantize_nf) with the dispatch
+ * of :270-279 / :296-298.  x: batch x numel fp32 in blocks of block_size:
+ *   scale = max(max|x_blk|, eps);  idx = #{t : x / scale > thr_t}  (uint8, reference layout)
+ *   deq   = level[idx] * scale
+ * idx / deq optional; err_out[b] = sum err_w[j % err_ncols] (deq - x)^2 (fp64) if non-NULL. */
+size_t cq_quantize_nf_workspace(int64_t batch, int64_t numel, int64_t block_size);
+int cq_quantize_nf(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, float eps,
+                   uint8_t* idx, float* deq, float* scale, const float* err_w, int64_t err_ncols,
+                   double* err_out, void* ws, size_t ws_bytes, void* stream);
+/* out[e] = level[idx[e]] * scale[e / block_size]  (quantization.py:87-91) */
+int cq_dequant_nf(const uint8_t* idx, const float* scale, int64_t total, int64_t block_size, int bits,
+                  float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * bbint4 / bbint2 (bitsandbytes-style affine codes with 6-sigma outliers).  Replaces
+ * quantization.py:107-154 (_quantize_bbint4), :175-222 (_quantize_bbint2) and their dequant
+ * :157-172 / :224-243.  Two calls with the same workspace (the outlier list is variable
+ * length, so the caller reads n_outliers between them):
+ *   cq_bbint_stats: per block mean (reference fp32 order), unbiased std (max eps), outlier
+ *     mask |x - mean| > 6 std, min / max of the outlier-replaced block, scale = max((max -
+ *     min) / (2^bits - 1), eps) -> bmin, bscale [batch * nblk]; n_outliers[b] per matrix.
+ *   cq_bbint_emit: packed codes (uint8, MSB-first, 8/bits per byte, reference layout
+ *     (nblk, block_size*bits/8)), deq (fp32, outliers restored), the outlier values and
+ *     their int64 (row, col) indices in the (nblk, block_size) view (torch.nonzero order),
+ *     all matrices concatenated (matrix b after matrix b-1), err_out as for the uniform
+ *     quantiser.  Any output may be NULL (out_vals and out_idx together). */
+size_t cq_bbint_workspace(int64_t batch, int64_t numel, int64_t block_size);
+int cq_bbint_stats(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, float eps,
+                   float* bmin, float* bscale, int64_t* n_outliers, void* ws, size_t ws_bytes, void* stream);
+int cq_bbint_emit(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, const float* bmin,
+                  const float* bscale, uint8_t* packed, float* deq, float* out_vals, int64_t* out_idx,
+                  const float* err_w, int64_t err_ncols, double* err_out, void* ws, size_t ws_bytes, void* stream);
+/* out = u * bscale[blk] + bmin[blk] from the packed codes, then out[row*bs + col] = value for
+ * each of the n_outliers listed outliers. */
+int cq_dequant_bbint(const uint8_t* packed, int bits, const float* bmin, const float* bscale, int64_t total,
+                     int64_t block_size, const float* out_vals, const int64_t* out_idx, int64_t n_outliers,
+                     float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Residual builder for the LR update.  Replaces alg.py:124 (residual = W - Q) and the
  * diagonal-H form of alg.py:211 (Y = residual @ H_sqrt @ eigvecs; for diagonal H this is
  * a column scaling by sqrt(h) up to a permutation that LR_init undoes):
  *   res_ij = float(Ws_ij) - (float(c_ij)/k)*scale_b    (Q from packed codes; packed==NULL: Q=0)
  *   Y_ij   = res_ij * ycol[j]                           (ycol == NULL: 1)
  * Ws: fp16 or fp32 (dtype).  Y and/or res_out may be NULL.
+ * bits == 32: `packed` is a dense fp32 dequantised Q (the codebook methods nf4/nf2/bbint,
+ * whose Q is not an affine function of one scale); `scale` is then unused.
  */
 int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const float* scale,
                       int bits, const float* ycol, int64_t batch, int64_t m, int64_t n,
@@ -241,7 +283,8 @@ int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out
  * K-blocked split halves of Y over its columns (hi/lo, layout of cq_split_f16 blocked) and
  * over its rows (thi/tlo: Y^T as an n x m operand, blocked), and sq_out[b] = ||Y||_F^2
  * (fp64).  The halves' scale (scale_out[b]) is the power of two for the bound
- * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|.  m % 32 == 0, n % 64 == 0. */
+ * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|.  m % 32 == 0, n % 64 == 0.
+ * bits == 32: `packed` is a dense fp32 Q and qscale[b] a bound on max|Q[b]|. */
 size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch);
 int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,
                       const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m,
