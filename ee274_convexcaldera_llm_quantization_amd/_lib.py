@@ -91,6 +91,7 @@ _SIGS = {
     "cq_gram_f64": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_int, c_i64, c_i64, c_vp, c_int, c_i64,
                             c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_spd_whiten": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "cq_spd_whiten_rcond": (c_int, [c_vp, c_i64, c_i64, c_double, c_vp, c_vp, c_vp, c_vp]),
     "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_size, c_vp]),
@@ -420,15 +421,16 @@ def gram_f64(A, B, *, ta=False, tb=False, out=None):
     return out
 
 
-def spd_whiten(S: torch.Tensor):
-    """S (B, p, p) fp64 SPD (overwritten) -> (Wt32, Wt64, info) with Wt^T S Wt = I."""
+def spd_whiten(S: torch.Tensor, rcond2: float = 1e-30):
+    """S (B, p, p) fp64 SPD (overwritten) -> (Wt32, Wt64, info) with Wt^T S Wt = I on the
+    independent columns; pivots <= rcond2 * max diag are dropped (info = their count)."""
     _require_hip(S)
     B, p, _ = S.shape
     Wt32 = torch.empty((B, p, p), dtype=torch.float32, device=S.device)
     Wt64 = torch.empty((B, p, p), dtype=torch.float64, device=S.device)
     info = torch.empty(B, dtype=torch.int32, device=S.device)
-    _check(load().cq_spd_whiten(_p(S), p, B, _p(Wt32), _p(Wt64), _p(info), _stream(S.device)),
-           "cq_spd_whiten")
+    _check(load().cq_spd_whiten_rcond(_p(S), p, B, float(rcond2), _p(Wt32), _p(Wt64), _p(info),
+                                      _stream(S.device)), "cq_spd_whiten_rcond")
     return Wt32, Wt64, info
 
 

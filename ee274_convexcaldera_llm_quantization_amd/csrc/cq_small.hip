@@ -215,12 +215,12 @@ constexpr int kSmallThreads = 1024;
 constexpr int kSmallWaves = kSmallThreads / 64;
 
 __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __restrict__ S_all,
-                                                                    int p, double* __restrict__ E_all,
+                                                                    int p, double rc2, double* __restrict__ E_all,
                                                                     float* __restrict__ W32,
                                                                     int* __restrict__ info) {
     extern __shared__ double fac[];  // row factors of the current step + pivots
     double* piv = fac + p;
-    __shared__ int bad;
+    __shared__ int bad;  // number of dropped (dependent) pivots
     __shared__ double dmax_s;
     const int64_t b = blockIdx.x;
     double* S = S_all + b * (int64_t)p * p;
@@ -238,13 +238,15 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __res
     const double dmax = dmax_s;
     for (int j = 0; j < p; ++j) {
         const double d = S[j * p + j];
-        if (!(d > 1e-300 && d > dmax * 1e-30)) {  // not positive definite (or NaN)
-            if (tid == 0) bad = j + 1;
-            __syncthreads();
-            break;
+        // a pivot at or below rc2 * max diag: column j depends on the previous ones; it is
+        // dropped (coefficient 0, Wt column 0) — the basic least-squares solution of gelsy
+        // (torch.linalg.lstsq's CPU driver) in index order
+        const bool drop = !(d > 1e-300 && d > dmax * rc2);
+        for (int i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = drop ? 0.0 : S[j * p + i] / d;  // upper row j
+        if (tid == 0) {
+            piv[j] = drop ? __longlong_as_double(0x7ff0000000000000ll) : d;
+            bad += drop;
         }
-        for (int i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = S[j * p + i] / d;  // upper row j
-        if (tid == 0) piv[j] = d;
         __syncthreads();
         // S[i][c] -= f_i S[j][c] for j < i <= c  (upper trailing);  E[i][c] -= f_i E[j][c], c <= j
         for (int i = j + 1 + wid; i < p; i += kSmallWaves) {
@@ -260,12 +262,8 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __res
         }
         __syncthreads();
     }
-    if (bad) {
-        if (tid == 0) info[b] = bad;
-        return;
-    }
-    if (tid == 0) info[b] = 0;
-    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular); staged in S (fp64)
+    if (tid == 0) info[b] = bad;
+    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular; 0 for dropped pivots); staged in S
     for (int a = wid; a < p; a += kSmallWaves)
         for (int c = lane; c < p; c += 64) {
             const double v = (c >= a) ? E[c * p + a] / sqrt(piv[c]) : 0.0;
@@ -919,7 +917,7 @@ static size_t jacobi_reg_bytes(int p) {
 constexpr int WNB = 32;
 
 __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
-    double* __restrict__ S_all, int p, double* __restrict__ E_all, float* __restrict__ W32,
+    double* __restrict__ S_all, int p, double rc2, double* __restrict__ E_all, float* __restrict__ W32,
     int* __restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     double* U = reinterpret_cast<double*>(smem_raw);      // WNB x p   (panel rows of S, cols >= J)
@@ -942,7 +940,7 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
     }
     __syncthreads();
     const double dmax = dmax_s;
-    for (int J = 0; J < p && !bad; J += WNB) {
+    for (int J = 0; J < p; J += WNB) {
         const int nb = min(WNB, p - J);
         // load panel rows of S (columns >= J, upper part) and E (columns < J + nb)
         for (int k = wid; k < nb; k += kSmallWaves)
@@ -954,12 +952,12 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
         // in-panel elimination of pivots J..J+nb-1
         for (int k = 0; k < nb; ++k) {
             const double d = U[k * p + J + k];
-            if (!(d > 1e-300 && d > dmax * 1e-30)) {
-                if (tid == 0) bad = J + k + 1;
-                break;
+            const bool drop = !(d > 1e-300 && d > dmax * rc2);  // dependent column (see spd_whiten_kernel)
+            if (tid < nb) fk[tid] = (!drop && tid > k) ? U[k * p + J + tid] / d : 0.0;
+            if (tid == 0) {
+                piv[J + k] = drop ? __longlong_as_double(0x7ff0000000000000ll) : d;
+                bad += drop;
             }
-            if (tid < nb) fk[tid] = (tid > k) ? U[k * p + J + tid] / d : 0.0;
-            if (tid == 0) piv[J + k] = d;
             __syncthreads();
             // rows k2 > k of the panel: U[k2][c] -= f_k2 U[k][c] (c >= J+k2); Ep[k2] -= f_k2 Ep[k]
             for (int k2 = k + 1 + wid; k2 < nb; k2 += kSmallWaves) {
@@ -970,7 +968,6 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
             __syncthreads();
         }
         __syncthreads();
-        if (bad) break;
         // write panel E rows back
         for (int k = wid; k < nb; k += kSmallWaves)
             for (int c = lane; c < J + nb; c += 64) E[(J + k) * p + c] = Ep[k * p + c];
@@ -997,11 +994,7 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
         }
         __syncthreads();
     }
-    if (bad) {
-        if (tid == 0) info[b] = bad;
-        return;
-    }
-    if (tid == 0) info[b] = 0;
+    if (tid == 0) info[b] = bad;
     for (int a2 = wid; a2 < p; a2 += kSmallWaves)
         for (int c = lane; c < p; c += 64) {
             const double v = (c >= a2) ? E[c * p + a2] / sqrt(piv[c]) : 0.0;
@@ -1097,14 +1090,20 @@ int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, 
 
 int cq_spd_whiten(double* S, int64_t p, int64_t batch, float* Wt32, double* Wt64, int* info,
                   void* stream) {
+    return cq_spd_whiten_rcond(S, p, batch, 1e-30, Wt32, Wt64, info, stream);
+}
+
+int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, float* Wt32, double* Wt64, int* info,
+                        void* stream) {
     CQ_REQUIRE(S && p > 0 && batch > 0 && info && Wt64, "cq_spd_whiten: bad args (Wt64 is required scratch)");
+    CQ_REQUIRE(rcond2 >= 0.0, "cq_spd_whiten: rcond2 must be >= 0");
     hipStream_t s = as_stream(stream);
     // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
     const size_t wl = whiten_lds_bytes((int)p);
     if (wl <= 160 * 1024)
-        spd_whiten_blocked_kernel<<<(unsigned)batch, kSmallThreads, wl, s>>>(S, (int)p, Wt64, Wt32, info);
+        spd_whiten_blocked_kernel<<<(unsigned)batch, kSmallThreads, wl, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     else
-        spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, (int)p, Wt64, Wt32, info);
+        spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     if (hipMemcpyAsync(Wt64, S, (size_t)batch * p * p * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
         return set_error(CQ_EHIP, "cq_spd_whiten: copy failed");
     return check_launch("cq_spd_whiten");

@@ -413,9 +413,12 @@ class CalderaEngine:
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
 
-    def _solve_normal(self, M64):
-        """Whitening of the r x r SPD normal matrix; Wt Wt^T = M^{-1}."""
-        Wt32, _, info = K.spd_whiten(M64)
+    def _solve_normal(self, M64, rows: int):
+        """Whitening of the r x r normal matrix A^T A of an lstsq with A (rows x r):
+        Wt Wt^T = M^{-1}; columns of A dependent at gelsy's rcond = eps32 * max(rows, r)
+        (torch.linalg.lstsq's default) are dropped, giving the basic solution."""
+        rc = float(torch.finfo(torch.float32).eps) * max(rows, M64.shape[-1])
+        Wt32, _, info = K.spd_whiten(M64, rcond2=rc * rc)
         return Wt32, info
 
     def _lplr(self, st, Y, res, L0, R0, wts: _Weights):
@@ -449,7 +452,7 @@ class CalderaEngine:
                 Rw = K.scale_rc(R, colscale=wts.ycol) if (aware and wts.ycol is not None) else R
             Bm = K.gemm(Ysrc, Rw, tb=True, C=tmp_mr)            # m x r
             Mr = K.gram_f64(Rw, Rw, ta=True, tb=True)          # r x r
-            Wr, info = self._solve_normal(Mr)
+            Wr, info = self._solve_normal(Mr, n)  # A = (R H_sqrt)^T: n x r
             T1 = K.gemm(Bm, Wr, C=torch.empty_like(tmp_mr))     # (Y Rw^T) Wr
             K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
             # --- quantise L^T as one block (alg.py:171-172)
@@ -463,7 +466,7 @@ class CalderaEngine:
                 L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
             Ml = K.gram_f64(L, L)                              # r x r
-            Wl, info2 = self._solve_normal(Ml)
+            Wl, info2 = self._solve_normal(Ml, m)  # A = L: m x r
             Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
             T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
             K.gemm(Wl, T2, C=Rn)

@@ -79,6 +79,8 @@ EVENT_PROBE = _EventProbe()
 
 
 X3_SCALE = 2.0 ** 6  # power-of-two scale of the filter iterates' fp16 halves (entries <= ~1)
+FILTER_MAX_AMP = 2.0e5  # bound on T_d(t0): config 2's degree-12 steps (T_12(1.6) ~ 1.4e5) stay uncapped
+MAX_OUTER = 40  # outer iterations per solve (the schedule's last degree repeats until converged)
 
 
 class SolverStats:
@@ -132,6 +134,7 @@ class RankRSolver:
         # split-fp16 filter needs K (= k) a multiple of 32 and 16-byte aligned rows
         self.x3 = filter_precision == "f16x3" and not self.direct and self.k % 32 == 0
         self._g_blocked = True  # K-blocked G halves: each K step of a tile is one contiguous run
+        self._x3f = True        # split-fp16 filter for the current outer iteration
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
@@ -206,12 +209,21 @@ class RankRSolver:
         e = np.where(ok, c / 2.0, 1.0)
         ctr = np.where(ok, c / 2.0, 0.0)
         t0 = np.where(ok, (ref - ctr) / e, 2.0)
+        # per-matrix degree cap: the filter amplifies the top of the wanted band by up to
+        # T_d(t0) against its bottom (~1); beyond ~1/eps of the products the wanted directions
+        # near theta_r drown in the top ones and the block degenerates.  Widely spread spectra
+        # (activation-weighted Y, theta_0/theta_r ~ 20 at config 3) thus get low degrees and more
+        # outer iterations; near-flat ones (config 2, t0 ~ 1.6) keep the full schedule.
+        cap = np.maximum(1, np.floor(np.arccosh(FILTER_MAX_AMP) / np.arccosh(np.maximum(t0, 1.0 + 1e-12))))
+        deg = int(min(deg, cap.max()))
         s = 1.0 / t0
         rows = [(s / e, np.zeros_like(s), -s * ctr / e)]
-        for _ in range(1, deg):
+        for i in range(1, deg):
             sn = 1.0 / (2.0 * t0 - s)
-            rows.append((2 * sn / e, -sn * s, -2 * sn * ctr / e))
-            s = sn
+            run = i < cap  # past its cap a matrix's iterate passes through: X_{i+1} = X_i
+            rows.append((np.where(run, 2 * sn / e, 0.0), np.where(run, -sn * s, 0.0),
+                         np.where(run, -2 * sn * ctr / e, 1.0)))
+            s = np.where(run, sn, s)
         tab = torch.from_numpy(np.asarray(rows, dtype=np.float64).astype(np.float32))
         return tab.to(dev)
 
@@ -219,7 +231,7 @@ class RankRSolver:
         """X <- p_d(G) X, p_d = Chebyshev polynomial of degree d = len(coef) damping [0, c],
         c = theta_p, scaled to 1 at theta_0 (scaled 3-term recurrence).  Returns a buffer
         other than X's (X is left intact)."""
-        if self.x3:
+        if self.x3 and self._x3f:
             return self._filter_x3(X, coef)
         G = self._G
         deg = coef.shape[0]
@@ -349,7 +361,10 @@ class RankRSolver:
             degs = self.deg_warm
         self.stats.resid_hist = []
         used = []
-        for d in degs:
+        n_outer = 0
+        while n_outer < MAX_OUTER:
+            d = degs[min(n_outer, len(degs) - 1)]
+            n_outer += 1
             self.stats.outer += 1
             while True:
                 coef = self._cheb_coeffs(ends, d, dev)
@@ -358,19 +373,23 @@ class RankRSolver:
                 Xb, _ = self._cholqr(Xa, X)
                 theta_n, Xn, Zn = self._rr(Xb, X)
                 res = K.ritz_residual(Xn, Zn, theta_n, self.r)  # (B,) per-matrix max residual
-                ovf = self._ovf.max().double() if self.x3 else torch.zeros((), dtype=torch.float64, device=dev)
+                ovf = (self._ovf.max().double() if self.x3 and self._x3f
+                       else torch.zeros((), dtype=torch.float64, device=dev))
                 chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res.double()])
                 yield
                 chk = chk.cpu().numpy()
-                if self.x3 and chk[0] != 0:
-                    # an fp16 half overflowed: redo this outer iteration with the fp32 filter
-                    self.x3 = False
+                if self.x3 and self._x3f and chk[0] != 0:
+                    # an fp16 half overflowed (a Ritz value far below the true top of the
+                    # spectrum, cold start): redo this outer iteration with the fp32 filter
+                    self._x3f = False
+                    self._ovf.zero_()
                     self.stats.x3_fallbacks += 1
                     if self._g_upper_only:  # the fp32 products need the full G
                         self._G.copy_(torch.triu(self._G) + torch.triu(self._G, 1).transpose(1, 2))
                         self._g_upper_only = False
                     continue
                 break
+            self._x3f = True
             theta, X, Z = theta_n, Xn, Zn
             ends = np.stack([chk[1:1 + B], chk[1 + B:1 + 2 * B]], 1)
             resid = chk[1 + 2 * B:]

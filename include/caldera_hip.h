@@ -197,7 +197,14 @@ int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, 
 
 /* SPD whitening by symmetric Gaussian elimination (Cholesky-equivalent):
  * for each b, finds upper-triangular Wt (p x p) with Wt^T S Wt = I, written as fp32
- * (Wt32) and/or fp64 (Wt64).  S is overwritten.  info[b] = 0 ok, j+1 if pivot j <= 0. */
+ * (Wt32) and/or fp64 (Wt64).  S is overwritten.  A pivot <= rcond2 * max_j S_jj (or not
+ * positive) marks a column dependent on the previous ones: it is dropped (its Wt column is
+ * 0), so Wt Wt^T is a generalised inverse and (A^T A) x = A^T y solved through it gives the
+ * basic least-squares solution — torch.linalg.lstsq's gelsy semantics (rcond = eps * max(m,
+ * n) on A, i.e. rcond2 = rcond^2 on the Gram), the rank decision taken in index order.
+ * info[b] = number of dropped pivots (0: full rank).  cq_spd_whiten: rcond2 = 1e-30. */
+int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, float* Wt32, double* Wt64,
+                        int* info, void* stream);
 int cq_spd_whiten(double* S, int64_t p, int64_t batch, float* Wt32, double* Wt64,
                   int* info, void* stream);
 

@@ -172,7 +172,9 @@ def test_solver_filter_precisions(prec, monkeypatch):
     U, th = sv.solve(Y)
     assert sv.stats.max_resid <= 5e-6
     if prec == "overflow":
-        assert sv.stats.x3_fallbacks == 1 and not sv.x3
+        # every overflowing outer iteration is redone with the fp32 filter; the split-fp16
+        # filter stays the default for the next iterations
+        assert sv.stats.x3_fallbacks >= 1 and sv.x3
     elif prec == "f16x3":
         assert sv.x3 and sv.stats.x3_fallbacks == 0
     Yd = Y.double().cpu()

@@ -581,3 +581,29 @@ def test_residual_split_matches_unfused(K, bits, weighted):
     # the transposed halves are (B, n, m) operands stored in (B, m, n)-shaped buffers
     assert torch.equal(thi.view(B, n, m), th_ref) and torch.equal(tlo.view(B, n, m), tl_ref)
     assert torch.allclose(sq, (Ysrc.double() ** 2).sum((1, 2)), rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("p", [24, 200, 300])  # blocked (LDS) and unblocked kernels
+def test_spd_whiten_rank_deficient_is_gelsy_basic_solution(K, p):
+    """lstsq through the normal equations with dependent columns (alg.py:162-177 with a
+    rank-deficient factor, e.g. a 2-bit L with an all-zero column): the dropped pivots give a
+    finite basic solution (dependent coefficients 0) at the least-squares optimum.  (torch's
+    gelsy returns huge cancelling coefficients on exactly dependent fp32 columns, whose fp64
+    residual is above the optimum, so the optimum is taken from an fp64 SVD lstsq.)"""
+    rng = np.random.default_rng(p)
+    m = 4 * p
+    A = rng.standard_normal((m, p)).astype(np.float32)
+    A[:, 5] = 0.0                       # zero column
+    A[:, 7] = 2.0 * A[:, 3]             # exactly dependent column
+    y = rng.standard_normal((m, 3)).astype(np.float32)
+    M = torch.from_numpy(A.astype(np.float64).T @ A.astype(np.float64)).to(DEV).unsqueeze(0)
+    rc = np.finfo(np.float32).eps * m
+    Wt32, Wt64, info = K.spd_whiten(M, rcond2=rc * rc)
+    assert int(info[0]) == 2
+    Wt = Wt64[0].cpu().numpy()
+    x = Wt @ Wt.T @ (A.T.astype(np.float64) @ y)
+    assert np.all(np.isfinite(x)) and np.all(x[5] == 0) and np.all(x[7] == 0)
+    ref = np.linalg.lstsq(A.astype(np.float64), y.astype(np.float64), rcond=None)[0]
+    r_ours = np.linalg.norm(A.astype(np.float64) @ x - y)
+    r_ref = np.linalg.norm(A.astype(np.float64) @ ref - y)
+    assert abs(r_ours - r_ref) <= 1e-6 * r_ref

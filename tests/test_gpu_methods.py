@@ -177,3 +177,17 @@ def test_rand_svd(api):
         dt = caldera(CP(rand_svd=True, **kw), Wt.to(DEV), None, device=DEV, use_tqdm=False)
         rt = O.caldera(O.Params(rand_svd=True, **kw), Wt.numpy())
         np.testing.assert_allclose(dt.errors["LR"], rt.errors["LR"], rtol=0, atol=5e-3)
+
+
+def test_rank_deficient_lplr(api):
+    """W of exact rank 4 < rank 8 with 4-bit factors: the LPLR normal equations are singular
+    (R from LR_init has 4 zero-energy rows); the dropped pivots reproduce gelsy's
+    least-squares error (alg.py:162-177) without NaN."""
+    caldera, CP, _ = api
+    g = torch.Generator().manual_seed(5)
+    W = ((torch.randn(128, 4, generator=g) @ torch.randn(4, 256, generator=g)) * 0.05).half()
+    kw = dict(Q_bits=8, L_bits=4, R_bits=4, rank=8, iters=2, lplr_iters=2, update_order=["LR", "Q"], sigma_reg=1e-8)
+    d = caldera(CP(**kw), W.to(DEV), None, device=DEV, use_tqdm=False)
+    ref = O.caldera(O.Params(**kw), W.numpy())
+    assert all(np.isfinite(d.errors["LR"])) and torch.isfinite(d.L).all() and torch.isfinite(d.R).all()
+    np.testing.assert_allclose(d.errors["LR"], ref.errors["LR"], rtol=0, atol=2e-2)
