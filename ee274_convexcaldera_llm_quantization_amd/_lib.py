@@ -106,6 +106,7 @@ _SIGS = {
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
+    "cq_x3_clock": (c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
@@ -572,12 +573,20 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         g.out_scale = out_scale
         g.overflow = overflow.data_ptr()
     g.tri = int(bool(tri))
-    g.b_blocked = int(bool(b_blocked))
+    g.b_blocked = int(b_blocked)  # 1: K-blocked by 32, 2: by 16 (4-stage kernel only)
     g.active = active.data_ptr() if active is not None else None
-    g.a_blocked = int(bool(a_blocked))
+    g.a_blocked = int(a_blocked)
     g.o_blocked = int(bool(o_blocked))
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
     return C
+
+
+def x3_clock():
+    """(shader ticks, 100 MHz ticks) summed over cq_gemm_x3 workgroups since the last call
+    (only with CQ_X3_CLOCK set when the library was first used); resets the sums."""
+    out = (ctypes.c_ulonglong * 2)()
+    _check(load().cq_x3_clock(out), "cq_x3_clock")
+    return int(out[0]), int(out[1])
 
 
 def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None, bits: int, *, eps: float = 1e-8,

@@ -49,7 +49,12 @@ struct X3K {
     int a_blocked;  // A halves K-blocked [K/32][lda rows][32] (lda = rows)
     int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
     int64_t tiles_n, tiles_m;
+    int probe;  // accumulate shader / constant-clock ticks per workgroup (clock diagnostics)
 };
+
+// clock diagnostics (CQ_X3_CLOCK=1): sum over workgroups of s_memtime (shader clock) and
+// s_memrealtime (100 MHz) ticks; their ratio is the average shader clock under this load
+__device__ unsigned long long cq_clk_acc[2];
 
 __device__ __forceinline__ void x3_load(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
                                         uint4 (&ra)[X3_NA], uint4 (&rb)[X3_NB]) {
@@ -429,6 +434,7 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _F
 
 // The 192 x 384 tile's K loop (shared by the filter/Gram product and the fused Q update):
 // acc = A[m0.., :] B[n0.., :]^T over K, split-fp16 products; nt = 0 leaves acc = 0.
+template <int MODE = 0>
 __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
                                             f32x16v (&acc)[3][2]) {
@@ -443,13 +449,14 @@ __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0,
     uint32_t off[XW_PER_WAVE];
     if (nt > 0) {
         xw_plan(a, m0, n0, wid, lane, off);
-        xw_issue(a, b, 0, smem, wid, off);
+        if (MODE != 2) xw_issue(a, b, 0, smem, wid, off);
     }
     for (int64_t t = 0; t < nt; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
-        if (t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
+        if (MODE != 2 && t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
+        if (MODE == 1) continue;
         const _Float16* sA = smem + (t & 1) * XW_STAGE;
         const _Float16* sB = sA + 2 * XW_APART;
 #pragma unroll
@@ -480,6 +487,120 @@ __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0,
     }
 }
 
+// ------------------------------------------------------------------ 4-stage ring (BK = 16)
+// Same 192 x 384 tile and wave layout, K steps of 16 in a 4-slot ring of 36 KB stages: the
+// loads of steps t+1..t+3 stay in flight while step t computes (counted vmcnt across raw
+// s_barriers), ~108 KB in flight per CU against one 72 KB stage of the 2-stage ring, whose
+// every step waited out a full HBM round trip.  Each wave-instruction fills 32 rows x 32 B
+// (one 16-deep half of a row's 64-B K-block run); the 16-B chunk index is XOR-swizzled by
+// (row >> 3) & 1 on the global source address so the fragment reads are conflict-free.
+constexpr int X4_BK = 16, X4_NS = 4;
+constexpr int X4_APART = XW_BM * X4_BK, X4_BPART = XW_BN * X4_BK;  // halves
+constexpr int X4_STAGE = 2 * X4_APART + 2 * X4_BPART;
+constexpr size_t X4_LDS_BYTES = (size_t)X4_NS * X4_STAGE * sizeof(_Float16);  // 144 KB
+constexpr int X4_PER_WAVE = (2 * XW_BM / 32 + 2 * XW_BN / 32) / (XW_THREADS / 64);  // 3
+static_assert(X4_PER_WAVE == 3, "vmcnt counts below assume 3 loads per wave per stage");
+static_assert(X4_LDS_BYTES <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ void x4_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
+                                        uint32_t (&off)[X4_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < X4_PER_WAVE; ++u) {
+        const int I = wid * X4_PER_WAVE + u;  // 0..35: Ah 0-5, Al 6-11, Bh 12-23, Bl 24-35
+        const bool isA = I < 12;
+        const int part = isA ? (I >= 6) : (I >= 24);
+        const int sub = isA ? (I - 6 * part) : (I - 12 - 12 * part);
+        const int row = 32 * sub + (lane >> 1);
+        const int c = (lane & 1) ^ ((row >> 3) & 1);
+        const int64_t lim = isA ? a.M : a.N;
+        int64_t gr = (isA ? m0 : n0) + row;
+        gr = gr < lim ? gr : lim - 1;  // clamp: rows past the edge feed only unstored outputs
+        const int bw = isA ? (a.a_blocked == 2 ? 16 : 32) : (a.b_blocked == 2 ? 16 : 32);
+        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * bw + c * 8 : gr * a.lda + c * 8)
+                                : (a.b_blocked ? gr * bw + c * 8 : gr * a.ldb + c * 8));
+    }
+}
+
+__device__ __forceinline__ void x4_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                         const uint32_t (&off)[X4_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < X4_PER_WAVE; ++u) {
+        const int I = wid * X4_PER_WAVE + u;
+        const bool isA = I < 12;
+        const int part = isA ? (I >= 6) : (I >= 24);
+        const int sub = isA ? (I - 6 * part) : (I - 12 - 12 * part);
+        const int64_t kb = (k0 >> 5) * 32, kr = k0 & 31;
+        const int64_t ka = a.a_blocked == 2 ? k0 * a.lda : kb * a.lda + kr;  // 16-blocked: k0 % 16 == 0
+        const int64_t kbb = a.b_blocked == 2 ? k0 * a.ldb : kb * a.ldb + kr;
+        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? ka : k0)
+                                   : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? kbb : k0);
+        _Float16* dst = stage + (isA ? part * X4_APART : 2 * X4_APART + part * X4_BPART) + (32 * sub) * X4_BK;
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
+                                         16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ f16x8 x4_frag(const _Float16* img, int row, int chunk) {
+    const int pc = chunk ^ ((row >> 3) & 1);
+    return *reinterpret_cast<const f16x8*>(img + row * X4_BK + pc * 8);
+}
+
+template <int MODE = 0>
+__device__ __forceinline__ void x4_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
+                                            _Float16* smem, int wid, int lane, int wm, int wn,
+                                            f32x16v (&acc)[3][2]) {
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    wid = __builtin_amdgcn_readfirstlane(wid);
+    uint32_t off[X4_PER_WAVE];
+    if (nt > 0) {
+        x4_plan(a, m0, n0, wid, lane, off);
+        if (MODE != 2)
+            for (int64_t s = 0; s < X4_NS - 1 && s < nt; ++s) x4_issue(a, b, s * X4_BK, smem + s * X4_STAGE, wid, off);
+    }
+    for (int64_t t = 0; t < nt; ++t) {
+        // stage t landed (this wave's part); the stages issued after it stay in flight
+        const int64_t after = nt - 1 - t;
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's part of stage t landed; slot of t-1 fully read
+        if (MODE != 2 && t + X4_NS - 1 < nt)
+            x4_issue(a, b, (t + X4_NS - 1) * X4_BK, smem + ((t + X4_NS - 1) & (X4_NS - 1)) * X4_STAGE, wid, off);
+        if (MODE == 1) continue;
+        const _Float16* sA = smem + (t & (X4_NS - 1)) * X4_STAGE;
+        const _Float16* sB = sA + 2 * X4_APART;
+        f16x8 ah[3], al[3], bh[2], bl[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = 64 * wn + 32 * j + lr;
+            bh[j] = x4_frag(sB, row, lh);
+            bl[j] = x4_frag(sB + X4_BPART, row, lh);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int row = 96 * wm + 32 * i + lr;
+            ah[i] = x4_frag(sA, row, lh);
+            al[i] = x4_frag(sA + X4_APART, row, lh);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+    }
+}
+
+template <int NS, int MODE = 0>
 __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
     extern __shared__ __attribute__((aligned(16))) char xw_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(xw_smem_raw);
@@ -496,11 +617,13 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
     const int lr = lane & 31, lh = lane >> 5;
+    unsigned long long c0 = 0, r0 = 0;
+    if (a.probe && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
 
     f32x16v acc[3][2];
     const bool live = !a.active || a.active[b];
-    const int64_t nt = live ? a.K / XW_BK : 0;
-    xw_mainloop(a, b, m0, n0, nt, smem, wid, lane, wm, wn, acc);
+    if (NS == 2) xw_mainloop<MODE>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+    else x4_mainloop<MODE>(a, b, m0, n0, live ? a.K / X4_BK : 0, smem, wid, lane, wm, wn, acc);
 
     const float sc = a.inv_scale[b];
     // inactive entries (converged matrices) pass D through unchanged
@@ -535,6 +658,159 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
             }
         }
     if (ovf) atomicOr(a.overflow + b, 1);
+    if (a.probe && threadIdx.x == 0) {
+        atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
+        atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
+    }
+}
+
+
+// ------------------------------------------------------------------ 16x16x32 MFMA variant
+// Same tile, ring and LDS image as gemm_x3w_kernel; each wave's 96 x 64 block is 6 x 4
+// v_mfma_f32_16x16x32_f16 tiles (one MFMA per 32-deep K step and product instead of two
+// 32x32x16).  Under the chip's power limit the 16x16x32 form runs at a higher clock for the
+// same work (MI355X_MICROARCH.md: ~1.15x the FLOP/s of 32x32x16 in bare loops).
+__device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
+                                            _Float16* smem, int wid, int lane, int wm, int wn,
+                                            f32x4v (&acc)[6][4]) {
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    wid = __builtin_amdgcn_readfirstlane(wid);
+    uint32_t off[XW_PER_WAVE];
+    if (nt > 0) {
+        xw_plan(a, m0, n0, wid, lane, off);
+        xw_issue(a, b, 0, smem, wid, off);
+    }
+    for (int64_t t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
+        if (t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
+        const _Float16* sA = smem + (t & 1) * XW_STAGE;
+        const _Float16* sB = sA + 2 * XW_APART;
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 64 * wn + 16 * j + l16;
+            bh[j] = xg_frag(sB, row, lq);
+            bl[j] = xg_frag(sB + XW_BPART, row, lq);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int row = 96 * wm + 16 * i + l16;
+            const f16x8 ah = xg_frag(sA, row, lq);
+            const f16x8 al = xg_frag(sA + XW_APART, row, lq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // transposed block: lanes run over A rows, registers over B rows
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char xv_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(xv_smem_raw);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+    const int64_t tn = lin % a.tiles_n;
+    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
+    const int64_t b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
+    if (a.tri && n0 + XW_BN <= m0) return;
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
+    const int l16 = lane & 15, lq = lane >> 4;
+    unsigned long long c0 = 0, r0 = 0;
+    if (a.probe && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+
+    f32x4v acc[6][4];
+    const bool live = !a.active || a.active[b];
+    xv_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+
+    const float sc = a.inv_scale[b];
+    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
+    bool ovf = false;
+    // lane = C row (A row), registers r = 4 consecutive C columns: 16-byte fp32 and 8-byte
+    // fp16 accesses (host guarantees N % 4 == 0 and 16-byte aligned rows)
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    auto al8 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; };
+    const bool vec = (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.sc & 3) == 0 && al16(a.C) &&
+                     (!a.P || ((a.ldp & 3) == 0 && (a.sp & 3) == 0 && al16(a.P))) &&
+                     (!a.D || ((a.ldd & 3) == 0 && (a.sd & 3) == 0 && al16(a.D))) &&
+                     (!a.Oh || ((a.o_blocked || (a.ldo & 3) == 0) && (a.so & 3) == 0 && al8(a.Oh) && al8(a.Ol)));
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int64_t row = m0 + 96 * wm + 16 * i + l16;
+        if (row >= a.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t col = n0 + 64 * wn + 16 * j + 4 * lq;
+            if (col >= a.N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = al_ * (acc[i][j][r] * sc);
+            if (vec) {
+                if (a.P && be_ != 0.f) {
+                    const float4 pv = *reinterpret_cast<const float4*>(a.P + b * a.sp + row * a.ldp + col);
+                    v[0] += be_ * pv.x; v[1] += be_ * pv.y; v[2] += be_ * pv.z; v[3] += be_ * pv.w;
+                }
+                if (a.D && ga_ != 0.f) {
+                    const float4 dv = *reinterpret_cast<const float4*>(a.D + b * a.sd + row * a.ldd + col);
+                    v[0] += ga_ * dv.x; v[1] += ga_ * dv.y; v[2] += ga_ * dv.z; v[3] += ga_ * dv.w;
+                }
+                *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) = make_float4(v[0], v[1], v[2], v[3]);
+                if (a.Oh) {
+                    _Float16 h[4], l[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float hs = v[r] * a.out_scale;
+                        h[r] = (_Float16)hs;
+                        l[r] = (_Float16)(hs - (float)h[r]);
+                        ovf |= !(fabsf(hs) < 65504.f);
+                    }
+                    const int64_t o = b * a.so + (a.o_blocked ? (col >> 5) * (a.M * 32) + row * 32 + (col & 31)
+                                                              : row * a.ldo + col);
+                    *reinterpret_cast<uint2*>(a.Oh + o) = *reinterpret_cast<const uint2*>(h);
+                    *reinterpret_cast<uint2*>(a.Ol + o) = *reinterpret_cast<const uint2*>(l);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t c = col + r;
+                    if (c >= a.N) continue;
+                    float w = v[r];
+                    if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + c];
+                    if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + c];
+                    a.C[b * a.sc + row * a.ldc + c] = w;
+                    if (a.Oh) {
+                        const float hs = w * a.out_scale;
+                        const _Float16 h = (_Float16)hs;
+                        const int64_t o = b * a.so + (a.o_blocked ? (c >> 5) * (a.M * 32) + row * 32 + (c & 31)
+                                                                  : row * a.ldo + c);
+                        a.Oh[o] = h;
+                        a.Ol[o] = (_Float16)(hs - (float)h);
+                        ovf |= !(fabsf(hs) < 65504.f);
+                    }
+                }
+            }
+        }
+    }
+    if (ovf) atomicOr(a.overflow + b, 1);
+    if (a.probe && threadIdx.x == 0) {
+        atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
+        atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
+    }
 }
 
 
@@ -1187,6 +1463,17 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     return check_launch("cq_residual_split");
 }
 
+// clock diagnostics: returns the accumulated (shader ticks, 100 MHz ticks) and zeroes them
+int cq_x3_clock(unsigned long long* out) {
+    CQ_REQUIRE(out, "cq_x3_clock: null");
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cq_clk_acc), sizeof(unsigned long long) * 2) != hipSuccess)
+        return set_error(CQ_EHIP, "cq_x3_clock: copy failed");
+    const unsigned long long z[2] = {0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cq_clk_acc), z, sizeof(z)) != hipSuccess)
+        return set_error(CQ_EHIP, "cq_x3_clock: reset failed");
+    return 0;
+}
+
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(g, "cq_gemm_x3: null args");
     CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && g->C && g->inv_scale, "cq_gemm_x3: null operand");
@@ -1222,25 +1509,39 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.active = g->active;
     a.a_blocked = g->a_blocked;
     a.o_blocked = g->o_blocked;
+    static const int probe = getenv("CQ_X3_CLOCK") ? 1 : 0;
+    a.probe = probe;
     CQ_REQUIRE(!g->o_blocked || g->N % 32 == 0, "cq_gemm_x3: blocked split output needs N % 32 == 0");
     CQ_REQUIRE(!g->a_blocked || g->lda >= g->M, "cq_gemm_x3: blocked A needs lda = rows >= M");
     CQ_REQUIRE(!g->active || g->D, "cq_gemm_x3: active needs D (the pass-through value)");
     CQ_REQUIRE(!g->b_blocked || g->ldb >= g->N, "cq_gemm_x3: blocked B needs ldb = rows >= N");
     static const int variant = [] {
         // A/B switch for benchmarking: "reg" register-staged 192x256, "g" LDS-DMA 192x192,
-        // default LDS-DMA 192x384
+        // "w2" LDS-DMA 192x384 2-stage ring on 32x32x16 MFMAs, "w4" 4-stage ring at BK 16
+        // (slower: 2.80 vs 2.52 ms per B = 128 filter product, tools/bench_filter.py); default
+        // ("v") the 2-stage ring on 16x16x32 MFMAs with the transposed, vectorised epilogue
+        // (2.66 vs 3.20 ms for the filter step)
         const char* e = getenv("CQ_X3_KERNEL");
-        if (!e) return 2;
-        return e[0] == 'r' ? 1 : e[0] == 'g' ? 0 : 2;
+        if (!e) return 8;
+        if (e[0] == 'w' && e[1] == '2') return e[2] == 'l' ? 4 : e[2] == 'm' ? 5 : 2;  // w2l / w2m: ablations
+        if (e[0] == 'w' && e[1] == '4') return e[2] == 'l' ? 6 : e[2] == 'm' ? 7 : 3;
+        if (e[0] == 'v') return 8;
+        return e[0] == 'r' ? 1 : e[0] == 'g' ? 0 : 3;
     }();
-    CQ_REQUIRE(variant == 2 || (!g->a_blocked && !g->o_blocked),
+    CQ_REQUIRE(variant >= 2 || (!g->a_blocked && !g->o_blocked),
                "cq_gemm_x3: blocked A / split output need the LDS-DMA 192x384 kernel");
-    if (variant == 2) {
+    if (variant >= 2) {
         a.tiles_n = ceil_div(g->N, XW_BN);
         a.tiles_m = ceil_div(g->M, XW_BM);
         const int64_t total = a.tiles_n * a.tiles_m * a.batch;
         CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-        gemm_x3w_kernel<<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        if (variant == 2) gemm_x3w_kernel<2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 4) gemm_x3w_kernel<2, 1><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 5) gemm_x3w_kernel<2, 2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 6) gemm_x3w_kernel<4, 1><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 7) gemm_x3w_kernel<4, 2><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 8) gemm_x3v_kernel<<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else gemm_x3w_kernel<4><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
     } else if (variant == 0 || g->b_blocked) {
         a.tiles_n = ceil_div(g->N, XG_BN);
         a.tiles_m = ceil_div(g->M, XG_BM);

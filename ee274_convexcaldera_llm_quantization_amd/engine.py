@@ -220,7 +220,7 @@ class BatchState:
 class CalderaEngine:
     """Decomposes a batch of B weight matrices (B, m, n) with shared params and H."""
 
-    def __init__(self, params: EngineParams, *, solver_tol: float = 5e-6, solver_p: int | None = None,
+    def __init__(self, params: EngineParams, *, solver_tol: float = 1e-5, solver_p: int | None = None,
                  filter_precision: str = "f16x3", profile: bool = False, solver_kwargs: dict | None = None):
         self.p = params
         self.solver_kwargs = dict(solver_kwargs or {})

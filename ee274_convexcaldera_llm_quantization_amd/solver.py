@@ -102,7 +102,7 @@ class RankRSolver:
     """Top-r eigenpairs of the Gram of a batch of matrices, warm-started across calls."""
 
     def __init__(self, B: int, m: int, n: int, r: int, device, *, p: int | None = None,
-                 tol: float = 5e-6, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 6, 6, 6, 6, 6),
+                 tol: float = 1e-5, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 6, 6, 6, 6, 6),
                  seed: int = 0x5EED, jacobi_tol: float = 1e-10, filter_precision: str = "f16x3"):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)

@@ -281,6 +281,12 @@ typedef struct cq_x3_args {
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
 
+/* Diagnostics: with the environment variable CQ_X3_CLOCK set at load time, every cq_gemm_x3
+ * workgroup adds its shader-clock (s_memtime) and 100 MHz (s_memrealtime) tick counts to a
+ * device accumulator; this returns both sums and zeroes them (out[0] / out[1] * 100 MHz is
+ * the average shader clock under that load).  No reference counterpart. */
+int cq_x3_clock(unsigned long long* out);
+
 /* out[b] = max |X[b]| (n_per values, fp16 or fp32), NaN sorting above inf. */
 int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out, void* stream);
 
