@@ -59,6 +59,10 @@ class X3Args(ctypes.Structure):
         ("active", c_vp),
         ("a_blocked", c_int),
         ("o_blocked", c_int),
+        ("sym_out", c_int),
+        ("out_bound", c_vp),
+        ("scale_out", c_vp),
+        ("inv_out", c_vp),
     ]
 
 
@@ -241,21 +245,24 @@ def quantize_known_max(x, absmax_bits, bits, eps=1e-8, *, codes=None, packed=Non
 
 
 def dequantize_uniform(codes: torch.Tensor, scale: torch.Tensor, bits: int, packed: bool = False,
-                       numel: int | None = None) -> torch.Tensor:
+                       numel: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """(float(c)/k) * scale per block; codes (..., ) int8/int16 or packed uint8; scale (nblocks,)."""
-    _require_hip(codes, scale)
+    _require_hip(codes, scale, out)
     total = numel if numel is not None else codes.numel()
     nb = scale.numel()
-    out = torch.empty(total, dtype=torch.float32, device=codes.device)
+    if out is None:
+        out = torch.empty(total, dtype=torch.float32, device=codes.device)
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == total
     _check(load().cq_dequant_uniform(_p(codes), int(packed), _p(scale), total, total // nb, bits, _p(out),
                                      _stream(codes.device)), "cq_dequant_uniform")
     return out
 
 
-def unpack_codes(packed: torch.Tensor, numel: int, bits: int) -> torch.Tensor:
-    _require_hip(packed)
+def unpack_codes(packed: torch.Tensor, numel: int, bits: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    _require_hip(packed, out)
     B = packed.shape[0]
-    codes = torch.empty((B, numel), dtype=torch.int8, device=packed.device)
+    codes = torch.empty((B, numel), dtype=torch.int8, device=packed.device) if out is None else out
+    assert codes.shape == (B, numel) and codes.dtype == torch.int8 and codes.is_contiguous()
     _check(load().cq_unpack_codes(_p(packed), B, numel, bits, _p(codes), _stream(packed.device)),
            "cq_unpack_codes")
     return codes
@@ -545,14 +552,17 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
-            a_blocked=False, o_blocked=False):
+            a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
-    same storage size); optional fp16 split of C into out_h/out_l."""
+    same storage size); optional fp16 split of C into out_h/out_l.
+    sym_bound (B,) fp64: symmetric Gram mode (tri): the K-blocked split of C is written from
+    its upper triangle with scale s[b] from the bound (scale_out, inv_out = 1/(s out_scale));
+    C may then be None."""
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, M, Kd = Ah.shape
     N = Bh.shape[1]
-    assert Bh.shape[2] == Kd and C.shape == (Bt, M, N)
+    assert Bh.shape[2] == Kd and (C is None or C.shape == (Bt, M, N))
     for t in (Ah, Al, Bh, Bl, C, P, D, out_h, out_l):
         assert t is None or t.is_contiguous()
     g = X3Args()
@@ -560,7 +570,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (M if a_blocked else Kd), M * Kd
     g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), (N if b_blocked else Kd), N * Kd
     g.inv_scale = inv_scale.data_ptr()
-    g.C, g.ldc, g.stride_c = C.data_ptr(), N, M * N
+    g.C, g.ldc, g.stride_c = (C.data_ptr() if C is not None else None), N, M * N
     if P is not None:
         g.P, g.ldp, g.stride_p = P.data_ptr(), N, M * N
     if D is not None:
@@ -568,7 +578,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.alpha_v = alpha_v.data_ptr() if alpha_v is not None else None
     g.beta_v = beta_v.data_ptr() if beta_v is not None else None
     g.gamma_v = gamma_v.data_ptr() if gamma_v is not None else None
-    if out_h is not None:
+    if out_h is not None and sym_bound is None:
         g.out_h, g.out_l, g.ldo, g.stride_o = out_h.data_ptr(), out_l.data_ptr(), N, M * N
         g.out_scale = out_scale
         g.overflow = overflow.data_ptr()
@@ -577,7 +587,12 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.active = active.data_ptr() if active is not None else None
     g.a_blocked = int(a_blocked)
     g.o_blocked = int(bool(o_blocked))
-    _check(load().cq_gemm_x3(ctypes.byref(g), _stream(C.device)), "cq_gemm_x3")
+    if sym_bound is not None:
+        g.sym_out = 1
+        g.out_bound, g.scale_out, g.inv_out = sym_bound.data_ptr(), scale_out.data_ptr(), inv_out.data_ptr()
+        g.out_h, g.out_l, g.ldo, g.stride_o = out_h.data_ptr(), out_l.data_ptr(), N, M * N
+        g.out_scale = out_scale
+    _check(load().cq_gemm_x3(ctypes.byref(g), _stream(Ah.device)), "cq_gemm_x3")
     return C
 
 

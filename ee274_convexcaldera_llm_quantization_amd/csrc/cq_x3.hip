@@ -50,7 +50,17 @@ struct X3K {
     int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
     int64_t tiles_n, tiles_m;
     int probe;  // accumulate shader / constant-clock ticks per workgroup (clock diagnostics)
+    int sym_out;               // tri Gram: write the blocked split of the symmetric C (mirrored upper)
+    const double* out_bound;   // [batch] bound on max|C|: split scale 2^(14 - e)
+    float* scale_out;          // [batch] that scale
+    float* inv_out;            // [batch] 1 / (scale * out_scale)
 };
+
+__device__ __forceinline__ float sym_split_scale(double bound) {
+    int e = 0;
+    if (bound > 0.0 && isfinite(bound)) frexp(bound, &e);
+    return ldexpf(1.f, 14 - e);
+}
 
 // clock diagnostics (CQ_X3_CLOCK=1): sum over workgroups of s_memtime (shader clock) and
 // s_memrealtime (100 MHz) ticks; their ratio is the average shader clock under this load
@@ -737,6 +747,61 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     xv_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
 
     const float sc = a.inv_scale[b];
+    if (a.sym_out) {
+        // symmetric Gram: entries on/above the diagonal are written at (row, col) and, mirrored,
+        // at (col, row) of the K-blocked split (the lower triangle of a straddling tile is not
+        // used, so the split is exactly symmetric); (fp32 C too if given)
+        const float gs = sym_split_scale(a.out_bound[b]);
+        if (tm == 0 && tn == 0 && threadIdx.x == 0) {
+            a.scale_out[b] = gs;
+            a.inv_out[b] = 1.f / (gs * a.out_scale);
+        }
+        const int64_t M = a.M;
+        _Float16* Oh = a.Oh + b * a.so;
+        _Float16* Ol = a.Ol + b * a.so;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int64_t row = m0 + 96 * wm + 16 * i + l16;
+            if (row >= M) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t col = n0 + 64 * wn + 16 * j + 4 * lq;
+                if (col + 3 < row || col >= a.N) continue;
+                _Float16 h[4], l[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = acc[i][j][r] * sc;
+                    if (a.C && col + r >= row && col + r < a.N) a.C[b * a.sc + row * a.ldc + col + r] = v;
+                    const float hs = v * gs;
+                    h[r] = (_Float16)hs;
+                    l[r] = (_Float16)(hs - (float)h[r]);
+                }
+                const int64_t o = (col >> 5) * (M * 32) + row * 32 + (col & 31);
+                if (col >= row && col + 3 < a.N) {
+                    *reinterpret_cast<uint2*>(Oh + o) = *reinterpret_cast<const uint2*>(h);
+                    *reinterpret_cast<uint2*>(Ol + o) = *reinterpret_cast<const uint2*>(l);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (col + r >= row && col + r < a.N) { Oh[o + r] = h[r]; Ol[o + r] = l[r]; }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {  // mirror (col + r, row)
+                    const int64_t c = col + r;
+                    if (c > row && c < a.N) {
+                        const int64_t om = (row >> 5) * (M * 32) + c * 32 + (row & 31);
+                        Oh[om] = h[r];
+                        Ol[om] = l[r];
+                    }
+                }
+            }
+        }
+        if (a.probe && threadIdx.x == 0) {
+            atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
+            atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
+        }
+        return;
+    }
     const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
     const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
     const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
@@ -1476,7 +1541,10 @@ int cq_x3_clock(unsigned long long* out) {
 
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(g, "cq_gemm_x3: null args");
-    CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && g->C && g->inv_scale, "cq_gemm_x3: null operand");
+    CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && (g->C || g->sym_out) && g->inv_scale, "cq_gemm_x3: null operand");
+    CQ_REQUIRE(!g->sym_out || (g->tri && g->out_h && g->out_l && g->out_bound && g->scale_out && g->inv_out &&
+                               g->out_scale > 0.f && g->N % 32 == 0),
+               "cq_gemm_x3: sym_out needs tri, out_h/out_l, out_bound, scale_out, inv_out, N % 32 == 0");
     CQ_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0 && g->batch > 0, "cq_gemm_x3: bad shape");
     CQ_REQUIRE(g->K % X3_BK == 0, "cq_gemm_x3: K must be a multiple of 32");
     CQ_REQUIRE(g->lda % 8 == 0 && g->ldb % 8 == 0 && g->stride_a % 8 == 0 && g->stride_b % 8 == 0,
@@ -1485,7 +1553,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
                    g->ldc >= g->N,
                "cq_gemm_x3: leading dimension too small");
     CQ_REQUIRE(!g->out_h == !g->out_l, "cq_gemm_x3: out_h and out_l go together");
-    CQ_REQUIRE(!g->out_h || (g->overflow && g->out_scale > 0.f), "cq_gemm_x3: split output needs overflow flags");
+    CQ_REQUIRE(!g->out_h || g->sym_out || (g->overflow && g->out_scale > 0.f),
+               "cq_gemm_x3: split output needs overflow flags");
     CQ_REQUIRE(!g->beta_v || g->P, "cq_gemm_x3: beta_v needs P");
     CQ_REQUIRE(!g->gamma_v || g->D, "cq_gemm_x3: gamma_v needs D");
     X3K a;
@@ -1502,8 +1571,12 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.Oh = reinterpret_cast<_Float16*>(g->out_h); a.Ol = reinterpret_cast<_Float16*>(g->out_l);
     a.ldo = g->ldo; a.so = g->stride_o; a.out_scale = g->out_scale;
     a.overflow = g->overflow;
-    CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && !g->out_h),
+    CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && (!g->out_h || g->sym_out)),
                "cq_gemm_x3: tri needs a square plain product");
+    a.sym_out = g->sym_out;
+    a.out_bound = g->out_bound;
+    a.scale_out = g->scale_out;
+    a.inv_out = g->inv_out;
     a.tri = g->tri;
     a.b_blocked = g->b_blocked;
     a.active = g->active;
@@ -1530,6 +1603,7 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     }();
     CQ_REQUIRE(variant >= 2 || (!g->a_blocked && !g->o_blocked),
                "cq_gemm_x3: blocked A / split output need the LDS-DMA 192x384 kernel");
+    CQ_REQUIRE(variant == 8 || !g->sym_out, "cq_gemm_x3: sym_out needs the default kernel");
     if (variant >= 2) {
         a.tiles_n = ceil_div(g->N, XW_BN);
         a.tiles_m = ceil_div(g->M, XW_BM);

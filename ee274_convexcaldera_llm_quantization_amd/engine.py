@@ -346,7 +346,7 @@ class CalderaEngine:
             K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
                              ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
                              res=res, Y=Y if weighted else None, scale=self._ys, sq=ysq, **halves)
-            y_split = (self._yh, self._yl, self._ys)
+            y_split = (self._yh, self._yl, self._ys, ysq)
         else:
             K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
@@ -595,7 +595,7 @@ class CalderaEngine:
         if self.solver is not None:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         self._yh = self._yl = None
-        return self._finalize(best, st, W, Ws, gs, errors, wts)
+        return self._finalize(best, st, W, Ws, gs, errors, wts, spare=(work, res))
 
     def _state_error(self, st, Ws, work, wts):
         B, m, n = st.B, st.m, st.n
@@ -613,7 +613,11 @@ class CalderaEngine:
         K.gemm(st.L, st.R, D=work, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
 
-    def _finalize(self, best, st, W, Ws, gs, errors, wts):
+    def _finalize(self, best, st, W, Ws, gs, errors, wts, spare=(None, None)):
+        """Per-matrix result dicts.  `best` is allocated by this run, so the results are views
+        of its batched tensors (no per-matrix copies); uniform Q is unpacked and dequantised
+        for the whole batch in one launch each, into this run's B x m x n work buffers (no
+        large allocation at the end of a run)."""
         p = self.p
         B, m, n = best.B, best.m, best.n
         dev = W.device
@@ -621,41 +625,50 @@ class CalderaEngine:
         gsl = gs.tolist()
         qs = best.Qs.tolist()
         # compact (storage / gather) form: packed codes as kept by the engine
-        self.last_packed = [dict(codes=best.Qc[b].clone(), Q_scale=qs[b], L=best.L[b].clone(),
-                                 R=best.R[b].clone(), global_scale=gsl[b],
+        self.last_packed = [dict(codes=best.Qc[b], Q_scale=qs[b], L=best.L[b], R=best.R[b], global_scale=gsl[b],
                                  errors={k: v[b] for k, v in errors.items()})
                             for b in range(B)]
+        codes_all = Qall = None
+        if not best.dense_q and any(best.flag_Q):
+            work, res = spare
+            if best.q_packed:
+                cbuf = None
+                if res is not None and res.is_contiguous():
+                    cbuf = res.view(-1).view(torch.int8)[: B * m * n].view(B, m * n)
+                codes_all = K.unpack_codes(best.Qc, m * n, p.Q_bits, out=cbuf)
+            else:
+                codes_all = best.Qc
+            # dequantize_block (quantization.py:103-105) on the reference int codes
+            qbuf = work.view(-1) if work is not None and work.is_contiguous() else None
+            Qall = K.dequantize_uniform(codes_all, best.Qs, p.Q_bits, out=qbuf).view(B, m, n)
         for b in range(B):
             d = {}
             if best.flag_Q[b] and best.dense_q:
-                d["Q"] = best.Qd[b].clone()
+                d["Q"] = best.Qd[b]
                 d["Q_idxs"], d["Q_scale"] = best.q_items[b]
             elif best.flag_Q[b]:
-                qc = best.Qc[b:b + 1]
-                codes = K.unpack_codes(qc, m * n, p.Q_bits) if best.q_packed else qc.clone()
-                # dequantize_block (quantization.py:103-105) on the reference int codes
-                d["Q"] = K.dequantize_uniform(codes, best.Qs[b:b + 1], p.Q_bits).view(m, n)
-                d["Q_idxs"] = codes.view(1, m * n)
-                d["Q_scale"] = best.Qs[b].view(1, 1).clone()
+                d["Q"] = Qall[b]
+                d["Q_idxs"] = codes_all[b].view(1, m * n)
+                d["Q_scale"] = best.Qs[b].view(1, 1)
             else:
                 d["Q"] = torch.zeros((m, n), dtype=torch.float32, device=dev)
                 d["Q_idxs"] = None
                 d["Q_scale"] = 1
-            d["L"] = best.L[b].clone()
-            d["R"] = best.R[b].clone()
+            d["L"] = best.L[b]
+            d["R"] = best.R[b]
             if isinstance(best.L_idxs, list) and best.flag_LR[b] and best.L_idxs[b] is not None:
                 d["L_idxs"], d["R_idxs"] = best.L_idxs[b], best.R_idxs[b]
                 d["L_scale"], d["R_scale"] = best.L_scale[b], best.R_scale[b]
             elif torch.is_tensor(best.L_idxs) and best.flag_LR[b]:
-                d["L_idxs"] = best.L_idxs[b].view(1, -1).clone()
-                d["R_idxs"] = best.R_idxs[b].view(1, -1).clone()
-                d["L_scale"] = best.L_scale[b].view(1, 1).clone()
-                d["R_scale"] = best.R_scale[b].view(1, 1).clone()
+                d["L_idxs"] = best.L_idxs[b].view(1, -1)
+                d["R_idxs"] = best.R_idxs[b].view(1, -1)
+                d["L_scale"] = best.L_scale[b].view(1, 1)
+                d["R_scale"] = best.R_scale[b].view(1, 1)
             else:
                 d["L_idxs"] = d["R_idxs"] = None
                 d["L_scale"] = d["R_scale"] = 1
             d["W"] = Ws[b]
-            d["global_scale"] = gsl[b] if True else 1
+            d["global_scale"] = gsl[b]
             d["errors"] = {k: v[b] for k, v in errors.items()}
             out.append(d)
         return out

@@ -142,7 +142,9 @@ class RankRSolver:
         if self._bufs is None:
             # 5 buffers: an outer iteration keeps its input alive until its overflow check
             self._bufs = [torch.empty((B, k, p), dtype=torch.float32, device=dev) for _ in range(5)]
-            self._G = torch.empty((B, k, k), dtype=torch.float32, device=dev)
+            # fp32 G only for the fp32 products (the split-fp16 path keeps G as its halves and
+            # allocates it on an fp16 overflow fallback)
+            self._G = None if self.x3 else torch.empty((B, k, k), dtype=torch.float32, device=dev)
             if self.x3:
                 f16 = torch.float16
                 self._Gh = torch.empty((B, k, k), dtype=f16, device=dev)
@@ -170,6 +172,13 @@ class RankRSolver:
         for name in ("_Gh", "_Gl", "_xt", "_xh", "_xl"):
             if hasattr(self, name):
                 setattr(self, name, None)
+
+    def _fill_G(self, Y):
+        """fp32 G = Y Y^T (m <= n) or Y^T Y on the fp32 MFMA GEMM (upper tiles + mirror)."""
+        if self.left:
+            K.gemm(Y, Y, tb=True, C=self._G, syrk=True)
+        else:
+            K.gemm(Y, Y, ta=True, C=self._G, syrk=True)
 
     # ------------------------------------------------------------------ steps
     def _cholqr(self, X, *keep):
@@ -297,8 +306,9 @@ class RankRSolver:
 
     def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None):
         """Generator form of solve(): yields before each host synchronisation (overlap.py).
-        y_split: optional (hi, lo, scale) K-blocked split-fp16 halves of the Gram operand (Y
-        for m <= n, Y^T otherwise) already produced by the caller (cq_residual_split)."""
+        y_split: optional (hi, lo, scale, sq) K-blocked split-fp16 halves of the Gram operand (Y
+        for m <= n, Y^T otherwise) and ||Y||_F^2 (fp64, or None) already produced by the caller
+        (cq_residual_split)."""
         B, k, p = self.B, self.k, self.p
         dev = Y.device
         self.stats.calls += 1
@@ -308,10 +318,14 @@ class RankRSolver:
             return V32[:, :, : self.r], theta[:, : self.r]
         self._alloc(dev)
         self._g_upper_only = False
+        self._Y = Y
+        g_split = False
         if self.x3 and (self.n if self.left else self.m) % 32 == 0:
-            # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two
+            # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two;
+            # the Gram writes G's K-blocked split halves itself (scale from ||Y||_F^2 >= max|G|)
+            ysq = None
             if y_split is not None:
-                yh, yl, ys = y_split
+                yh, yl, ys, ysq = y_split
             else:
                 if self._yh is None:
                     self._yh = torch.empty((B, k, Y.shape[1] + Y.shape[2] - k), dtype=torch.float16, device=dev)
@@ -324,17 +338,23 @@ class RankRSolver:
                 else:
                     K.transpose_split(Y, hi=yh, lo=yl, scale=ys, blocked=True)
             yinv = 1.0 / (ys * ys)
-            K.gemm_x3(yh, yl, yh, yl, yinv, self._G, tri=True,  # upper triangle
-                      a_blocked=True, b_blocked=True)
-            self._g_upper_only = True
-        elif self.left:
-            K.gemm(Y, Y, tb=True, C=self._G, syrk=True)  # Y Y^T (upper tiles + mirror)
-        else:
-            K.gemm(Y, Y, ta=True, C=self._G, syrk=True)  # Y^T Y
+            if ysq is None:
+                ysq = K.weighted_sqsum(Y, None, Y.shape[2])
+            K.gemm_x3(yh, yl, yh, yl, yinv, None, tri=True, a_blocked=True, b_blocked=True,
+                      out_h=self._Gh, out_l=self._Gl, out_scale=X3_SCALE, sym_bound=ysq,
+                      scale_out=self._gscale, inv_out=self._ginv)
+            g_split = True
+        elif not self.x3:
+            self._fill_G(Y)  # Y Y^T (upper tiles + mirror) or Y^T Y
         self._active.fill_(1)
         if self.x3:
-            K.sym_split_f16(self._G, X3_SCALE, hi=self._Gh, lo=self._Gl, scale=self._gscale,
-                            inv_scale=self._ginv, upper_only=self._g_upper_only, blocked=self._g_blocked)
+            if not g_split:
+                if self._G is None:
+                    self._G = torch.empty((B, k, k), dtype=torch.float32, device=dev)
+                self._fill_G(Y)
+                K.sym_split_f16(self._G, X3_SCALE, hi=self._Gh, lo=self._Gl, scale=self._gscale,
+                                inv_scale=self._ginv, upper_only=False, blocked=self._g_blocked)
+            self._g_fp32_valid = not g_split
             self._ovf.zero_()
         cold = not (warm and self.X is not None)
         if cold:
@@ -384,9 +404,11 @@ class RankRSolver:
                     self._x3f = False
                     self._ovf.zero_()
                     self.stats.x3_fallbacks += 1
-                    if self._g_upper_only:  # the fp32 products need the full G
-                        self._G.copy_(torch.triu(self._G) + torch.triu(self._G, 1).transpose(1, 2))
-                        self._g_upper_only = False
+                    if not self._g_fp32_valid:  # the fp32 products need G itself
+                        if self._G is None:
+                            self._G = torch.empty((B, k, k), dtype=torch.float32, device=dev)
+                        self._fill_G(self._Y)
+                        self._g_fp32_valid = True
                     continue
                 break
             self._x3f = True

@@ -277,6 +277,14 @@ typedef struct cq_x3_args {
     int a_blocked;                 /* A halves K-blocked like b_blocked; lda = rows */
     int o_blocked;                 /* out_h/out_l written K-blocked over C's columns (an A
                                       operand of the next product); N % 32 == 0 */
+    int sym_out;                   /* with tri: write the split of the symmetric C directly,
+                                      K-blocked (o_blocked layout), from its upper triangle
+                                      (mirrored), with the per-matrix power-of-two scale
+                                      s[b] = 2^(14 - e) for out_bound[b] in [2^(e-1), 2^e);
+                                      C (fp32) may be NULL.  Replaces cq_sym_split_f16. */
+    const double* out_bound;       /* [batch] bound on max|C[b]| (e.g. ||Y||_F^2 for Y Y^T) */
+    float* scale_out;              /* [batch] s[b] */
+    float* inv_out;                /* [batch] 1 / (s[b] * out_scale) */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

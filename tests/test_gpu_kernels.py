@@ -607,3 +607,42 @@ def test_spd_whiten_rank_deficient_is_gelsy_basic_solution(K, p):
     r_ours = np.linalg.norm(A.astype(np.float64) @ x - y)
     r_ref = np.linalg.norm(A.astype(np.float64) @ ref - y)
     assert abs(r_ours - r_ref) <= 1e-6 * r_ref
+
+
+@pytest.mark.parametrize("n,kd", [(416, 320), (4096, 256)])
+def test_gram_sym_split_output(K, n, kd):
+    """Gram Y Y^T in sym_out mode (the solver's path): its K-blocked halves are exactly
+    symmetric and equal the blocked split of the fp32 upper-triangle Gram (cq_sym_split_f16)
+    up to the power-of-two scale, which comes from the ||Y||_F^2 bound."""
+    g = torch.Generator(device=DEV).manual_seed(21)
+    B = 2
+    Y = torch.randn(B, n, kd, device=DEV, generator=g) * 0.03
+    ys = K.pow2_scale(Y, 14)
+    yh, yl = K.split_f16(Y, ys, blocked=True)
+    yinv = 1.0 / (ys * ys)
+    G = torch.empty(B, n, n, device=DEV)
+    K.gemm_x3(yh, yl, yh, yl, yinv, G, tri=True, a_blocked=True, b_blocked=True)
+    rh, rl, rs, rinv = K.sym_split_f16(G, 64.0, upper_only=True, blocked=True)
+    ysq = K.weighted_sqsum(Y, None, kd)
+    hh = torch.full((B, n, n), float("nan"), device=DEV, dtype=torch.float16)
+    hl = hh.clone()
+    s = torch.empty(B, device=DEV)
+    inv = torch.empty(B, device=DEV)
+    K.gemm_x3(yh, yl, yh, yl, yinv, None, tri=True, a_blocked=True, b_blocked=True, out_h=hh, out_l=hl,
+              out_scale=64.0, sym_bound=ysq, scale_out=s, inv_out=inv)
+    assert not torch.isnan(hh.float()).any() and not torch.isnan(hl.float()).any()  # every entry written
+
+    def unblock(t):
+        return t.view(B, n // 32, n, 32).permute(0, 2, 1, 3).reshape(B, n, n)
+
+    for b in range(B):
+        e = math.frexp(float(ysq[b]))[1]
+        assert float(s[b]) == 2.0 ** (14 - e) and float(inv[b]) == pytest.approx(1 / (float(s[b]) * 64), rel=1e-7)
+        H = unblock(hh)[b].double() + unblock(hl)[b].double()
+        assert torch.equal(H, H.T)
+        Gr = (unblock(rh)[b].double() + unblock(rl)[b].double()) / float(rs[b])
+        # same fp32 values split at another power-of-two scale: equal up to the fp16 subnormal
+        # resolution of the small entries' lo halves (2^-24 / s absolute)
+        tol = 2.0 ** -24 / min(float(s[b]), float(rs[b]))
+        assert float((H / float(s[b]) - Gr).abs().max()) <= tol
+        assert tol <= 2.0 ** -22 * float(Gr.abs().max())  # still fp32-grade
