@@ -122,29 +122,39 @@ def main():
         engines = [CalderaEngine(ep) for _ in range(parts)]
         bnd = [B * i // parts for i in range(parts + 1)]
         outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], None, True) for i, e in enumerate(engines)], dev)
-        eng = engines[0]
-        eng.parts = engines
-        return [d for o in outs for d in o], eng
+        # no reference cycles: the previous step's buffers must be freed as soon as the
+        # next step drops them, or the caching allocator grows and stalls on hipMalloc
+        return [d for o in outs for d in o], engines[0]
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if os.environ.get("CQ_BENCH_VERBOSE"):
+        print(f"warmup done; reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     # time the dominant kernel (the G X filter GEMMs) with HIP events on its stream
     solver.EVENT_PROBE.enable(True)
+    solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * max(1, args.streams or 1))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     decs = eng = None
-    for _ in range(args.steps):
+    verbose = bool(os.environ.get("CQ_BENCH_VERBOSE"))
+    for i in range(args.steps):
         decs = eng = None  # release the previous step's results before the next allocates
         decs, eng = step()
+        if verbose:
+            torch.cuda.synchronize()
+            print(f"step {i}: {time.perf_counter() - t0:.3f} s (cumulative); reserved "
+                  f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     solver.EVENT_PROBE.enable(False)
     probe = solver.EVENT_PROBE.summary()
+    qprobe = solver.QUANT_PROBE.summary()
+    solver.QUANT_PROBE.enable(False)
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -190,8 +200,25 @@ def main():
                      "flops_per_launch_fp32_equiv": flops, "achieved_tflops_fp32_equiv": ach_tf,
                      "mfma_frac": ach_tf / mfma_peak, "solver_block_p": solver_p})
         result["roofline"] = roof
+    # the quantise kernel (fused Q update, both passes; SURVEY.md 8(d) bytes_Q per call):
+    # "w" = first Q step (quantise W itself, pure HBM), "lr" = Q steps recomputing W - L R on
+    # split-fp16 MFMAs (3 fp16 products per fp32-equivalent flop, both passes)
+    qroof = {}
+    for kind, g in qprobe.items():
+        t = g["avg_ms"] * 1e-3
+        gbs = g["bytes_per_launch"] / t / 1e9
+        f16 = 2 * 3 * g["flops_per_launch"]  # two passes, three fp16 products each
+        t_mfma = f16 / (PEAK_F16_MFMA_TFLOPS * 1e12)
+        t_hbm = g["bytes_per_launch"] / (PEAK_HBM_GBS * 1e9)
+        qroof["first_Q" if kind == "w" else "Q_with_LR"] = {
+            "bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved_gbs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
+            "achieved_tflops_f16": f16 / t / 1e12, "frac_mfma": (f16 / t / 1e12) / PEAK_F16_MFMA_TFLOPS,
+            "frac_of_bound": max(t_hbm, t_mfma) / t, "launches_timed": g["count"], "avg_call_ms": g["avg_ms"],
+            "bytes_per_call": g["bytes_per_launch"], "kernel": "q_update_v_kernel<0|1, bits> (cq_q_update_x3)"}
+    if qroof:
+        result["roofline_quantise"] = qroof
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
-    result["solver"] = {"parts": len(eng.parts), "matvecs_per_part": st.get("matvecs", 0),
+    result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0)}
     if rank == 0 and world == 1 and not args.no_parity:
         W0 = synth_batch(1, 0, "cpu")[0]

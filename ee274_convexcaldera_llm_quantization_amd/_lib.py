@@ -117,7 +117,7 @@ _SIGS = {
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -552,22 +552,25 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
-            a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None):
+            a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
     sym_bound (B,) fp64: symmetric Gram mode (tri): the K-blocked split of C is written from
     its upper triangle with scale s[b] from the bound (scale_out, inv_out = 1/(s out_scale));
-    C may then be None."""
+    C may then be None.  lda / M (a_blocked only): A holds lda >= M rows of which the first M
+    are used (C has M rows)."""
     _require_hip(Ah, Al, Bh, Bl, C)
-    Bt, M, Kd = Ah.shape
+    Bt, MA, Kd = Ah.shape
+    M = MA if M is None else M
     N = Bh.shape[1]
+    assert lda is None or (a_blocked and lda == MA and M <= MA)
     assert Bh.shape[2] == Kd and (C is None or C.shape == (Bt, M, N))
     for t in (Ah, Al, Bh, Bl, C, P, D, out_h, out_l):
         assert t is None or t.is_contiguous()
     g = X3Args()
     g.M, g.N, g.K, g.batch = M, N, Kd, Bt
-    g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (M if a_blocked else Kd), M * Kd
+    g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (MA if a_blocked else Kd), MA * Kd
     g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), (N if b_blocked else Kd), N * Kd
     g.inv_scale = inv_scale.data_ptr()
     g.C, g.ldc, g.stride_c = (C.data_ptr() if C is not None else None), N, M * N
@@ -605,7 +608,7 @@ def x3_clock():
 
 
 def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None, bits: int, *, eps: float = 1e-8,
-                codes=None, packed=None, scale=None, err_w=None, err_out=None):
+                codes=None, packed=None, scale=None, err_w=None, err_out=None, events=None, absmax_in=None):
     """Fused Q update: quantise res = W - L R (W alone if L is None) per matrix, never
     materialising res.  W (B, m, n) fp16/fp32, L (B, m, r), R (B, r, n) fp32 with r % 32 == 0.
     Fills packed (B, m*n*bits/8) uint8 and/or codes, scale (B,), err_out (B,) fp64."""
@@ -628,9 +631,14 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
     ws = workspace(lib.cq_q_update_workspace(m, n, B), dev)
+    if events is not None:  # HIP events around the quantise kernels only (bench roofline)
+        events[0].record()
     _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),
-                              _p(packed), _p(scale), _p(err_w), _p(err_out), _p(ws), ws.numel(), _stream(dev)),
+                              _p(packed), _p(scale), _p(err_w), _p(err_out), _p(absmax_in if r == 0 else None),
+                              _p(ws), ws.numel(), _stream(dev)),
            "cq_q_update_x3")
+    if events is not None:
+        events[1].record()
 
 
 def absmax(X: torch.Tensor) -> torch.Tensor:

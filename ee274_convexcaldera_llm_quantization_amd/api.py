@@ -74,7 +74,8 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
             for i, e in enumerate(engines)]
     res = [d for part in run_interleaved(gens, comp) for d in part]
     eng = engines[0]
-    eng.parts = engines
+    if return_engine:  # (a reference cycle: only when the caller asks for the engine)
+        eng.parts = engines
     out = []
     lr_dev = dev_req if dev_req.type == "cpu" else comp
     # alg.py:81 keeps W on the host: one batched copy into pinned memory instead of B

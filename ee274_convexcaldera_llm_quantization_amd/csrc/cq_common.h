@@ -80,6 +80,33 @@ __device__ __forceinline__ float quant_code(float x, float s, float k) {
 }
 __device__ __forceinline__ float dequant(float c, float k, float s) { return (c / k) * s; }
 
+// Correctly rounded a / b for many quotients with one divisor (Markstein): y = RN(1/b) from
+// one IEEE division, q = RN(a y), r = a - q b (exact by FMA), q' = RN(q + r y) = RN(a / b)
+// (Muller et al., Handbook of Floating-Point Arithmetic, Thm 5.8) whenever the quotient is a
+// normal number; zero, tiny, huge and non-finite cases take the IEEE division.  Three VALU
+// ops instead of the ~10 of the correctly rounded division sequence.
+__device__ __forceinline__ float div_rn(float a, float b, float y) {
+    const float q = a * y;
+    const float aq = fabsf(q);
+    if (!(aq >= 0x1p-100f && aq <= 0x1p100f)) return a / b;
+    const float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+// Branch-free form for kernels that checked once that the divisor is a finite normal number
+// and that |a| <= |b| (a quantiser's scale is the max |x|): quotients then never overflow,
+// and a tiny quotient only needs |result| << 1/2, which the FMA path gives.
+__device__ __forceinline__ float div_fast(float a, float b, float y) {
+    const float q = a * y;
+    const float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+__device__ __forceinline__ bool div_fast_ok(float b) { return b >= 0x1p-126f && b <= 0x1p126f; }
+// quant_code / dequant with the divisor reciprocals precomputed (ys = RN(1/s), yk = RN(1/k))
+__device__ __forceinline__ float quant_code_r(float x, float s, float ys, float k) {
+    return rintf(div_rn(x, s, ys) * k);
+}
+__device__ __forceinline__ float dequant_r(float c, float k, float yk, float s) { return div_rn(c, k, yk) * s; }
+
 }  // namespace cq
 
 #define CQ_REQUIRE(cond, ...)                                  \

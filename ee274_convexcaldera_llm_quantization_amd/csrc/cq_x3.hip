@@ -680,6 +680,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
 // v_mfma_f32_16x16x32_f16 tiles (one MFMA per 32-deep K step and product instead of two
 // 32x32x16).  Under the chip's power limit the 16x16x32 form runs at a higher clock for the
 // same work (MI355X_MICROARCH.md: ~1.15x the FLOP/s of 32x32x16 in bare loops).
+// PERMB: block j's B fragment row for output register index t = 4 lq + r is LDS row
+// 64 wn + 16 (t >> 2) + 4 j + (t & 3), so lane (l16, lq) ends up holding the 16 consecutive
+// B rows 64 wn + 16 lq + [0, 16) in acc[i][0..3][0..3] (used by the fused Q update).
+template <bool PERMB = false>
 __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
                                             f32x4v (&acc)[6][4]) {
@@ -704,7 +708,7 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
         f16x8 bh[4], bl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int row = 64 * wn + 16 * j + l16;
+            const int row = PERMB ? 64 * wn + 16 * (l16 >> 2) + 4 * j + (l16 & 3) : 64 * wn + 16 * j + l16;
             bh[j] = xg_frag(sB, row, lq);
             bl[j] = xg_frag(sB + XW_BPART, row, lq);
         }
@@ -1007,6 +1011,237 @@ __global__ __launch_bounds__(XW_THREADS, 1) void q_update_x3_kernel(QUK q) {
     }
 }
 
+// Fused Q update on the 16x16x32 ring (default): A = L halves (tile rows = rows of W),
+// B = R^T halves with PERMB, so each lane owns 16 consecutive columns of one W row: W loads
+// of 32 B (fp16) per lane, one 32-bit store of 16 two-bit codes (64 bits at 4 bits), and a
+// wave-instruction covers 16 rows x 64 columns.  Same two passes and arithmetic as
+// q_update_x3_kernel (res = W - L R with identical code in both passes).  n % 16 == 0.
+template <int PASS, int BITS, int DT>
+__global__ __launch_bounds__(XW_THREADS, 1) void q_update_v_kernel(QUK q) {
+    extern __shared__ __attribute__((aligned(16))) char qv_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(qv_smem_raw);
+    const X3K& a = q.x;
+    const int64_t tiles = a.tiles_n * a.tiles_m;
+    const int64_t total = tiles * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
+    const int64_t tile = lin % tiles;
+    const int64_t tn = tile % a.tiles_n, tm = tile / a.tiles_n;
+    const int64_t b = lin / tiles;
+    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid & 1, wn = wid >> 1;
+    const int l16 = lane & 15, lq = lane >> 4;
+
+    f32x4v acc[6][4];
+    xv_mainloop<true>(a, b, m0, n0, a.K / XW_BK, smem, wid, lane, wm, wn, acc);
+    const float sc = a.K > 0 ? a.inv_scale[b] : 0.f;
+    const int64_t MN = q.m * q.n;
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN;
+    const float* Wf = reinterpret_cast<const float*>(q.W) + b * MN;
+    constexpr float kq = (float)((1 << (BITS - 1)) - 1);
+    uint32_t mx = 0;
+    double err = 0.0;
+    float s = 0.f;
+    if (PASS == 1) s = quant_scale(q.absmax[b], q.eps);
+    const float ys = 1.f / s, yk = 1.f / kq;  // IEEE reciprocals for div_rn
+    const int64_t col = n0 + 64 * wn + 16 * lq;  // this lane's 16 consecutive columns
+    const bool colok = col < q.n;                 // n % 16 == 0: a run is all in or all out
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int64_t row = m0 + 96 * wm + 16 * i + l16;
+        if (row >= q.m || !colok) continue;
+        const int64_t e = row * q.n + col;
+        // W kept packed (fp16: 8 registers) and converted 4 columns at a time
+        uint4 wr[4];
+        if (DT == CQ_F16) {
+            wr[0] = *reinterpret_cast<const uint4*>(Wh + e);
+            wr[1] = *reinterpret_cast<const uint4*>(Wh + e + 8);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wr[u] = *reinterpret_cast<const uint4*>(Wf + e + 4 * u);
+        }
+        uint32_t pk[4] = {0u, 0u, 0u, 0u};  // packed / int8 code words
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float w;
+                if (DT == CQ_F16) {
+                    const uint32_t pr = (&wr[j >> 1].x)[(j & 1) * 2 + (r >> 1)];
+                    w = (float)__builtin_bit_cast(_Float16, (uint16_t)((r & 1) ? (pr >> 16) : (pr & 0xffffu)));
+                } else {
+                    w = __uint_as_float((&wr[j].x)[r]);
+                }
+                v[r] = a.K > 0 ? w - acc[i][j][r] * sc : w;  // res = W - L R (alg.py:262)
+            }
+            if (PASS == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx = max(mx, abs_bits(v[r]));
+                continue;
+            }
+            int cq[4];
+            float e4[4];
+            float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
+            if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + col + 4 * j);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float c = quant_code_r(v[r], s, ys, kq);
+                const float d = dequant_r(c, kq, yk, s) - v[r];
+                e4[r] = (d * d) * (&wv.x)[r];
+                cq[r] = (int)c;
+            }
+            err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
+            if (BITS == 2) {  // byte j = codes 4j..4j+3, MSB-first (offset binary c + 1)
+                const uint32_t by = ((uint32_t)(cq[0] + 1) << 6) | ((uint32_t)(cq[1] + 1) << 4) |
+                                    ((uint32_t)(cq[2] + 1) << 2) | (uint32_t)(cq[3] + 1);
+                pk[0] |= by << (8 * j);
+            } else if (BITS == 4) {  // bytes 2j, 2j+1 = codes (4j, 4j+1), (4j+2, 4j+3)
+                const uint32_t b0 = ((uint32_t)(cq[0] + 7) << 4) | (uint32_t)(cq[1] + 7);
+                const uint32_t b1 = ((uint32_t)(cq[2] + 7) << 4) | (uint32_t)(cq[3] + 7);
+                pk[j >> 1] |= (b0 | (b1 << 8)) << (16 * (j & 1));
+            } else if (BITS == 8) {
+                pk[j] = (uint32_t)(uint8_t)(int8_t)cq[0] | ((uint32_t)(uint8_t)(int8_t)cq[1] << 8) |
+                        ((uint32_t)(uint8_t)(int8_t)cq[2] << 16) | ((uint32_t)(uint8_t)(int8_t)cq[3] << 24);
+            } else if (q.codes) {
+                *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(q.codes) + b * MN + e + 4 * j) =
+                    make_short4((short)cq[0], (short)cq[1], (short)cq[2], (short)cq[3]);
+            }
+            if (BITS <= 4 && q.codes) {  // unpacked int8 codes alongside the packed bytes
+                *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e + 4 * j) =
+                    (uint32_t)(uint8_t)(int8_t)cq[0] | ((uint32_t)(uint8_t)(int8_t)cq[1] << 8) |
+                    ((uint32_t)(uint8_t)(int8_t)cq[2] << 16) | ((uint32_t)(uint8_t)(int8_t)cq[3] << 24);
+            }
+        }
+        if (PASS == 1) {
+            if (BITS == 2 && q.packed) *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 4) = pk[0];
+            if (BITS == 4 && q.packed) *reinterpret_cast<uint2*>(q.packed + (b * MN + e) / 2) = make_uint2(pk[0], pk[1]);
+            if (BITS == 8 && q.codes)
+                *reinterpret_cast<uint4*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+        asm volatile("" ::: "memory");  // keep the row blocks' W loads from being hoisted together (VGPRs)
+    }
+    if (PASS == 0) {
+        mx = wave_max_u32(mx);
+        if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
+    } else if (q.part) {
+        __shared__ double red[16];
+        const double tsum = block_sum_f64(err, red);
+        if (threadIdx.x == 0) q.part[b * tiles + tile] = tsum;
+    }
+}
+
+// First Q step (r = 0, max|W| known): a plain streaming quantise of W, 16 consecutive
+// elements per thread per step (32-byte fp16 loads, one 32-bit store of 16 two-bit codes),
+// no LDS and no MFMA, so many workgroups per CU keep HBM busy.  Same arithmetic as pass 1 of
+// the fused kernels with res = W.  n % 16 == 0; per-block fp64 error partials in part.
+template <int DT, int BITS, bool FAST>
+__device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t MN, int64_t e, const uint4 (&wr)[4],
+                                              float s, float ys, float yk, double& err) {
+    constexpr float kq = (float)((1 << (BITS - 1)) - 1);
+    const int64_t col = e % q.n;
+    uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int cq[4];
+        float e4[4];
+        float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + col + 4 * j);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v;
+            if (DT == CQ_F16) {
+                const uint32_t pr = (&wr[j >> 1].x)[(j & 1) * 2 + (r >> 1)];
+                v = (float)__builtin_bit_cast(_Float16, (uint16_t)((r & 1) ? (pr >> 16) : (pr & 0xffffu)));
+            } else {
+                v = __uint_as_float((&wr[j].x)[r]);
+            }
+            const float c = FAST ? rintf(div_fast(v, s, ys) * kq) : quant_code(v, s, kq);
+            const float d = (FAST ? div_fast(c, kq, yk) * s : dequant(c, kq, s)) - v;
+            e4[r] = (d * d) * (&wv.x)[r];
+            cq[r] = (int)c;
+        }
+        err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
+        if (BITS == 2) {
+            pk[0] |= (((uint32_t)(cq[0] + 1) << 6) | ((uint32_t)(cq[1] + 1) << 4) | ((uint32_t)(cq[2] + 1) << 2) |
+                      (uint32_t)(cq[3] + 1)) << (8 * j);
+        } else if (BITS == 4) {
+            const uint32_t b0 = ((uint32_t)(cq[0] + 7) << 4) | (uint32_t)(cq[1] + 7);
+            const uint32_t b1 = ((uint32_t)(cq[2] + 7) << 4) | (uint32_t)(cq[3] + 7);
+            pk[j >> 1] |= (b0 | (b1 << 8)) << (16 * (j & 1));
+        } else if (BITS == 8) {
+            pk[j] = (uint32_t)(uint8_t)(int8_t)cq[0] | ((uint32_t)(uint8_t)(int8_t)cq[1] << 8) |
+                    ((uint32_t)(uint8_t)(int8_t)cq[2] << 16) | ((uint32_t)(uint8_t)(int8_t)cq[3] << 24);
+        } else if (q.codes) {
+            *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(q.codes) + b * MN + e + 4 * j) =
+                make_short4((short)cq[0], (short)cq[1], (short)cq[2], (short)cq[3]);
+        }
+        if (BITS <= 4 && q.codes)
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e + 4 * j) =
+                (uint32_t)(uint8_t)(int8_t)cq[0] | ((uint32_t)(uint8_t)(int8_t)cq[1] << 8) |
+                ((uint32_t)(uint8_t)(int8_t)cq[2] << 16) | ((uint32_t)(uint8_t)(int8_t)cq[3] << 24);
+    }
+    if (BITS == 2 && q.packed) *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 4) = pk[0];
+    if (BITS == 4 && q.packed) *reinterpret_cast<uint2*>(q.packed + (b * MN + e) / 2) = make_uint2(pk[0], pk[1]);
+    if (BITS == 8 && q.codes)
+        *reinterpret_cast<uint4*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+}
+
+template <int DT>
+__device__ __forceinline__ void qstream_load(const QUK& q, int64_t b, int64_t MN, int64_t e, uint4 (&wr)[4]) {
+    if (DT == CQ_F16) {
+        const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN + e;
+        wr[0] = *reinterpret_cast<const uint4*>(Wh);
+        wr[1] = *reinterpret_cast<const uint4*>(Wh + 8);
+    } else {
+        const float* Wf = reinterpret_cast<const float*>(q.W) + b * MN + e;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wr[u] = *reinterpret_cast<const uint4*>(Wf + 4 * u);
+    }
+}
+
+// First Q step (r = 0, max|W| known): a plain streaming quantise of W, 16 consecutive
+// elements per thread per group, the next group's load in flight (32-byte fp16 loads, one
+// 32-bit store of 16 two-bit codes), no LDS and no MFMA, so many workgroups per CU keep HBM
+// busy.  Same arithmetic as pass 1 of the fused kernels with res = W.  n % 16 == 0;
+// per-block fp64 error partials in part.
+template <int DT, int BITS>
+__global__ __launch_bounds__(256) void quant_w_stream_kernel(QUK q) {
+    constexpr float kq = (float)((1 << (BITS - 1)) - 1);
+    const int64_t b = blockIdx.y;
+    const int64_t MN = q.m * q.n;
+    const int64_t ng = MN / 16;
+    const float s = quant_scale(q.absmax[b], q.eps);
+    const float ys = 1.f / s, yk = 1.f / kq;  // IEEE reciprocals for div_rn
+    double err = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (div_fast_ok(s)) {  // uniform: the common case, branch-free correctly rounded division
+        uint4 nx[4];  // the next group's W, loaded while this one is quantised
+        if (g < ng) qstream_load<DT>(q, b, MN, g * 16, nx);
+        for (; g < ng; g += stride) {
+            uint4 cur[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cur[u] = nx[u];
+            if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx);
+            qstream_group<DT, BITS, true>(q, b, MN, g * 16, cur, s, ys, yk, err);
+        }
+    } else {  // non-finite / subnormal scale: IEEE divisions
+        for (; g < ng; g += stride) {
+            uint4 w0[4];
+            qstream_load<DT>(q, b, MN, g * 16, w0);
+            qstream_group<DT, BITS, false>(q, b, MN, g * 16, w0, s, ys, yk, err);
+        }
+    }
+    if (q.part) {
+        __shared__ double red[16];
+        const double tsum = block_sum_f64(err, red);
+        if (threadIdx.x == 0) q.part[b * gridDim.x + blockIdx.x] = tsum;
+    }
+}
+
 __global__ void q_update_finalize_kernel(const uint32_t* absmax, const double* part, int64_t tiles, int64_t batch,
                                          float eps, float* scale, double* err_out) {
     const int64_t b = blockIdx.x;
@@ -1167,6 +1402,26 @@ template <int DT>
 __global__ void absmax_dt_kernel(const void* __restrict__ X, int64_t n_per, uint32_t* __restrict__ out) {
     const int64_t b = blockIdx.y;
     uint32_t mx = 0;
+    // 16-byte vector loads (8 halves / 4 floats per load) where the rows allow it
+    constexpr int V = DT == CQ_F16 ? 8 : 4;
+    const bool vec = n_per % V == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+    if (vec) {
+        const uint4* Xv = reinterpret_cast<const uint4*>(X) + b * (n_per / V);
+        for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n_per / V; q += (int64_t)gridDim.x * blockDim.x) {
+            const uint4 r = Xv[q];
+            if (DT == CQ_F16) {
+                const _Float16* h = reinterpret_cast<const _Float16*>(&r);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) mx = max(mx, abs_bits((float)h[u]));
+            } else {
+                mx = max(mx, max(max(abs_bits(__uint_as_float(r.x)), abs_bits(__uint_as_float(r.y))),
+                                 max(abs_bits(__uint_as_float(r.z)), abs_bits(__uint_as_float(r.w)))));
+            }
+        }
+        mx = wave_max_u32(mx);
+        if ((threadIdx.x & 63) == 0 && mx) atomicMax(out + b, mx);
+        return;
+    }
     for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n_per; q += (int64_t)gridDim.x * blockDim.x) {
         const float v = DT == CQ_F16 ? (float)reinterpret_cast<const _Float16*>(X)[b * n_per + q]
                                      : reinterpret_cast<const float*>(X)[b * n_per + q];
@@ -1427,14 +1682,16 @@ int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch
 
 
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
-    const int64_t tiles = ceil_div(n, XW_BM) * ceil_div(m, XW_BN);
+    // tile counts of both Q-update kernels (q_update_v_kernel tiles W as m x n, the 32x32
+    // kernel as n x m)
+    const int64_t tiles = std::max(ceil_div(n, XW_BM) * ceil_div(m, XW_BN), ceil_div(m, XW_BM) * ceil_div(n, XW_BN));
     return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) + (size_t)batch * tiles * sizeof(double);
 }
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
                    const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl, const float* inv_scale, int bits,
                    float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w, double* err_out,
-                   void* ws, size_t ws_bytes, void* stream) {
+                   const float* absmax_in, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(W && m > 0 && n > 0 && batch > 0 && r >= 0, "cq_q_update_x3: bad shape");
     CQ_REQUIRE(dtype == CQ_F16 || dtype == CQ_F32, "cq_q_update_x3: dtype must be f16/f32");
     if (bits != 2 && bits != 4 && bits != 8 && bits != 16) return set_error(CQ_EINVAL, "Bit-width not supported!");
@@ -1447,16 +1704,33 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     QUK q;
     X3K& a = q.x;
     memset(&a, 0, sizeof(a));  // a_blocked = b_blocked = 0, no active mask
-    // A operand R^T (n x r): tile rows run over W's columns; B operand L (m x r): tile
-    // columns run over W's rows (see q_update_x3_kernel)
-    a.M = n; a.N = m; a.K = r; a.batch = batch;
-    a.Ah = reinterpret_cast<const _Float16*>(Rth); a.Al = reinterpret_cast<const _Float16*>(Rtl);
-    a.lda = r; a.sa = n * r;
-    a.Bh = reinterpret_cast<const _Float16*>(Lh); a.Bl = reinterpret_cast<const _Float16*>(Ll);
-    a.ldb = r; a.sb = m * r;
+    static const bool legacy = getenv("CQ_QU_KERNEL") != nullptr;  // A/B switch: the 32x32 kernel
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool vk = !legacy && n % 16 == 0 && al16(W) && (!codes || al16(codes)) && (!packed || al16(packed)) &&
+                    (!err_w || al16(err_w));
+    if (vk) {
+        // A operand L (m x r): tile rows run over W's rows; B operand R^T (n x r): tile
+        // columns over W's columns (see q_update_v_kernel)
+        a.M = m; a.N = n;
+        a.Ah = reinterpret_cast<const _Float16*>(Lh); a.Al = reinterpret_cast<const _Float16*>(Ll);
+        a.lda = r; a.sa = m * r;
+        a.Bh = reinterpret_cast<const _Float16*>(Rth); a.Bl = reinterpret_cast<const _Float16*>(Rtl);
+        a.ldb = r; a.sb = n * r;
+        a.tiles_n = ceil_div(n, XW_BN);
+        a.tiles_m = ceil_div(m, XW_BM);
+    } else {
+        // A operand R^T (n x r): tile rows run over W's columns; B operand L (m x r): tile
+        // columns run over W's rows (see q_update_x3_kernel)
+        a.M = n; a.N = m;
+        a.Ah = reinterpret_cast<const _Float16*>(Rth); a.Al = reinterpret_cast<const _Float16*>(Rtl);
+        a.lda = r; a.sa = n * r;
+        a.Bh = reinterpret_cast<const _Float16*>(Lh); a.Bl = reinterpret_cast<const _Float16*>(Ll);
+        a.ldb = r; a.sb = m * r;
+        a.tiles_n = ceil_div(m, XW_BN);
+        a.tiles_m = ceil_div(n, XW_BM);
+    }
+    a.K = r; a.batch = batch;
     a.inv_scale = inv_scale;
-    a.tiles_n = ceil_div(m, XW_BN);
-    a.tiles_m = ceil_div(n, XW_BM);
     const int64_t tiles = a.tiles_n * a.tiles_m;
     CQ_REQUIRE(tiles * batch < (1ll << 31), "cq_q_update_x3: grid too large");
     q.W = W; q.wf16 = dtype == CQ_F16; q.m = m; q.n = n;
@@ -1464,11 +1738,37 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     q.part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + align_up((size_t)batch * sizeof(uint32_t), 256));
     q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w;
     hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(q.absmax, 0, batch * sizeof(uint32_t), s) != hipSuccess)
+    const bool known = absmax_in && r == 0;  // max|W| bits given: skip the absmax pass
+    if (known) {
+        if (hipMemcpyAsync(q.absmax, absmax_in, batch * sizeof(uint32_t), hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return set_error(CQ_EHIP, "cq_q_update_x3: copy failed");
+    } else if (hipMemsetAsync(q.absmax, 0, batch * sizeof(uint32_t), s) != hipSuccess) {
         return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
+    }
     const unsigned grid = (unsigned)(tiles * batch);
-#define CQ_QU(B) do { q_update_x3_kernel<0, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); \
-                      q_update_x3_kernel<1, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); } while (0)
+    if (known && vk) {  // r = 0 with max|W| known: one streaming pass over W
+        const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(tiles, ceil_div(m * n / 16, 256)));
+        CQ_REQUIRE(batch < 65536, "cq_q_update_x3: batch too large");
+        const dim3 sg((unsigned)gx, (unsigned)batch);
+#define CQ_QS(DT, B) quant_w_stream_kernel<DT, B><<<sg, 256, 0, s>>>(q)
+        if (dtype == CQ_F16) {
+            switch (bits) { case 2: CQ_QS(CQ_F16, 2); break; case 4: CQ_QS(CQ_F16, 4); break;
+                            case 8: CQ_QS(CQ_F16, 8); break; default: CQ_QS(CQ_F16, 16); }
+        } else {
+            switch (bits) { case 2: CQ_QS(CQ_F32, 2); break; case 4: CQ_QS(CQ_F32, 4); break;
+                            case 8: CQ_QS(CQ_F32, 8); break; default: CQ_QS(CQ_F32, 16); }
+        }
+#undef CQ_QS
+        q_update_finalize_kernel<<<(unsigned)batch, 64, 0, s>>>(q.absmax, q.part, gx, batch, eps, scale_out, err_out);
+        return check_launch("cq_q_update_x3");
+    }
+#define CQ_QU(B) do { if (vk && dtype == CQ_F16) { \
+                          if (!known) q_update_v_kernel<0, B, CQ_F16><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); \
+                          q_update_v_kernel<1, B, CQ_F16><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); } \
+                      else if (vk) { if (!known) q_update_v_kernel<0, B, CQ_F32><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); \
+                                     q_update_v_kernel<1, B, CQ_F32><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); } \
+                      else { if (!known) q_update_x3_kernel<0, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); \
+                             q_update_x3_kernel<1, B><<<grid, XW_THREADS, XW_LDS_BYTES, s>>>(q); } } while (0)
     switch (bits) {
         case 2: CQ_QU(2); break;
         case 4: CQ_QU(4); break;

@@ -26,7 +26,8 @@ import torch
 from . import _lib as K
 from . import qlog
 from .overlap import run_to_end
-from .solver import RandSVD, RankRSolver
+from . import scratch
+from .solver import QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
 
 
 @dataclass
@@ -85,6 +86,7 @@ class _Weights:
         h = h.to(device=dev, dtype=f32)
         if not p.activation_aware_LR:
             self.err = h
+            self.err_unit = bool(torch.all(h == 1.0).item())
             self.ycol = None
             self.ycol_max = 1.0
             self.rinv = None
@@ -107,6 +109,7 @@ class _Weights:
         self.ycol_max = 1.0 if self.identity else float(sq.max().item())
         self.rinv = None if self.identity else 1.0 / sq
         self.lplr = None if self.identity else lam  # ||Y - L (R*ycol)||^2 uses unit weights
+        self.err_unit = bool(torch.all(herr == 1.0).item())
 
 
     def _init_dense(self, H, n, p: EngineParams, dev):
@@ -126,6 +129,7 @@ class _Weights:
         self.identity = False
         self.ycol = self.rinv = self.lplr = None
         self.err = None
+        self.err_unit = True
         self.ycol_max = 1.0
         Hs = (H + H.t()) * 0.5
         lam, V = torch.linalg.eigh(Hs)
@@ -247,10 +251,19 @@ class CalderaEngine:
             err = torch.empty(B, dtype=torch.float64, device=Ws.device)
             Lm = st.L if Kdim else None
             Rm = st.R if Kdim else None
+            # algorithmic bytes of a quantise call: W read once, packed codes
+            # written; the rank-r recompute adds 2 m n r flops (fp32-equivalent)
+            ev = QUANT_PROBE.start("lr" if Kdim else "w", 2.0 * B * m * n * Kdim,
+                                   B * (m * n * Ws.element_size() + m * n * p.Q_bits / 8.0 + 4))
+            # first Q step: res = W, whose max |.| is already known (self._wmax): one pass over W
+            amax = self._wmax if not Kdim else None
+            ew = None if wts.err_unit else wts.err  # unit weights: the same sums without the loads
             if st.q_packed:
-                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, packed=st.Qc, scale=st.Qs, err_w=wts.err, err_out=err)
+                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, packed=st.Qc, scale=st.Qs, err_w=ew, err_out=err, events=ev,
+                              absmax_in=amax)
             else:
-                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, codes=st.Qc, scale=st.Qs, err_w=wts.err, err_out=err)
+                K.q_update_x3(Ws, Lm, Rm, p.Q_bits, codes=st.Qc, scale=st.Qs, err_w=ew, err_out=err, events=ev,
+                              absmax_in=amax)
             st.has_Q = True
             return err
         absmax = torch.zeros(B, dtype=torch.int32, device=Ws.device)  # |res| max as uint32 bits
@@ -336,16 +349,25 @@ class CalderaEngine:
             if weighted:
                 K.gemm(res, wts.Vs, C=Y)
         elif sv.x3 and not sv.direct and m % 32 == 0 and n % 64 == 0 and (st.q_packed or st.dense_q):
-            # one pass: res / Y (fp32), the solver's Gram operand halves and ||Y||^2
-            if self._yh is None:
-                self._yh = torch.empty((B, m, n), dtype=torch.float16, device=dev)
-                self._yl = torch.empty_like(self._yh)
+            # one pass: the solver's Gram operand halves, ||Y||^2 and, for m <= n, the halves of
+            # Y^T (operand of R = U^T Y on split-fp16 products); res / Y in fp32 only where a
+            # later step still reads them (quantised factors, wide-right shapes)
+            if self._yh is None:  # cached scratch (scratch.py)
+                self._yh = scratch.get("lr.yh", (B, m, n), torch.float16, dev)
+                self._yl = scratch.get("lr.yl", (B, m, n), torch.float16, dev)
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
             halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)
+            x3_r = sv.left and not quantized and p.activation_aware_LR
+            if x3_r:
+                if self._yth is None:
+                    self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
+                    self._ytl = scratch.get("lr.ytl", (B, n, m), torch.float16, dev)
+                halves.update(thi=self._yth, tlo=self._ytl)
             K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
                              ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
-                             res=res, Y=Y if weighted else None, scale=self._ys, sq=ysq, **halves)
+                             res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
+                             scale=self._ys, sq=ysq, **halves)
             y_split = (self._yh, self._yl, self._ys, ysq)
         else:
             K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
@@ -366,6 +388,8 @@ class CalderaEngine:
                 # R = (U^T Y) diag(1/sqrt(lam))   (alg.py:219-225); randomized: S Vh as returned
                 if rand:
                     R.copy_(sv.SVh)
+                elif y_split is not None and self._yth is not None:
+                    self._ut_y(sv, R)
                 else:
                     K.gemm(U, Ysrc, ta=True, C=R)
                 if wts.rinv is not None:
@@ -377,6 +401,8 @@ class CalderaEngine:
                 K.scale_rc(U, colscale=sq, out=L)  # L = U sqrt(S)
                 if rand:
                     R.copy_(sv.SVh)
+                elif y_split is not None and self._yth is not None:
+                    self._ut_y(sv, R)  # S Vh
                 else:
                     K.gemm(U, Ysrc, ta=True, C=R)  # S Vh
                 rs = torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30))
@@ -412,6 +438,17 @@ class CalderaEngine:
         err = torch.empty(B, dtype=torch.float64, device=dev)
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
+
+    def _ut_y(self, sv, R):
+        """R = U^T Y (U = the solver's Ritz block, first r columns; m <= n) as a split-fp16
+        product: A = X^T halves (the block's transposed split, rows r of p), B = Y^T halves
+        written by cq_residual_split (K-blocked over m)."""
+        X = sv.X  # (B, m, p), orthonormal columns
+        B, m, p = X.shape
+        r = R.shape[1]
+        xh, xl = sv.split_block_t(X)
+        inv = 1.0 / (self._ys * X3_SCALE)
+        K.gemm_x3(xh, xl, self._yth, self._ytl, inv, R, a_blocked=True, b_blocked=True, lda=p, M=r)
 
     def _solve_normal(self, M64, rows: int):
         """Whitening of the r x r normal matrix A^T A of an lstsq with A (rows x r):
@@ -546,6 +583,7 @@ class CalderaEngine:
         wts = _Weights(h, n, p, dev)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
         self._yh = self._yl = self._ys = None
+        self._yth = self._ytl = None
         if wts.dense:  # den = tr(W H W^T) (alg.py:298)
             self._etmp = torch.empty((B, m, n), dtype=torch.float32, device=dev)
             wf = torch.empty((B, m, n), dtype=torch.float32, device=dev)
@@ -595,6 +633,7 @@ class CalderaEngine:
         if self.solver is not None:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         self._yh = self._yl = None
+        self._yth = self._ytl = None
         return self._finalize(best, st, W, Ws, gs, errors, wts, spare=(work, res))
 
     def _state_error(self, st, Ws, work, wts):

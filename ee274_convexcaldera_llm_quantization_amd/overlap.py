@@ -26,13 +26,27 @@ def run_to_end(gen):
         return stop.value
 
 
+_STREAMS: dict = {}
+
+
+def _part_streams(device, n):
+    """The same n streams of `device` on every call (the cached scratch of scratch.py is
+    keyed by stream, so a fixed set keeps it bounded)."""
+    dev = torch.device(device)
+    lst = _STREAMS.setdefault(dev, [])
+    while len(lst) < n:
+        lst.append(torch.cuda.Stream(device=dev))
+    return lst[:n]
+
+
 def run_interleaved(gens, device):
-    """Round-robin over generators, each on a fresh stream of `device`.  Returns the list
-    of their return values.  The caller's stream is joined before and after."""
+    """Round-robin over generators, each on its own stream of `device` (a fixed per-device
+    set).  Returns the list of their return values.  The caller's stream is joined before
+    and after."""
     if len(gens) == 1:
         return [run_to_end(gens[0])]
     caller = torch.cuda.current_stream(device)
-    streams = [torch.cuda.Stream(device=device) for _ in gens]
+    streams = _part_streams(device, len(gens))
     for s in streams:
         s.wait_stream(caller)
     out = [None] * len(gens)

@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib as K
+from . import scratch
 from .overlap import run_to_end
 
 
@@ -76,6 +77,47 @@ class _EventProbe:
 
 
 EVENT_PROBE = _EventProbe()
+
+
+class _GroupProbe:
+    """HIP-event timing of the fused Q-update launches (the quantise kernel: both passes of
+    cq_q_update_x3 on its stream), grouped by kind (first Q step without L R, and with the
+    rank-r recompute); used by bench.py for the quantise kernel's roofline."""
+
+    def __init__(self):
+        self.on = False
+        self.pool = []
+        self.meta = []
+
+    def enable(self, on: bool, max_pairs: int = 64):
+        self.on = on
+        if on:
+            self.pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                         for _ in range(max_pairs)]
+            self.meta = []
+
+    def start(self, kind, flops, nbytes):
+        if not self.on or len(self.meta) >= len(self.pool):
+            return None
+        ev = self.pool[len(self.meta)]
+        self.meta.append((kind, flops, nbytes))
+        return ev  # recorded by the caller around the kernel launches (_lib.q_update_x3 events=)
+
+    def summary(self):
+        if not self.meta:
+            return {}
+        torch.cuda.synchronize()
+        out = {}
+        for (a, b), (kind, fl, nb) in zip(self.pool, self.meta):
+            g = out.setdefault(kind, {"count": 0, "ms": 0.0, "flops_per_launch": fl, "bytes_per_launch": nb})
+            g["count"] += 1
+            g["ms"] += a.elapsed_time(b)
+        for g in out.values():
+            g["avg_ms"] = g.pop("ms") / g["count"]
+        return out
+
+
+QUANT_PROBE = _GroupProbe()
 
 
 X3_SCALE = 2.0 ** 6  # power-of-two scale of the filter iterates' fp16 halves (entries <= ~1)
@@ -141,19 +183,20 @@ class RankRSolver:
         B, k, p = self.B, self.k, self.p
         if self._bufs is None:
             # 5 buffers: an outer iteration keeps its input alive until its overflow check
-            self._bufs = [torch.empty((B, k, p), dtype=torch.float32, device=dev) for _ in range(5)]
+            # large work buffers: cached scratch (scratch.py), reused by later solves
+            f32, f16 = torch.float32, torch.float16
+            self._bufs = [scratch.get(f"solver.blk{i}", (B, k, p), f32, dev) for i in range(5)]
             # fp32 G only for the fp32 products (the split-fp16 path keeps G as its halves and
             # allocates it on an fp16 overflow fallback)
-            self._G = None if self.x3 else torch.empty((B, k, k), dtype=torch.float32, device=dev)
+            self._G = None if self.x3 else torch.empty((B, k, k), dtype=f32, device=dev)
             if self.x3:
-                f16 = torch.float16
-                self._Gh = torch.empty((B, k, k), dtype=f16, device=dev)
-                self._Gl = torch.empty((B, k, k), dtype=f16, device=dev)
-                self._gscale = torch.empty(B, dtype=torch.float32, device=dev)
-                self._ginv = torch.empty(B, dtype=torch.float32, device=dev)
-                self._xt = [torch.empty((B, p, k), dtype=torch.float32, device=dev) for _ in range(2)]
-                self._xh = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
-                self._xl = [torch.empty((B, p, k), dtype=f16, device=dev) for _ in range(2)]
+                self._Gh = scratch.get("solver.Gh", (B, k, k), f16, dev)
+                self._Gl = scratch.get("solver.Gl", (B, k, k), f16, dev)
+                self._gscale = torch.empty(B, dtype=f32, device=dev)
+                self._ginv = torch.empty(B, dtype=f32, device=dev)
+                self._xt = [scratch.get(f"solver.xt{i}", (B, p, k), f32, dev) for i in range(2)]
+                self._xh = [scratch.get(f"solver.xh{i}", (B, p, k), f16, dev) for i in range(2)]
+                self._xl = [scratch.get(f"solver.xl{i}", (B, p, k), f16, dev) for i in range(2)]
                 self._ovf = torch.zeros(B, dtype=torch.int32, device=dev)
             self._active = torch.ones(B, dtype=torch.int32, device=dev)
 
@@ -173,8 +216,20 @@ class RankRSolver:
             if hasattr(self, name):
                 setattr(self, name, None)
 
+    def split_block_t(self, X):
+        """K-blocked split-fp16 halves of X^T (B, p, k) at X3_SCALE, in the solver's iterate
+        buffers (valid until the next solve)."""
+        K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
+        return self._xh[0], self._xl[0]
+
     def _fill_G(self, Y):
-        """fp32 G = Y Y^T (m <= n) or Y^T Y on the fp32 MFMA GEMM (upper tiles + mirror)."""
+        """fp32 G = Y Y^T (m <= n) or Y^T Y: from the Gram operand's split halves when the
+        caller provided them (Y itself may not exist in fp32), else on the fp32 MFMA GEMM."""
+        if self._y_halves is not None:
+            yh, yl, ys = self._y_halves
+            K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), self._G, tri=True, a_blocked=True, b_blocked=True)
+            self._G.copy_(torch.triu(self._G) + torch.triu(self._G, 1).transpose(1, 2))
+            return
         if self.left:
             K.gemm(Y, Y, tb=True, C=self._G, syrk=True)
         else:
@@ -319,6 +374,7 @@ class RankRSolver:
         self._alloc(dev)
         self._g_upper_only = False
         self._Y = Y
+        self._y_halves = None
         g_split = False
         if self.x3 and (self.n if self.left else self.m) % 32 == 0:
             # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two;
@@ -328,8 +384,9 @@ class RankRSolver:
                 yh, yl, ys, ysq = y_split
             else:
                 if self._yh is None:
-                    self._yh = torch.empty((B, k, Y.shape[1] + Y.shape[2] - k), dtype=torch.float16, device=dev)
-                    self._yl = torch.empty_like(self._yh)
+                    yshape = (B, k, Y.shape[1] + Y.shape[2] - k)
+                    self._yh = scratch.get("solver.yh", yshape, torch.float16, dev)
+                    self._yl = scratch.get("solver.yl", yshape, torch.float16, dev)
                     self._ys = torch.empty(B, dtype=torch.float32, device=dev)
                 yh, yl, ys = self._yh, self._yl, self._ys
                 K.pow2_scale(Y, 14, out=ys)
@@ -338,6 +395,7 @@ class RankRSolver:
                 else:
                     K.transpose_split(Y, hi=yh, lo=yl, scale=ys, blocked=True)
             yinv = 1.0 / (ys * ys)
+            self._y_halves = (yh, yl, ys)
             if ysq is None:
                 ysq = K.weighted_sqsum(Y, None, Y.shape[2])
             K.gemm_x3(yh, yl, yh, yl, yinv, None, tri=True, a_blocked=True, b_blocked=True,

@@ -319,13 +319,15 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  * inv_scale[b] = 1 / (scale_L * scale_R)) and never written; two passes over W (absmax, then
  * quantise).  r = 0 (no LR yet): res = W exactly, factor pointers may be NULL.  Outputs:
  * packed offset-binary codes (bits 2/4) and/or int8/int16 codes, scale_out[b] =
- * max(max|res|, eps), err_out[b] = sum_ij err_w[j] (deq - res)^2 (fp64; err_w NULL = 1). */
+ * max(max|res|, eps), err_out[b] = sum_ij err_w[j] (deq - res)^2 (fp64; err_w NULL = 1).
+ * absmax_in (r = 0 only, may be NULL): max|W[b]| already known (cq_absmax of the same W),
+ * so the absmax pass is skipped and W is read once. */
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch);
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
                    const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
                    const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,
-                   float* scale_out, const float* err_w, double* err_out, void* ws,
-                   size_t ws_bytes, void* stream);
+                   float* scale_out, const float* err_w, double* err_out, const float* absmax_in,
+                   void* ws, size_t ws_bytes, void* stream);
 
 /* Chebyshev 3-term recurrence support and elementwise helpers. */
 /* out[b] = sum(x[b]^2 * w[j % ncols]) fp64 (w may be NULL) — denominators of alg.py:298 */

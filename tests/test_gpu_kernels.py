@@ -646,3 +646,61 @@ def test_gram_sym_split_output(K, n, kd):
         tol = 2.0 ** -24 / min(float(s[b]), float(rs[b]))
         assert float((H / float(s[b]) - Gr).abs().max()) <= tol
         assert tol <= 2.0 ** -22 * float(Gr.abs().max())  # still fp32-grade
+
+
+@pytest.mark.parametrize("bits", [2, 4, 8, 16])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_q_update_known_absmax_stream(K, bits, dtype):
+    """First Q step with max|W| known (streaming kernel, one pass) == the two-pass fused
+    update: identical codes and scale, error equal to fp64 summation order."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B, m, n = 3, 192, 1040
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.02).to(dtype)
+    W[1, 7, 33] = 0.5  # a planted maximum
+    ew = torch.rand(n, device=DEV, generator=g) + 0.5
+    packed = bits <= 4
+    outs = []
+    for amax in (None, K.absmax(W)):
+        codes = torch.empty(B, m * n, dtype=K.code_dtype(bits), device=DEV)
+        pk = torch.empty(B, m * n * bits // 8, dtype=torch.uint8, device=DEV) if packed else None
+        sc = torch.empty(B, device=DEV)
+        err = torch.empty(B, dtype=torch.float64, device=DEV)
+        K.q_update_x3(W, None, None, bits, codes=codes, packed=pk, scale=sc, err_w=ew, err_out=err, absmax_in=amax)
+        outs.append((codes, pk, sc, err))
+    (c0, p0, s0, e0), (c1, p1, s1, e1) = outs
+    assert torch.equal(c0, c1) and torch.equal(s0, s1)
+    if packed:
+        assert torch.equal(p0, p1)
+    assert torch.allclose(e0, e1, rtol=1e-12, atol=0)
+    # codes against the oracle's uniform quantiser of the same W
+    for b in range(B):
+        x = W[b].float().cpu().numpy().reshape(1, -1)
+        ref_c, ref_s = O.quantize_uniform(x, bits, block_size=m * n)
+        assert np.array_equal(c1[b].cpu().numpy().reshape(1, -1), ref_c.reshape(1, -1))
+        assert float(s1[b]) == float(np.asarray(ref_s).reshape(-1)[0])
+
+
+@pytest.mark.parametrize("bits", [2, 4, 8, 16])
+def test_q_update_kernels_kat_bit_exact(K, kat, bits):
+    """The fused Q-update kernels (two-pass and the known-max streaming pass, both with the
+    one-divisor correctly rounded division) reproduce the reference's whole-matrix KAT codes,
+    scale and quantisation error bit for bit, ties included; inputs are zero-padded to a
+    multiple of 16 columns (zeros change neither the max nor the other codes)."""
+    for name in _inputs(kat):
+        x = kat["in_" + name].reshape(-1).astype(np.float32)
+        key = f"uniform_b{bits}_bsall_{name}"
+        npad = -(-x.size // 16) * 16
+        xp = np.zeros(npad, np.float32)
+        xp[: x.size] = x
+        W = torch.from_numpy(xp).to(DEV).view(1, 1, npad)
+        d32 = (kat[key + "_deq"].reshape(-1).astype(np.float32) - x).astype(np.float32)
+        e_ref = float((d32 * d32).astype(np.float64).sum())
+        for amax in (None, K.absmax(W)):
+            codes = torch.empty(1, npad, dtype=K.code_dtype(bits), device=DEV)
+            sc = torch.empty(1, device=DEV)
+            err = torch.empty(1, dtype=torch.float64, device=DEV)
+            K.q_update_x3(W, None, None, bits, codes=codes, scale=sc, err_out=err, absmax_in=amax)
+            np.testing.assert_array_equal(codes.cpu().numpy()[0, : x.size], kat[key + "_codes"].reshape(-1), err_msg=key)
+            assert float(sc[0]) == float(kat[key + "_scale"].reshape(-1)[0]), key
+            # the kernels sum d^2 in fp32 within runs of 4 elements, in fp64 across runs
+            assert float(err[0]) == pytest.approx(e_ref, rel=1e-6, abs=1e-30), key

@@ -5,6 +5,7 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeou
 tail -15 gpurun_out/gpu_all.log
 [ $rc -eq 0 ] || exit $rc
 [ -n "$NO_BENCH" ] && exit 0
-timeout -k 10 600 python3 bench.py ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/bench.log 2>&1; rc=$?
+if [ "$1" = full ]; then BA=""; else BA="--no-cpu-baseline"; fi
+timeout -k 10 600 python3 bench.py $BA > gpurun_out/bench.log 2>&1; rc=$?
 grep -v amdgpu.ids gpurun_out/bench.log | tail -3
 exit $rc
