@@ -63,6 +63,7 @@ class X3Args(ctypes.Structure):
         ("out_bound", c_vp),
         ("scale_out", c_vp),
         ("inv_out", c_vp),
+        ("single", c_int),
     ]
 
 
@@ -552,7 +553,8 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
-            a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None):
+            a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
+            single=False):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
@@ -590,6 +592,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.active = active.data_ptr() if active is not None else None
     g.a_blocked = int(a_blocked)
     g.o_blocked = int(bool(o_blocked))
+    g.single = int(bool(single))
     if sym_bound is not None:
         g.sym_out = 1
         g.out_bound, g.scale_out, g.inv_out = sym_bound.data_ptr(), scale_out.data_ptr(), inv_out.data_ptr()

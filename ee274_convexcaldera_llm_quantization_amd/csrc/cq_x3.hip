@@ -50,6 +50,7 @@ struct X3K {
     int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
     int64_t tiles_n, tiles_m;
     int probe;  // accumulate shader / constant-clock ticks per workgroup (clock diagnostics)
+    int single;                // one product hi x hi (lo halves not read): ~2^-11 relative
     int sym_out;               // tri Gram: write the blocked split of the symmetric C (mirrored upper)
     const double* out_bound;   // [batch] bound on max|C|: split scale 2^(14 - e)
     float* scale_out;          // [batch] that scale
@@ -442,6 +443,41 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _F
     }
 }
 
+// Hi-only load plan (single product): the 36 hi-half wave-instructions of a stage spread
+// 3 per wave (Ah 0-11, Bh 12-35).
+constexpr int XW1_PER_WAVE = 3;
+__device__ __forceinline__ void xw1_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
+                                         uint32_t (&off)[XW1_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW1_PER_WAVE; ++u) {
+        const int I = wid * XW1_PER_WAVE + u;
+        const bool isA = I < 12;
+        const int sub = isA ? I : I - 12;
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        const int64_t lim = isA ? a.M : a.N;
+        int64_t gr = (isA ? m0 : n0) + row;
+        gr = gr < lim ? gr : lim - 1;
+        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * 32 + c * 8 : gr * a.lda + c * 8)
+                                : (a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8));
+    }
+}
+
+__device__ __forceinline__ void xw1_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                          const uint32_t (&off)[XW1_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW1_PER_WAVE; ++u) {
+        const int I = wid * XW1_PER_WAVE + u;
+        const bool isA = I < 12;
+        const int sub = isA ? I : I - 12;
+        const _Float16* base = isA ? a.Ah + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
+                                   : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
+        _Float16* dst = stage + (isA ? 0 : 2 * XW_APART) + (16 * sub) * XW_BK;
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
+                                         16, 0, 0);
+    }
+}
+
 // The 192 x 384 tile's K loop (shared by the filter/Gram product and the fused Q update):
 // acc = A[m0.., :] B[n0.., :]^T over K, split-fp16 products; nt = 0 leaves acc = 0.
 template <int MODE = 0>
@@ -683,7 +719,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
 // PERMB: block j's B fragment row for output register index t = 4 lq + r is LDS row
 // 64 wn + 16 (t >> 2) + 4 j + (t & 3), so lane (l16, lq) ends up holding the 16 consecutive
 // B rows 64 wn + 16 lq + [0, 16) in acc[i][0..3][0..3] (used by the fused Q update).
-template <bool PERMB = false>
+template <bool PERMB = false, bool X1 = false>
 __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
                                             f32x4v (&acc)[6][4]) {
@@ -693,16 +729,21 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
     wid = __builtin_amdgcn_readfirstlane(wid);
-    uint32_t off[XW_PER_WAVE];
+    uint32_t off[X1 ? XW1_PER_WAVE : XW_PER_WAVE];
+    auto issue = [&](int64_t k0, _Float16* st) {
+        if constexpr (X1) xw1_issue(a, b, k0, st, wid, off);
+        else xw_issue(a, b, k0, st, wid, off);
+    };
     if (nt > 0) {
-        xw_plan(a, m0, n0, wid, lane, off);
-        xw_issue(a, b, 0, smem, wid, off);
+        if constexpr (X1) xw1_plan(a, m0, n0, wid, lane, off);
+        else xw_plan(a, m0, n0, wid, lane, off);
+        issue(0, smem);
     }
     for (int64_t t = 0; t < nt; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
-        if (t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
+        if (t + 1 < nt) issue((t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE);
         const _Float16* sA = smem + (t & 1) * XW_STAGE;
         const _Float16* sB = sA + 2 * XW_APART;
         f16x8 bh[4], bl[4];
@@ -710,12 +751,18 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
         for (int j = 0; j < 4; ++j) {
             const int row = PERMB ? 64 * wn + 16 * (l16 >> 2) + 4 * j + (l16 & 3) : 64 * wn + 16 * j + l16;
             bh[j] = xg_frag(sB, row, lq);
-            bl[j] = xg_frag(sB + XW_BPART, row, lq);
+            if constexpr (!X1) bl[j] = xg_frag(sB + XW_BPART, row, lq);
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const int row = 96 * wm + 16 * i + l16;
             const f16x8 ah = xg_frag(sA, row, lq);
+            if constexpr (X1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+                continue;
+            }
             const f16x8 al = xg_frag(sA + XW_APART, row, lq);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {  // transposed block: lanes run over A rows, registers over B rows
@@ -727,6 +774,7 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
     }
 }
 
+template <bool X1>
 __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     extern __shared__ __attribute__((aligned(16))) char xv_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(xv_smem_raw);
@@ -748,7 +796,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
 
     f32x4v acc[6][4];
     const bool live = !a.active || a.active[b];
-    xv_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+    xv_mainloop<false, X1>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
 
     const float sc = a.inv_scale[b];
     if (a.sym_out) {
@@ -1873,6 +1921,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.overflow = g->overflow;
     CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && (!g->out_h || g->sym_out)),
                "cq_gemm_x3: tri needs a square plain product");
+    a.single = g->single;
+    CQ_REQUIRE(!g->single || !g->sym_out, "cq_gemm_x3: single-product mode is for the filter");
     a.sym_out = g->sym_out;
     a.out_bound = g->out_bound;
     a.scale_out = g->scale_out;
@@ -1903,7 +1953,7 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     }();
     CQ_REQUIRE(variant >= 2 || (!g->a_blocked && !g->o_blocked),
                "cq_gemm_x3: blocked A / split output need the LDS-DMA 192x384 kernel");
-    CQ_REQUIRE(variant == 8 || !g->sym_out, "cq_gemm_x3: sym_out needs the default kernel");
+    CQ_REQUIRE(variant == 8 || (!g->sym_out && !g->single), "cq_gemm_x3: sym_out / single need the default kernel");
     if (variant >= 2) {
         a.tiles_n = ceil_div(g->N, XW_BN);
         a.tiles_m = ceil_div(g->M, XW_BM);
@@ -1914,7 +1964,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         else if (variant == 5) gemm_x3w_kernel<2, 2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
         else if (variant == 6) gemm_x3w_kernel<4, 1><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
         else if (variant == 7) gemm_x3w_kernel<4, 2><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 8) gemm_x3v_kernel<<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 8 && a.single) gemm_x3v_kernel<true><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+        else if (variant == 8) gemm_x3v_kernel<false><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
         else gemm_x3w_kernel<4><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
     } else if (variant == 0 || g->b_blocked) {
         a.tiles_n = ceil_div(g->N, XG_BN);

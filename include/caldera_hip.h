@@ -285,6 +285,8 @@ typedef struct cq_x3_args {
     const double* out_bound;       /* [batch] bound on max|C[b]| (e.g. ||Y||_F^2 for Y Y^T) */
     float* scale_out;              /* [batch] s[b] */
     float* inv_out;                /* [batch] 1 / (s[b] * out_scale) */
+    int single;                    /* one fp16 product hi x hi (Al, Bl not read): ~2^-11
+                                      relative, for filter steps whose error later steps damp */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
