@@ -253,13 +253,17 @@ class RankRSolver:
         K.gemm(X, Wt32, C=out)
         return out, info
 
-    def _rr(self, X, *keep):
+    def _rr(self, X, *keep, single=False):
+        """Rayleigh-Ritz on the block X.  single: Z = G X with one fp16 product (cheap outer
+        iterations: the Ritz values only set the next filter's bounds, and the residuals it
+        reports sit at the ~1.5e-4 floor of that product, far above the tolerance, so no
+        matrix can be declared converged on them)."""
         G = self._G
         Z = self._free(X, *keep)
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
             K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
             K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked,
-                      a_blocked=True)
+                      a_blocked=True, single=single and self._x3f)
             K.transpose_split(self._xt[0], out=Z)
         else:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
@@ -435,7 +439,7 @@ class RankRSolver:
             X.copy_(torch.randn((1, k, p), generator=g, device=dev, dtype=torch.float32).expand(B, k, p))
             X, _ = self._cholqr(X)
             X, _ = self._cholqr(X)
-            theta, X, Z = self._rr(X)
+            theta, X, Z = self._rr(X, single=self.cheap_cold > 0)
             ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
             yield
             ends = ends.cpu().numpy()
@@ -457,10 +461,11 @@ class RankRSolver:
             self.stats.outer += 1
             while True:
                 coef = self._cheb_coeffs(ends, d, dev)
-                Xf = self._filter(X, coef, single=n_outer <= (self.cheap_cold if cold else self.cheap_warm))
+                cheap = n_outer <= (self.cheap_cold if cold else self.cheap_warm)
+                Xf = self._filter(X, coef, single=cheap)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._cholqr(Xa, X)
-                theta_n, Xn, Zn = self._rr(Xb, X)
+                theta_n, Xn, Zn = self._rr(Xb, X, single=cheap)
                 res = K.ritz_residual(Xn, Zn, theta_n, self.r)  # (B,) per-matrix max residual
                 ovf = (self._ovf.max().double() if self.x3 and self._x3f
                        else torch.zeros((), dtype=torch.float64, device=dev))
