@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcaldera_hip.so")
 
-CQ_F32, CQ_F16 = 0, 1
+CQ_F32, CQ_F16, CQ_BF16 = 0, 1, 2
 EPI_LINEAR, EPI_RESID, EPI_WERR = 0, 1, 2
 CQ_EINVAL, CQ_EHIP, CQ_EWORKSPACE = -1, -2, -3
 
@@ -119,6 +119,9 @@ _SIGS = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_act_sqsum_workspace": (c_size, [c_i64, c_i64]),
+    "cq_act_sqsum_cols": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp, c_size, c_vp]),
+    "cq_act_sqsum_rows": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -147,7 +150,17 @@ class CalderaHipError(RuntimeError):
     pass
 
 
+_SYNC_CHECK = bool(os.environ.get("CQ_SYNC_CHECK"))
+
+
 def _check(st: int, what: str):
+    if _SYNC_CHECK and st == 0:  # debugging: attribute an asynchronous fault to its launch
+        import sys
+        import traceback
+        fr = traceback.extract_stack(limit=4)
+        print(f"[cq] {what} <- {' <- '.join(f'{f.name}:{f.lineno}' for f in reversed(fr[:-1]))}",
+              file=sys.stderr, flush=True)
+        torch.cuda.synchronize()
     if st != 0:
         msg = load().cq_last_error().decode(errors="replace")
         if st == CQ_EINVAL:
@@ -570,6 +583,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     assert Bh.shape[2] == Kd and (C is None or C.shape == (Bt, M, N))
     for t in (Ah, Al, Bh, Bl, C, P, D, out_h, out_l):
         assert t is None or t.is_contiguous()
+    for t in (out_h, out_l):  # the split output is M x N per matrix (sym_out: M = N)
+        assert t is None or t.numel() >= Bt * M * N, "gemm_x3: split output buffer too small"
     g = X3Args()
     g.M, g.N, g.K, g.batch = M, N, Kd, Bt
     g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (MA if a_blocked else Kd), MA * Kd
@@ -666,3 +681,45 @@ def residual_split(Ws, packed, qscale, bits, wmax, *, ycol=None, ycol_max=1.0, r
     _check(lib.cq_residual_split(dt, _p(Ws), _p(packed), _p(qscale), int(bits), _p(ycol), float(ycol_max), _p(wmax),
                                  B, m, n, _p(res), _p(Y), _p(hi), _p(lo), _p(thi), _p(tlo), _p(scale), _p(sq), _p(ws),
                                  0 if ws is None else ws.numel(), _stream(Ws.device)), "cq_residual_split")
+
+
+# ---------------------------------------------------------------------------- calibration
+_ACT_DT = {torch.float32: CQ_F32, torch.float16: CQ_F16, torch.bfloat16: CQ_BF16}
+
+
+def _act_2d(x: torch.Tensor):
+    """(rows, cols) view with unit column stride, or a contiguous copy."""
+    if x.dtype not in _ACT_DT:
+        raise TypeError(f"activations must be fp32/fp16/bf16, got {x.dtype}")
+    if x.dim() != 2:
+        raise ValueError("activations must be 2-D (rows, cols)")
+    if x.stride(1) != 1 or (x.shape[0] > 1 and x.stride(0) < x.shape[1]):
+        x = x.contiguous()
+    return x, (x.stride(0) if x.shape[0] > 1 else x.shape[1])
+
+
+def act_sqsum_cols(x: torch.Tensor, out: torch.Tensor, *, accumulate: bool = True, post: float = 1.0):
+    """out (cols,) fp64 <- ((accumulate ? out : 0) + sum_i x[i, :]^2) * post  (diag of X^T X)."""
+    _require_hip(x, out)
+    x, ld = _act_2d(x)
+    rows, cols = x.shape
+    assert out.dtype == torch.float64 and out.numel() == cols and out.is_contiguous()
+    lib = load()
+    nws = lib.cq_act_sqsum_workspace(rows, cols)
+    ws = workspace(nws, x.device) if nws else None
+    _check(lib.cq_act_sqsum_cols(_ACT_DT[x.dtype], _p(x) if rows else None, rows, cols, max(ld, cols), _p(out),
+                                 int(bool(accumulate)), float(post), _p(ws), 0 if ws is None else ws.numel(),
+                                 _stream(x.device)), "cq_act_sqsum_cols")
+    return out
+
+
+def act_sqsum_rows(x: torch.Tensor, out: torch.Tensor, *, accumulate: bool = True, post: float = 1.0):
+    """out (rows,) fp64 <- ((accumulate ? out : 0) + sum_j x[:, j]^2) * post  (diag of X X^T)."""
+    _require_hip(x, out)
+    x, ld = _act_2d(x)
+    rows, length = x.shape
+    assert out.dtype == torch.float64 and out.numel() == rows and out.is_contiguous()
+    _check(load().cq_act_sqsum_rows(_ACT_DT[x.dtype], _p(x) if length else None, rows, length, max(ld, length),
+                                    _p(out), int(bool(accumulate)), float(post), _stream(x.device)),
+           "cq_act_sqsum_rows")
+    return out

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcaldera_hip.so")
-SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_codebook.hip"]
+SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_codebook.hip", "cq_calib.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          # bit-exact quantiser: no FMA contraction, IEEE-correct fp32 division/sqrt
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"]
@@ -33,13 +33,25 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Each source compiles to its own object in parallel (no relocatable device code: every
+    kernel is launched from its own translation unit), then one link."""
     if not force and not needs_build():
         return OUT
+    objdir = os.path.join(HERE, "_build")
+    os.makedirs(objdir, exist_ok=True)
+    procs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        cmd = [hipcc(), *[f for f in FLAGS if f != "-shared"], "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), src))
+    failed = [src for p, src in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError(f"hipcc failed on {failed}")
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    subprocess.run([hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, OUT)
     return OUT
 

@@ -353,8 +353,11 @@ class CalderaEngine:
             # Y^T (operand of R = U^T Y on split-fp16 products); res / Y in fp32 only where a
             # later step still reads them (quantised factors, wide-right shapes)
             if self._yh is None:  # cached scratch (scratch.py)
-                self._yh = scratch.get("lr.yh", (B, m, n), torch.float16, dev)
-                self._yl = scratch.get("lr.yl", (B, m, n), torch.float16, dev)
+                # shaped as the Gram operand (Y, or Y^T when m > n): the split products take
+                # their M / K from these shapes
+                gshape = (B, m, n) if sv.left else (B, n, m)
+                self._yh = scratch.get("lr.yh", gshape, torch.float16, dev)
+                self._yl = scratch.get("lr.yl", gshape, torch.float16, dev)
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
             halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)

@@ -397,6 +397,8 @@ class RankRSolver:
             ysq = None
             if y_split is not None:
                 yh, yl, ys, ysq = y_split
+                # the Gram operand: Y (k x n) when m <= n, Y^T (k x m) otherwise
+                assert yh.shape == (B, k, Y.shape[1] + Y.shape[2] - k), "solver: Gram operand halves misshaped"
             else:
                 if self._yh is None:
                     yshape = (B, k, Y.shape[1] + Y.shape[2] - k)

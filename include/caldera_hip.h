@@ -38,6 +38,7 @@ extern "C" {
 /* dtype tags */
 #define CQ_F32 0
 #define CQ_F16 1
+#define CQ_BF16 2
 
 int cq_abi_version(void);
 const char* cq_last_error(void);
@@ -343,6 +344,23 @@ int cq_scale_rc(const float* X, int64_t ldx, int64_t stride_x, int trans_x, floa
                 int64_t ldy, int64_t stride_y, int64_t rows, int64_t cols, int64_t batch,
                 const float* rowscale, int64_t rowscale_stride, const float* colscale,
                 int64_t colscale_stride, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Hessian calibration.  Replaces the activation accumulation of
+ * main.py:296-308 (a_aT = A A^T in float64, summed over samples) for the diagonal that
+ * diag_Hessians.pt ships (`Hall[name]`, main.py:163).  Activations x (fp32 | fp16 | bf16).
+ *
+ * cq_act_sqsum_cols: out[j] = (accumulate ? out[j] : 0) + sum_i x[i*ld + j]^2, then * post
+ *   (rows x cols, row stride ld): diag(X^T X) of a token-major activation block — the
+ *   per-channel sum over tokens.  fp64 accumulation in a fixed order (deterministic).
+ * cq_act_sqsum_rows: out[i] = (accumulate ? out[i] : 0) + sum_j x[i*ld + j]^2, then * post
+ *   — diag(X X^T) of the reference's `activations.view(D, -1)` (main.py:302-305).
+ * post = 1/(idx+1) reproduces main.py:307's running division. */
+size_t cq_act_sqsum_workspace(int64_t rows, int64_t cols);
+int cq_act_sqsum_cols(int dtype, const void* x, int64_t rows, int64_t cols, int64_t ld, double* out,
+                      int accumulate, double post, void* ws, size_t ws_bytes, void* stream);
+int cq_act_sqsum_rows(int dtype, const void* x, int64_t rows, int64_t len, int64_t ld, double* out,
+                      int accumulate, double post, void* stream);
 
 #ifdef __cplusplus
 }

@@ -185,3 +185,24 @@ def test_solver_filter_precisions(prec, monkeypatch):
         P1 = U[b].double().cpu() @ U[b].double().cpu().T
         P2 = V @ V.T
         assert torch.linalg.norm(P1 - P2) / math.sqrt(r) < 1e-4
+
+
+@pytest.mark.parametrize("m,n,r,dtype,diag_h", [(640, 512, 32, torch.float32, True), (1024, 512, 64, torch.float16, False),
+                                                 (512, 640, 32, torch.float32, True)])
+def test_tall_and_wide_vs_oracle(api, m, n, r, dtype, diag_h):
+    """m > n: the solver works on Y^T Y (right singular vectors) with the split-fp16 Gram
+    operand written transposed by the residual pass; L = Y V / S (alg.py:217-225)."""
+    caldera, CP, _ = api
+    g = torch.Generator().manual_seed(m + n)
+    W = (torch.randn(m, n, generator=g) * 0.02).to(dtype)
+    h = (torch.rand(n, generator=g) + 0.05) if diag_h else None
+    kw = dict(Q_bits=2, L_bits=16, R_bits=16, rank=r, iters=3, update_order=["Q", "LR"], sigma_reg=1e-8)
+    d = caldera(CP(**kw), W.to(DEV), None if h is None else torch.diag_embed(h).to(DEV), device=DEV,
+                use_tqdm=False)
+    ref = O.caldera(O.Params(**kw), W.numpy(), None if h is None else np.diag(h.numpy()))
+    assert abs(d.errors["Q"][0] - ref.errors["Q"][0]) < 1e-6
+    assert abs(d.errors["LR"][0] - ref.errors["LR"][0]) < 1e-5
+    np.testing.assert_allclose(d.errors["LR"], ref.errors["LR"], rtol=0, atol=1e-2)
+    out = (d.Q.double() + d.L.double() @ d.R.double()).cpu().numpy()
+    exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
+    assert np.linalg.norm(out - exp) / np.linalg.norm(exp) < 1e-4
