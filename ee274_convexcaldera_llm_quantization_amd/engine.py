@@ -336,6 +336,8 @@ class CalderaEngine:
         if self.solver is None:
             self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
                                       filter_precision=self.filter_precision, **self.solver_kwargs)
+            if not self.solver.left and self._n_true < n:
+                self.solver.valid_k = self._n_true
         sv = self.solver
         y_split = None
         ysq = None
@@ -575,14 +577,30 @@ class CalderaEngine:
         dev = W.device
         if W.dtype not in (torch.float16, torch.float32):
             W = W.float()
-        if n % 4:
-            raise NotImplementedError("caldera-mi355x: W.shape[1] must be a multiple of 4")
+        pad = (-n) % 4
+        if pad and (p.method_Q != "uniform" or p.method_LR != "uniform" or (h is not None and h.dim() == 2)):
+            raise NotImplementedError("caldera-mi355x: W.shape[1] % 4 != 0 needs uniform quantisers and a "
+                                      "diagonal (or no) H")
         if p.compute_quantized_component and "Q" in p.update_order:
             qlog.check_method_bits(p.method_Q, p.Q_bits)  # get_quant_info (alg.py:238-242)
         if p.compute_low_rank_factors and "LR" in p.update_order and (p.L_bits < 16 or p.R_bits < 16):
             qlog.check_method_bits(p.method_LR, p.L_bits)
             qlog.check_method_bits(p.method_LR, p.R_bits)
-        gs, Ws = K.rms_scale(W, scale_W)
+        gs, Ws = K.rms_scale(W, scale_W)  # on the true numel (alg.py:38-42)
+        Ws_out = Ws
+        self._n_true = n
+        if pad:
+            # ragged n: zero columns up to a multiple of 4 (the kernels' vector width).  Zeros
+            # quantise to code 0 (dequantised 0) and leave every whole-matrix absmax, the
+            # residual, Y = res sqrt(h), R = U^T Y diag(1/sqrt h) and all error sums unchanged;
+            # h is padded with max(h) so sigma_reg's shift (alg.py:59-64) is the same; the
+            # solver keeps its block out of the padded rows when they are its rows (m > n).
+            # Outputs are cut back to n columns in _finalize.
+            n_true = n
+            Ws = torch.nn.functional.pad(Ws, (0, pad))
+            n = n + pad
+            if h is not None:
+                h = torch.cat([h, h.max().expand(pad)])
         wts = _Weights(h, n, p, dev)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
         self._yh = self._yl = self._ys = None
@@ -637,7 +655,25 @@ class CalderaEngine:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         self._yh = self._yl = None
         self._yth = self._ytl = None
-        return self._finalize(best, st, W, Ws, gs, errors, wts, spare=(work, res))
+        out = self._finalize(best, st, W, Ws_out, gs, errors, wts, spare=(work, res))
+        if pad:
+            out = [self._cut_columns(d, m, n, n_true) for d in out]
+            for lp in self.last_packed:  # packed codes stay in the padded (m, n + pad) grid
+                lp["R"] = lp["R"][:, :n_true]
+                lp["n_padded"] = n
+        return out
+
+    @staticmethod
+    def _cut_columns(d, m, n_pad, n):
+        """Drop the zero-padding columns of a result dict (ragged n)."""
+        d["Q"] = d["Q"][:, :n]
+        if torch.is_tensor(d["Q_idxs"]):
+            d["Q_idxs"] = d["Q_idxs"].view(m, n_pad)[:, :n].reshape(1, m * n)
+        r = d["R"].shape[0]
+        d["R"] = d["R"][:, :n]
+        if torch.is_tensor(d["R_idxs"]):
+            d["R_idxs"] = d["R_idxs"].view(r, n_pad)[:, :n].reshape(1, r * n)
+        return d
 
     def _state_error(self, st, Ws, work, wts):
         B, m, n = st.B, st.m, st.n

@@ -169,6 +169,7 @@ class RankRSolver:
         self.X = None      # warm-start Ritz block (B, k, p)
         self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
         self.stats = SolverStats()
+        self.valid_k = self.k  # rows >= valid_k of the eigenproblem are zero padding (engine.py)
         self._bufs = None
         self._G = None
         self._yh = self._yl = None
@@ -344,9 +345,12 @@ class RankRSolver:
         # bytes a recurrence step moves: G halves (4 B/elem) + X^T halves + prev, cur in,
         # new out (fp32) + new halves out
         nb = float(self.B) * (4.0 * self.k * self.k + 20.0 * self.p * self.k)
-        kn = "gemm_x3_kernel (split-fp16 G X, Chebyshev filter)"
+        kn = "gemm_x3v_kernel<false> (split-fp16 G X, Chebyshev filter)"
+        # the probe (bench.py's roofline) times the split-fp16 steps only: a single-product
+        # step moves 2k^2 + 18pk bytes per matrix, not the 4k^2 + 20pk counted here
+        probe = EVENT_PROBE.start if not single else (lambda *a: None)
         last = deg == 1
-        ev = EVENT_PROBE.start(fl, nb, kn)
+        ev = probe(fl, nb, kn)
         K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
                   gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
                   out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked, active=self._active,
@@ -356,7 +360,7 @@ class RankRSolver:
         prev, cur = 0, 1
         for i in range(1, deg):
             last = i == deg - 1
-            ev = EVENT_PROBE.start(fl, nb, kn)
+            ev = probe(fl, nb, kn)
             K.gemm_x3(xh[cur], xl[cur], self._Gh, self._Gl, self._ginv, xt[prev], P=xt[prev], D=xt[cur],
                       alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
                       out_h=None if last else xh[prev], out_l=None if last else xl[prev],
@@ -439,6 +443,8 @@ class RankRSolver:
             g = torch.Generator(device=dev)
             g.manual_seed(self.seed)
             X.copy_(torch.randn((1, k, p), generator=g, device=dev, dtype=torch.float32).expand(B, k, p))
+            if self.valid_k < k:  # zero-padded columns of W (engine.py): keep the block out of them
+                X[:, self.valid_k:, :] = 0.0
             X, _ = self._cholqr(X)
             X, _ = self._cholqr(X)
             theta, X, Z = self._rr(X, single=self.cheap_cold > 0)

@@ -206,3 +206,35 @@ def test_tall_and_wide_vs_oracle(api, m, n, r, dtype, diag_h):
     out = (d.Q.double() + d.L.double() @ d.R.double()).cpu().numpy()
     exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
     assert np.linalg.norm(out - exp) / np.linalg.norm(exp) < 1e-4
+
+
+@pytest.mark.parametrize("m,n,r,qb,lrb,dtype", [
+    (333, 517, 20, 4, 16, torch.float16),    # k % 32 != 0: fp32 MFMA solver path
+    (517, 333, 20, 2, 16, torch.float32),    # tall ragged
+    (333, 517, 20, 2, 4, torch.float16),     # ragged with 4-bit factors (LPLR loop)
+    (960, 1440, 64, 2, 16, torch.float16),   # split-fp16 solver, n % 64 != 0 (no fused residual pass)
+    (1000, 700, 40, 4, 16, torch.float32),   # tall, k % 32 != 0
+])
+def test_ragged_shapes_vs_oracle(api, m, n, r, qb, lrb, dtype):
+    """Shapes off every kernel's preferred multiple (ragged tiles, scalar tails)."""
+    caldera, CP, _ = api
+    g = torch.Generator().manual_seed(m * 3 + n)
+    W = (torch.randn(m, n, generator=g) * 0.02).to(dtype)
+    h = torch.rand(n, generator=g) + 0.05
+    kw = dict(Q_bits=qb, L_bits=lrb, R_bits=lrb, rank=r, iters=2, lplr_iters=3, update_order=["Q", "LR"],
+              sigma_reg=1e-8)
+    d = caldera(CP(**kw), W.to(DEV), torch.diag_embed(h).to(DEV), device=DEV, use_tqdm=False)
+    ref = O.caldera(O.Params(**kw), W.numpy(), np.diag(h.numpy()))
+    if dtype == torch.float16:  # fp16 mean: exact; fp32: torch CPU's fp32 summation order is not replayed
+        assert d.global_scale == ref.global_scale
+    else:
+        assert abs(d.global_scale - ref.global_scale) <= 2e-7 * ref.global_scale
+    assert abs(d.errors["Q"][0] - ref.errors["Q"][0]) < 1e-6
+    if lrb == 16:
+        assert abs(d.errors["LR"][0] - ref.errors["LR"][0]) < 1e-5
+        out = (d.Q.double() + d.L.double() @ d.R.double()).cpu().numpy()
+        exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
+        assert np.linalg.norm(out - exp) / np.linalg.norm(exp) < 1e-4
+    else:  # quantised factors: chaotic code flips (SURVEY.md §7.3-2), compared loosely
+        np.testing.assert_allclose(d.errors["LR"], ref.errors["LR"], rtol=0, atol=2e-2)
+    assert d.Q.shape == (m, n) and d.L.shape == (m, r) and d.R.shape == (r, n)

@@ -23,6 +23,23 @@ def stats(d):
               f"{float(r['AverageNs']) / 1e3:10.1f}  {r['Name'][:110]}")
 
 
+def by_grid(d, pattern="gemm_x3v_kernel"):
+    """Launches of the split-fp16 product kernels grouped by (instantiation, grid): the filter,
+    Rayleigh-Ritz and U^T Y products share one grid (M = p rows, N = k), the Gram has its own."""
+    fs = glob.glob(os.path.join(d, "*kernel_trace.csv"))
+    if not fs:
+        return
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(fs[0])):
+        if pattern in r["Kernel_Name"]:
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            agg[(r["Kernel_Name"], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))].append(dur)
+    print(f"# {pattern} launches by grid: {fs[0]}")
+    print(f"{'calls':>6} {'avg_us':>10} {'workgroups':>10}  kernel")
+    for (k, g), v in sorted(agg.items(), key=lambda x: -sum(x[1])):
+        print(f"{len(v):>6} {sum(v) / len(v):10.1f} {g:>10}  {k[:80]}")
+
+
 def pmc(d):
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
     rows = list(csv.DictReader(open(f)))
@@ -37,6 +54,8 @@ def pmc(d):
 
 if __name__ == "__main__":
     stats(sys.argv[1])
+    print()
+    by_grid(sys.argv[1])
     for d in sys.argv[2:]:
         print()
         pmc(d)
