@@ -739,6 +739,25 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
         else xw_plan(a, m0, n0, wid, lane, off);
         issue(0, smem);
     }
+    // a wave whose 96 x 64 output block lies wholly past the matrix edge (ragged last tiles)
+    // or, for a symmetric Gram (tri), wholly below the diagonal is never stored: it runs only
+    // its share of the loads and barriers, no fragment reads or MFMAs (power-bound kernel:
+    // fewer MFMA joules per launch; per-strip or per-block skips inside the K loop make the
+    // register allocator spill the accumulators)
+    // (PERMB: a fragment's 16 columns interleave with stride 16 across the wave's 64; the
+    // wave-level test below only needs the block's first row and column)
+    const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
+    uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
+    live = __builtin_amdgcn_readfirstlane(live);
+    if (!live) {  // the wave's whole 96 x 64 block is dead: its share of the loads and barriers only
+        for (int64_t t = 0; t < nt; ++t) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < nt) issue((t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE);
+        }
+        return;
+    }
     for (int64_t t = 0; t < nt; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
