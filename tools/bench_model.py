@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--sequential", action="store_true",
+                    help="one batch after another (default: all shape batches at once, each engine on "
+                         "its own HIP stream, overlap.py)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -64,7 +67,19 @@ def main():
     t0 = time.perf_counter()
     results = []
     per_shape = {}
-    for part, W in batches:
+    if not args.sequential:
+        from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
+        engines = [CalderaEngine(eng_params) for _ in batches]
+        run_interleaved([e.run_iter(W) for e, (_, W) in zip(engines, batches)], dev)
+        for eng, (part, W) in zip(engines, batches):
+            for (name, m, n, seed), d in zip(part, eng.last_packed):
+                results.append(S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"],
+                                              d["L"], d["R"], d["global_scale"], d["errors"]))
+        torch.cuda.synchronize()
+        batches_seq = []
+    else:
+        batches_seq = batches
+    for part, W in batches_seq:
         ts = time.perf_counter()
         eng = CalderaEngine(eng_params)
         eng.run(W)
@@ -92,7 +107,7 @@ def main():
             assert got == n_all, (got, n_all)
         print(json.dumps({"workload": "BASELINE configs[3]: Llama-2-7B linear weights (random-init fp16), r=128, Q2, "
                                       "L/R 16, iters 5, H=I",
-                          "layers": args.layers, "matrices": n_all, "n_gpus": world, "seconds": float(tmax.item()),
+                          "layers": args.layers, "interleave": not args.sequential, "matrices": n_all, "n_gpus": world, "seconds": float(tmax.item()),
                           "matrices_per_s": n_all / float(tmax.item()),
                           "rank0_seconds_by_shape": per_shape,
                           "extrapolated_full_model_s_at_this_world": float(tmax.item()) * 32 / args.layers,
