@@ -456,12 +456,15 @@ def spd_whiten(S: torch.Tensor, rcond2: float = 1e-30):
     return Wt32, Wt64, info
 
 
-def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want64=False):
-    """A (B, p, p) fp64 symmetric (overwritten) -> (evals desc (B,p) fp64, V32, V64, sweeps)."""
+def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want64=False, want_vectors=True):
+    """A (B, p, p) fp64 symmetric (overwritten) -> (evals desc (B,p) fp64, V32, V64, sweeps);
+    want_vectors=False: eigenvalues only (V32 = V64 = None; the p <= 192 register kernel then
+    skips its eigenvector rotations)."""
     _require_hip(A)
     B, p, _ = A.shape
     ev = torch.empty((B, p), dtype=torch.float64, device=A.device)
-    V32 = torch.empty((B, p, p), dtype=torch.float32, device=A.device)
+    V32 = torch.empty((B, p, p), dtype=torch.float32, device=A.device) if want_vectors else None
+    want64 = want64 and want_vectors
     V64 = torch.empty((B, p, p), dtype=torch.float64, device=A.device) if want64 else None
     sw = torch.empty(B, dtype=torch.int32, device=A.device)
     lib = load()

@@ -671,6 +671,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
     const int64_t b = blockIdx.x;
     const double* Ag = A_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool wantv = V32 != nullptr || V64 != nullptr;  // else eigenvalues only: no V work
     const int pg = lane & 31;                 // pair group
     const int rg = 2 * wid + (lane >> 5);     // row group
     const int k0 = pg * PPT, x0 = rg * RPT;
@@ -826,9 +827,10 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                         }
                     }
                 }
-                // ---- V rotations (registers)
+                // ---- V rotations (registers; skipped when only eigenvalues are wanted)
 #pragma unroll
                 for (int u = 0; u < ((CQ_JAC_ABL & 2) ? 0 : PPT); ++u) {
+                    if (!wantv) break;
                     const int k = k0 + u;
                     if (k < H) {
                         const float c = (float)cs[k], s = (float)sn[k];
@@ -847,6 +849,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             // ---- seat shift of V (every round, rotations or not)
 #pragma unroll
             for (int r = 0; r < ((CQ_JAC_ABL & 4) ? 0 : RPT); ++r) {
+                if (!wantv) break;
                 const float from_left = __shfl_up(ev[PPT - 1][r], 1, 32);   // ev of pair k0-1
                 const float from_right = __shfl_down(od[0][r], 1, 32);      // od of pair k0+PPT
                 float ne[PPT], no[PPT];

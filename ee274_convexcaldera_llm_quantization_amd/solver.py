@@ -27,6 +27,8 @@ the only host synchronisation is the convergence test once per outer iteration.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 
@@ -261,11 +263,13 @@ class RankRSolver:
         K.gemm(X, Wt32, C=out)
         return out, info
 
-    def _rr(self, X, *keep, single=False):
+    def _rr(self, X, *keep, single=False, values_only=False):
         """Rayleigh-Ritz on the block X.  single: Z = G X with one fp16 product (cheap outer
         iterations: the Ritz values only set the next filter's bounds, and the residuals it
         reports sit at the ~1.5e-4 floor of that product, far above the tolerance, so no
-        matrix can be declared converged on them)."""
+        matrix can be declared converged on them).  values_only: Ritz values only, X returned
+        unrotated and Z = None — the next filter sees the same subspace either way, so a
+        cheap iteration needs no eigenvectors, rotations or residuals."""
         G = self._G
         Z = self._free(X, *keep)
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
@@ -277,6 +281,9 @@ class RankRSolver:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
+        if values_only:
+            theta, _, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol, want_vectors=False)
+            return theta, X, None
         theta, V32, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol)
         Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
@@ -454,7 +461,7 @@ class RankRSolver:
                 X[:, self.valid_k:, :] = 0.0
             X, _ = self._cholqr(X)
             X, _ = self._cholqr(X)
-            theta, X, Z = self._rr(X, single=self.cheap_cold > 0)
+            theta, X, Z = self._rr(X, single=self.cheap_cold > 0, values_only=self.cheap_cold > 0)
             ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
             yield
             ends = ends.cpu().numpy()
@@ -466,6 +473,7 @@ class RankRSolver:
             X = self.X
             theta = self.theta
             ends = self._ends
+            Z = None
             degs = self.deg_warm
         self.stats.resid_hist = []
         used = []
@@ -495,11 +503,13 @@ class RankRSolver:
                 Xf = self._filter(X, coef, single=cheap)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._cholqr(Xa, X)
-                theta_n, Xn, Zn = self._rr(Xb, X, single=cheap)
-                res = K.ritz_residual(Xn, Zn, theta_n, self.r)  # (B,) per-matrix max residual
+                theta_n, Xn, Zn = self._rr(Xb, X, single=cheap, values_only=cheap)
+                # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
+                res = (K.ritz_residual(Xn, Zn, theta_n, self.r).double() if not cheap
+                       else torch.full((B,), math.inf, dtype=torch.float64, device=dev))
                 ovf = (self._ovf.max().double() if self.x3 and self._x3f
                        else torch.zeros((), dtype=torch.float64, device=dev))
-                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res.double()])
+                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res])
                 yield
                 chk = chk.cpu().numpy()
                 if self.x3 and self._x3f and chk[0] != 0:
@@ -527,6 +537,8 @@ class RankRSolver:
             used.append(d)
             if mr <= self.tol:
                 break
+        if Z is None:  # left the loop on a values-only iteration (MAX_OUTER): rotate once
+            theta, X, Z = self._rr(X)
         self.stats.history.append((cold, used, list(self.stats.resid_hist)))
         # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
         # one CholQR pass restores orthonormality without moving the converged subspace
