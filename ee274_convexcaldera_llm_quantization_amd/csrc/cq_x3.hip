@@ -44,6 +44,7 @@ struct X3K {
     float out_scale;
     int* overflow;
     int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
+    int noskip;  // A/B switch (CQ_X3_NOSKIP=1): dead waves run their MFMAs anyway
     int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
     const int* active;  // per batch (NULL = all): inactive entries skip the product, C = D
     int a_blocked;  // A halves K-blocked [K/32][lda rows][32] (lda = rows)
@@ -741,13 +742,14 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
     }
     // a wave whose 96 x 64 output block lies wholly past the matrix edge (ragged last tiles)
     // or, for a symmetric Gram (tri), wholly below the diagonal is never stored: it runs only
-    // its share of the loads and barriers, no fragment reads or MFMAs (power-bound kernel:
-    // fewer MFMA joules per launch; per-strip or per-block skips inside the K loop make the
-    // register allocator spill the accumulators)
+    // its share of the loads and barriers, no fragment reads or MFMAs (fewer MFMA joules;
+    // measured time-neutral — the workgroup still waits for its live waves at every barrier:
+    // Gram 6.16 vs 6.13 ms, filter 2.65 vs 2.65 ms at B = 128/32, CQ_X3_NOSKIP=1 A/B;
+    // per-strip or per-block skips inside the K loop make the allocator spill the accumulators)
     // (PERMB: a fragment's 16 columns interleave with stride 16 across the wave's 64; the
     // wave-level test below only needs the block's first row and column)
     const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
-    uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
+    uint32_t live = (a.noskip || (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0))) ? 1u : 0u;
     live = __builtin_amdgcn_readfirstlane(live);
     if (!live) {  // the wave's whole 96 x 64 block is dead: its share of the loads and barriers only
         for (int64_t t = 0; t < nt; ++t) {
@@ -1953,6 +1955,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.o_blocked = g->o_blocked;
     static const int probe = getenv("CQ_X3_CLOCK") ? 1 : 0;
     a.probe = probe;
+    static const int noskip = getenv("CQ_X3_NOSKIP") ? 1 : 0;
+    a.noskip = noskip;
     CQ_REQUIRE(!g->o_blocked || g->N % 32 == 0, "cq_gemm_x3: blocked split output needs N % 32 == 0");
     CQ_REQUIRE(!g->a_blocked || g->lda >= g->M, "cq_gemm_x3: blocked A needs lda = rows >= M");
     CQ_REQUIRE(!g->active || g->D, "cq_gemm_x3: active needs D (the pass-through value)");
