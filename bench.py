@@ -214,7 +214,9 @@ def main():
             "bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved_gbs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
             "achieved_tflops_f16": f16 / t / 1e12, "frac_mfma": (f16 / t / 1e12) / PEAK_F16_MFMA_TFLOPS,
             "frac_of_bound": max(t_hbm, t_mfma) / t, "launches_timed": g["count"], "avg_call_ms": g["avg_ms"],
-            "bytes_per_call": g["bytes_per_launch"], "kernel": "q_update_v_kernel<0|1, bits> (cq_q_update_x3)"}
+            "bytes_per_call": g["bytes_per_launch"],
+            "kernel": ("quant_w_stream_kernel (cq_q_update_x3, r = 0, max|W| known)" if kind == "w"
+                       else "q_update_v_kernel<0|1, bits> (cq_q_update_x3)")}
     if qroof:
         result["roofline_quantise"] = qroof
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
