@@ -45,11 +45,15 @@ def make_params():
 
 
 def synth_batch(B, seed0, dev):
-    ws = []
+    """B synthetic weights with the survey's recipe: per matrix
+    torch.manual_seed(seed); randn(4096, 4096) * 0.02 -> fp16 on the host generator (the
+    seed-0 matrix is the one the golden sketch pins).  Each matrix goes to `dev` as soon as it
+    is made, so host memory stays at one matrix per rank."""
+    out = torch.empty((B, M, N), dtype=torch.float16, device=dev)
     for i in range(B):
         torch.manual_seed(seed0 + i)
-        ws.append((torch.randn(M, N) * 0.02).to(torch.float16))
-    return torch.stack(ws).to(dev)
+        out[i].copy_((torch.randn(M, N) * 0.02).to(torch.float16))
+    return out
 
 
 def frob_vs_reference(dec_gpu, W_cpu, do_oracle):
