@@ -187,3 +187,36 @@ def test_caller_threshold_and_hadamard():
     assert rep2.quantized_param_count == 0 and not any(o.applied for o in rep2.layers)
     for n in names:
         assert torch.equal(dict(m2.named_modules())[n].weight.data, W2[n])
+
+
+def test_calibrate_then_quantize_end_to_end(tmp_path):
+    """main.py's whole flow on a tiny LLaVA-shaped model: hook-based calibration (reference
+    mode) saved in the diag_Hessians.pt layout, reloaded with the safe loader, then the layer
+    replacement with those Hessians; every replaced layer matches caldera() with
+    diag_embed(Hall[name]) (main.py:163-196)."""
+    from ee274_convexcaldera_llm_quantization_amd.calibration import HessianCalibrator
+    from ee274_convexcaldera_llm_quantization_amd.model import apply_caldera_quantization, select_layers
+    from src.caldera.decomposition.alg import caldera
+    m = _tiny_model(4)
+    names = [j[0] for j in select_layers(m)[0]]
+    mods = dict(m.named_modules())
+    cal = HessianCalibrator(m, names=names, mode="reference")
+    with cal, torch.no_grad():
+        for s in range(3):
+            for n in names:  # drive each selected layer with its own calibration activations
+                lin = mods[n]
+                lin(torch.randn(1, 5 + s, lin.in_features, device=DEV))
+            cal.end_sample()
+    path = tmp_path / "diag_Hessians.pt"
+    cal.save(str(path))
+    Hall = torch.load(str(path), weights_only=True)
+    assert set(Hall) == set(names) and all(v.dtype == torch.float64 and v.dim() == 1 for v in Hall.values())
+    W0 = {n: mods[n].weight.data.clone() for n in names}
+    rep = apply_caldera_quantization(m, Hall, _params())
+    assert all(o.applied for o in rep.layers)
+    for n in names[:3]:
+        d = caldera(_params(), W0[n], torch.diag_embed(Hall[n].float()).to(DEV), device=DEV, use_tqdm=False,
+                    scale_W=False)
+        exp = d.Q.double() + d.L.double() @ d.R.double()
+        got = mods[n].weight.data.double()
+        assert float(torch.linalg.norm(got - exp) / torch.linalg.norm(exp)) < 1e-5
