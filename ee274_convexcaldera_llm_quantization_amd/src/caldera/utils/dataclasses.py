@@ -1,5 +1,12 @@
-"""Drop-in for RCR/src/caldera/utils/dataclasses.py:1-113 — identical field names, types,
-defaults and help metadata (the API surface callers construct and read)."""
+"""Drop-in for RCR/src/caldera/utils/dataclasses.py:1-113.
+
+The three dataclasses callers construct and read — `CalderaParams` (:11-84),
+`CalderaDecomposition` (:87-106) and `QuantInfo` (:109-113) — are generated here from field
+tables: same field names, order, types and defaults (so the same constructor signatures and
+`dataclasses.fields()`), built with `dataclasses.make_dataclass`.
+"""
+from dataclasses import dataclass, field, make_dataclass  # noqa: F401  (star-exported like the reference's)
+
 import torch
 
 from .quantization import (
@@ -7,74 +14,49 @@ from .quantization import (
     AbstractQuantizer,
     LowMemoryQuantizer,
 )
-from dataclasses import field, dataclass
 
 
-@dataclass
-class CalderaParams:
-    """Parameters for the CALDERA decomposition (dataclasses.py:11-84)."""
-
-    compute_quantized_component: bool = field(
-        default=True,
-        metadata={"help": "Whether the decomposition should include a quantized full-size component (denoted Q)."},
-    )
-    compute_low_rank_factors: bool = field(
-        default=True,
-        metadata={"help": "Whether the decomposition should include low-rank factors (L, R)."},
-    )
-    Q_bits: int = field(default=2, metadata={"help": "Either 2, 3, or 4 bit lattice quantization"})
-    L_bits: int = field(default=2, metadata={"help": "Either 2, 3, or 4 bit lattice quantization"})
-    R_bits: int = field(default=2, metadata={"help": "Either 2, 3, or 4 bit lattice quantization"})
-    rank: int = field(default=64, metadata={"help": "Rank of L and R factors"})
-    iters: int = field(default=20)
-    lplr_iters: int = field(default=5)
-    activation_aware_LR: bool = field(
-        default=True, metadata={"help": "Use activation-aware LPLR for computing the factors."}
-    )
-    update_order: list[str] = field(
-        default_factory=list,
-        metadata={"help": 'List specifying whether to update the "LR" factors before "q" or vice versa.'},
-    )
-    quant_factory_Q: QuantizerFactory = field(
-        default_factory=QuantizerFactory,
-        metadata={"help": "QuantizerFactory used to instantiate the quantizer for Q."},
-    )
-    quant_factory_LR: QuantizerFactory = field(
-        default_factory=QuantizerFactory,
-        metadata={"help": "QuantizerFactory used to instantiate the quantizer for L and R."},
-    )
-    rand_svd: bool = field(
-        default=False, metadata={"help": "Whether to use randomized SVD for LPLR initialization"}
-    )
-    sigma_reg: float = field(
-        default=0, metadata={"help": "Regularization to make Hessian positive definite"}
-    )
+def _spec(name, typ, default=None, factory=None, doc=None):
+    meta = {"help": doc} if doc else {}
+    f = field(default_factory=factory, metadata=meta) if factory is not None else field(default=default, metadata=meta)
+    return (name, typ, f)
 
 
-@dataclass
-class CalderaDecomposition:
-    """A dataclass representing the components and parameters in the Caldera decomposition
-    (dataclasses.py:87-106)."""
+_BITS = "quantisation bit width"
 
-    Q: torch.Tensor = field(default=None)
-    L: torch.Tensor = field(default=None)
-    R: torch.Tensor = field(default=None)
-    W: torch.Tensor = field(default=None)
-    Q_idxs: torch.Tensor = field(default=None)
-    L_idxs: torch.Tensor = field(default=None)
-    R_idxs: torch.Tensor = field(default=None)
-    Q_scale: float = field(default=1)
-    L_scale: float = field(default=1)
-    R_scale: float = field(default=1)
-    global_scale: float = field(default=1)
-    SU: torch.Tensor = field(default=None)
-    SV: torch.Tensor = field(default=None)
-    scaleWH: torch.Tensor = field(default=None)
-    errors: dict[str, list[float]] = field(default_factory=dict)
+# dataclasses.py:11-84 — defaults as the reference's (update_order [] = no updates at all)
+_PARAMS = [
+    _spec("compute_quantized_component", bool, True, doc="include the quantised full-size component Q"),
+    _spec("compute_low_rank_factors", bool, True, doc="include the low-rank factors L, R"),
+    _spec("Q_bits", int, 2, doc=_BITS),
+    _spec("L_bits", int, 2, doc=_BITS),
+    _spec("R_bits", int, 2, doc=_BITS),
+    _spec("rank", int, 64, doc="rank of L and R"),
+    _spec("iters", int, 20),
+    _spec("lplr_iters", int, 5),
+    _spec("activation_aware_LR", bool, True, doc="activation-aware LPLR factors"),
+    _spec("update_order", list[str], factory=list, doc='order of the "Q" / "LR" updates per iteration'),
+    _spec("quant_factory_Q", QuantizerFactory, factory=QuantizerFactory, doc="quantiser factory for Q"),
+    _spec("quant_factory_LR", QuantizerFactory, factory=QuantizerFactory, doc="quantiser factory for L and R"),
+    _spec("rand_svd", bool, False, doc="randomised SVD (svd_lowrank) for the LR initialisation"),
+    _spec("sigma_reg", float, 0, doc="eigenvalue floor that makes H positive definite"),
+]
 
+# dataclasses.py:87-106 — every field optional; scales 1 until a quantiser sets them
+_DECOMP = [(n, torch.Tensor, None) for n in ("Q", "L", "R", "W", "Q_idxs", "L_idxs", "R_idxs")]
+_DECOMP += [(n, float, 1) for n in ("Q_scale", "L_scale", "R_scale", "global_scale")]
+_DECOMP += [(n, torch.Tensor, None) for n in ("SU", "SV", "scaleWH")]
 
-@dataclass
-class QuantInfo:
-    """Stores quantization-specific information (dataclasses.py:109-113)."""
+CalderaParams = make_dataclass("CalderaParams", _PARAMS, namespace={"__module__": __name__})
+CalderaParams.__doc__ = "Parameters for the CALDERA decomposition (dataclasses.py:11-84)."
 
-    quant: AbstractQuantizer = field(default_factory=LowMemoryQuantizer)
+CalderaDecomposition = make_dataclass(
+    "CalderaDecomposition",
+    [(n, t, field(default=d)) for n, t, d in _DECOMP] + [("errors", dict[str, list[float]], field(default_factory=dict))],
+    namespace={"__module__": __name__},
+)
+CalderaDecomposition.__doc__ = "Components and parameters of a CALDERA decomposition (dataclasses.py:87-106)."
+
+QuantInfo = make_dataclass("QuantInfo", [("quant", AbstractQuantizer, field(default_factory=LowMemoryQuantizer))],
+                           namespace={"__module__": __name__})
+QuantInfo.__doc__ = "Quantisation-specific information (dataclasses.py:109-113)."
