@@ -61,6 +61,11 @@ class EngineParams:
                    rand_svd=qp.rand_svd, sigma_reg=qp.sigma_reg)
 
 
+# below this relative error the Pythagorean LR error (||Y||^2 - ||R||_h^2, fp32-grade R) has
+# lost more than ~1e-5 absolute accuracy to cancellation; such errors are recomputed directly
+PYTH_MIN_ERR = 3e-2
+
+
 def _uniform_k(bits):
     return 2 ** (bits - 1) - 1
 
@@ -439,6 +444,7 @@ class CalderaEngine:
             # sum_j h_j (res - L R)_ij^2 = ||Y||^2 - ||U^T Y||^2 = ||Y||^2 - sum_j h_j R_ij^2
             # (two fp64 reductions instead of an m x n x r product; U orthonormal to ~1e-7)
             ysq = K.weighted_sqsum(Ysrc, None, n) if ysq is None else ysq
+            self._pyth = True  # run_iter recomputes small errors directly (cancellation)
             return ysq - K.weighted_sqsum(R, wts.err if wts.ycol is not None else None, n)
         err = torch.empty(B, dtype=torch.float64, device=dev)
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
@@ -631,6 +637,7 @@ class CalderaEngine:
         for _ in to_iter:
             for mtx in p.update_order:
                 num = None
+                self._pyth = False
                 if mtx == "LR" and p.compute_low_rank_factors:
                     num = yield from self._lr_update(st, Ws, work, res, wts, den)
                 elif mtx == "Q" and p.compute_quantized_component:
@@ -643,6 +650,14 @@ class CalderaEngine:
                 e = torch.sqrt((num.float() / den.float()))  # fp32 ratio + sqrt (alg.py:297-301)
                 yield
                 e = e.tolist()
+                if self._pyth and min(e) < PYTH_MIN_ERR:
+                    # ||Y||^2 - ||U^T Y||^2 cancels when L R reproduces Y almost exactly (rank at
+                    # or above the residual's effective rank): those errors are recomputed from
+                    # the residual itself
+                    e2 = torch.sqrt(self._state_error(st, Ws, work, wts).float() / den.float())
+                    yield
+                    e2 = e2.tolist()
+                    e = [e2[b] if e[b] < PYTH_MIN_ERR else e[b] for b in range(B)]
                 for b in range(B):
                     errors[mtx][b].append(float(e[b]))
                 if all(updated.values()):

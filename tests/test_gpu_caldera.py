@@ -238,3 +238,19 @@ def test_ragged_shapes_vs_oracle(api, m, n, r, qb, lrb, dtype):
     else:  # quantised factors: chaotic code flips, compared loosely
         np.testing.assert_allclose(d.errors["LR"], ref.errors["LR"], rtol=0, atol=2e-2)
     assert d.Q.shape == (m, n) and d.L.shape == (m, r) and d.R.shape == (r, n)
+
+
+@pytest.mark.parametrize("m,n", [(64, 48), (48, 64)])
+def test_rank_above_min_dim(api, m, n):
+    """rank > min(m, n): the reference's SVD keeps min(m, n) columns (alg.py:217-225), so L
+    is m x k and R k x n with k = min(m, n), and Q + L R reproduces the residual exactly."""
+    caldera, CP, _ = api
+    g = torch.Generator().manual_seed(3)
+    W = (torch.randn(m, n, generator=g) * 0.02).half()
+    kw = dict(Q_bits=4, L_bits=16, R_bits=16, rank=64, iters=2, update_order=["Q", "LR"], sigma_reg=1e-8)
+    d = caldera(CP(**kw), W.to(DEV), None, device=DEV, use_tqdm=False)
+    ref = O.caldera(O.Params(**kw), W.numpy())
+    k = min(m, n)
+    assert tuple(d.L.shape) == ref.L.shape == (m, k) and tuple(d.R.shape) == ref.R.shape == (k, n)
+    assert abs(d.errors["Q"][0] - ref.errors["Q"][0]) < 1e-6
+    assert max(d.errors["LR"]) < 1e-5
