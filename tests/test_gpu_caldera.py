@@ -254,3 +254,33 @@ def test_rank_above_min_dim(api, m, n):
     assert tuple(d.L.shape) == ref.L.shape == (m, k) and tuple(d.R.shape) == ref.R.shape == (k, n)
     assert abs(d.errors["Q"][0] - ref.errors["Q"][0]) < 1e-6
     assert max(d.errors["LR"]) < 1e-5
+
+
+@pytest.mark.parametrize("order,aware,cq,clr", [
+    (["Q"], True, True, True),          # Q only: LR never set (zeros)
+    (["LR"], True, True, True),         # LR only: Q never set
+    (["LR", "Q"], True, True, True),    # LR first
+    (["Q", "LR"], False, True, True),   # not activation-aware: L = U sqrt(S), R = sqrt(S) Vh
+    (["Q", "LR"], True, False, True),   # compute_quantized_component=False
+    (["Q", "LR"], True, True, False),   # compute_low_rank_factors=False
+])
+def test_update_orders_and_flags_vs_oracle(api, order, aware, cq, clr):
+    """alg.py:92-107's loop over update_order with the compute_* switches and both LR
+    branches (alg.py:201-235), diag H, against the oracle."""
+    caldera, CP, _ = api
+    g = torch.Generator().manual_seed(21)
+    W = (torch.randn(256, 384, generator=g) * 0.02).half()
+    h = torch.rand(384, generator=g) + 0.1
+    kw = dict(Q_bits=2, L_bits=16, R_bits=16, rank=32, iters=3, update_order=order, sigma_reg=1e-8,
+              activation_aware_LR=aware, compute_quantized_component=cq, compute_low_rank_factors=clr)
+    d = caldera(CP(**kw), W.to(DEV), torch.diag_embed(h).to(DEV), device=DEV, use_tqdm=False)
+    ref = O.caldera(O.Params(**kw), W.numpy(), np.diag(h.numpy()))
+    assert set(d.errors) == set(ref.errors)
+    for k in ref.errors:
+        if ref.errors[k]:
+            assert abs(d.errors[k][0] - ref.errors[k][0]) < 1e-5
+        np.testing.assert_allclose(d.errors[k], ref.errors[k], rtol=0, atol=2e-3)
+    out = (d.Q.double() + d.L.double() @ d.R.double()).cpu().numpy()
+    exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
+    den = max(np.linalg.norm(exp), 1e-30)
+    assert np.linalg.norm(out - exp) / den < 1e-4
