@@ -318,13 +318,20 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
             }
         }
     __syncthreads();
+    // Threshold Jacobi: a pair whose |a_ij| is below thr * sqrt|a_ii a_jj| is not rotated.  With
+    // thr = tol / (2 sqrt p), a matrix whose pairs are all below it already has
+    // off^2 <= thr^2 (sum |a_ii|)^2 <= thr^2 p sum a_ii^2 = tol^2 dg / 4, i.e. passes the stop
+    // test, so skipping cannot stall convergence.  Near-diagonal (warm Rayleigh-Ritz) matrices
+    // then skip most of the scattered 2x2 block updates of A and most V row updates.
+    const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
         for (int i = wid; i < p; i += kSmallWaves)
             for (int c = lane; c < p; c += 64) {
+                if (c < i) continue;  // sweeps keep the upper triangle only
                 const double v = A[i * p + c];
-                if (i == c) dg += v * v; else off += v * v;
+                if (i == c) dg += v * v; else off += 2.0 * v * v;
             }
         const double offs = block_sum_f64(off, red);
         const double dgs = block_sum_f64(dg, red);
@@ -341,7 +348,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
                 if (j < p) {
                     const double aij = A[i * p + j];
                     const double aii = A[i * p + i], ajj = A[j * p + j];
-                    if (fabs(aij) > 1e-300 && fabs(aij) > 1e-17 * sqrt(fabs(aii * ajj))) {
+                    if (fabs(aij) > 1e-300 && fabs(aij) > thr * sqrt(fabs(aii * ajj))) {
                         const double th = (ajj - aii) / (2.0 * aij);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
                         c = 1.0 / sqrt(1.0 + t * t);
@@ -365,28 +372,32 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
                     if (sa == 0.0 && sb == 0.0) continue;
                     const int ia = pi[qa], ja = pj[qa];
                     const bool va = ja < p;
-                    const double x00 = A[ia * p + ib];
-                    const double x01 = vb ? A[ia * p + jb] : 0.0;
-                    const double x10 = va ? A[ja * p + ib] : 0.0;
-                    const double x11 = (va && vb) ? A[ja * p + jb] : 0.0;
+                    // upper-triangle element (r, c) of the symmetric A: half the stores
+                    const int u00 = ia < ib ? ia * p + ib : ib * p + ia;
+                    const int u01 = ia < jb ? ia * p + jb : jb * p + ia;
+                    const int u10 = ja < ib ? ja * p + ib : ib * p + ja;
+                    const int u11 = ja < jb ? ja * p + jb : jb * p + ja;
+                    const double x00 = A[u00];
+                    const double x01 = vb ? A[u01] : 0.0;
+                    const double x10 = va ? A[u10] : 0.0;
+                    const double x11 = (va && vb) ? A[u11] : 0.0;
                     const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
                     const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                    double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
-                    double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
-                    if (qa == qb) {
-                        z01 = 0.0; z10 = 0.0;
-                        A[ia * p + ib] = z00;
-                        if (va && vb) A[ja * p + jb] = z11;
-                        if (vb) A[ia * p + jb] = 0.0;
-                        if (va) A[ja * p + ib] = 0.0;
+                    const double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
+                    const double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
+                    if (qa == qb) {  // diagonal block: (ia, ja) is the annihilated pair
+                        A[u00] = z00;
+                        if (va && vb) A[u11] = z11;
+                        if (vb) A[u01] = 0.0;
                     } else {
-                        A[ia * p + ib] = z00; A[ib * p + ia] = z00;
-                        if (vb) { A[ia * p + jb] = z01; A[jb * p + ia] = z01; }
-                        if (va) { A[ja * p + ib] = z10; A[ib * p + ja] = z10; }
-                        if (va && vb) { A[ja * p + jb] = z11; A[jb * p + ja] = z11; }
+                        A[u00] = z00;
+                        if (vb) A[u01] = z01;
+                        if (va) A[u10] = z10;
+                        if (va && vb) A[u11] = z11;
                     }
                 }
             }
+
             // ---- Vt rows i, j of each active pair (coalesced along the row)
             for (int q = wid; q < H; q += kSmallWaves) {
                 const double s = sn[q];

@@ -255,6 +255,33 @@ def test_jacobi_fp32_lds_path_p256(K):
     assert off.abs().max().item() < 1e-5 * nrm.max().item()
 
 
+@pytest.mark.parametrize("near_diag", [False, True])
+def test_jacobi_global_path_p384(K, near_diag):
+    """p = 384 (rank-256 Rayleigh-Ritz, config 5) runs the global-memory threshold Jacobi:
+    pairs below tol / (2 sqrt p) of sqrt|a_ii a_jj| are skipped, which must not stop the
+    off-norm test from passing (cold and warm / near-diagonal matrices)."""
+    torch.manual_seed(10)
+    p = 384
+    X = torch.randn(1, 2048, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    if near_diag:  # a warm Rayleigh-Ritz matrix: eigenbasis of S perturbed by 1e-4
+        _, U = torch.linalg.eigh(S)
+        Qp, _ = torch.linalg.qr(U + 1e-4 * torch.randn_like(U))
+        S = Qp.transpose(1, 2) @ S @ Qp
+        S = 0.5 * (S + S.transpose(1, 2))
+    ref = torch.linalg.eigvalsh(S).flip(-1)
+    nrm = ref[:, 0:1]
+    for tol in (1e-7, 1e-13):
+        ev, V32, V64, sw = K.jacobi_eigh(S.clone().to(DEV), tol=tol, want64=True)
+        assert int(sw.max()) < 30
+        assert ((ev.cpu() - ref).abs() / nrm).max().item() < max(tol * tol * 1e4, 1e-12)
+        V = V64.cpu()
+        assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 1e-10
+        D = V.transpose(1, 2) @ S @ V
+        off = D - torch.diag_embed(torch.diagonal(D, dim1=1, dim2=2))
+        assert off.norm().item() <= 2 * tol * D.norm().item() + 1e-12 * nrm.max().item()
+
+
 @pytest.mark.parametrize("p", [64, 128, 180, 192])
 def test_jacobi_register_path_accuracy(K, p):
     """p <= 192: fp64 A in LDS + fp32 V in registers (the solver's Rayleigh-Ritz path):
