@@ -928,8 +928,8 @@ static size_t jacobi_reg_bytes(int p) {
 // then the trailing upper triangle receives one rank-32 Schur update
 //   S[i][c] -= sum_k U[k][i] U[k][c] / d_k ,   E[i][:] = -sum_k (U[k][i]/d_k) E[k][:]
 // (U = panel rows after in-panel elimination), E = L^{-1}; finally Wt = E^T D^{-1/2}.
-constexpr int WNB = 32;
-
+// NB = 32, or 16 when a 32-row panel pair does not fit the 160 KB of LDS (p up to 620).
+template <int WNB>
 __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
     double* __restrict__ S_all, int p, double rc2, double* __restrict__ E_all, float* __restrict__ W32,
     int* __restrict__ info) {
@@ -1017,8 +1017,8 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
         }
 }
 
-static size_t whiten_lds_bytes(int p) {
-    return (size_t)(2 * WNB * p + p + WNB) * sizeof(double) + 16;
+static size_t whiten_lds_bytes(int p, int nb) {
+    return (size_t)(2 * nb * p + p + nb) * sizeof(double) + 16;
 }
 
 // ------------------------------------------------------------------ Ritz residuals
@@ -1113,9 +1113,11 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
     CQ_REQUIRE(rcond2 >= 0.0, "cq_spd_whiten: rcond2 must be >= 0");
     hipStream_t s = as_stream(stream);
     // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
-    const size_t wl = whiten_lds_bytes((int)p);
-    if (wl <= 160 * 1024)
-        spd_whiten_blocked_kernel<<<(unsigned)batch, kSmallThreads, wl, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    const size_t wl32 = whiten_lds_bytes((int)p, 32), wl16 = whiten_lds_bytes((int)p, 16);
+    if (wl32 <= 160 * 1024)
+        spd_whiten_blocked_kernel<32><<<(unsigned)batch, kSmallThreads, wl32, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    else if (wl16 <= 160 * 1024)
+        spd_whiten_blocked_kernel<16><<<(unsigned)batch, kSmallThreads, wl16, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     else
         spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     if (hipMemcpyAsync(Wt64, S, (size_t)batch * p * p * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)

@@ -299,9 +299,9 @@ def test_jacobi_register_path_accuracy(K, p):
     assert torch.equal(V32.cpu().double(), V)
 
 
-def test_whiten_blocked_p256(K):
+@pytest.mark.parametrize("p", [256, 384])  # panel 32 / panel 16
+def test_whiten_blocked(K, p):
     torch.manual_seed(10)
-    p = 256
     X = torch.randn(2, 2048, p, dtype=torch.float64) * torch.logspace(0, 3, p, dtype=torch.float64)
     S = X.transpose(1, 2) @ X
     Wt32, Wt64, info = K.spd_whiten(S.clone().to(DEV))
@@ -610,7 +610,7 @@ def test_residual_split_matches_unfused(K, bits, weighted):
     assert torch.allclose(sq, (Ysrc.double() ** 2).sum((1, 2)), rtol=1e-12, atol=0)
 
 
-@pytest.mark.parametrize("p", [24, 200, 300])  # blocked (LDS) and unblocked kernels
+@pytest.mark.parametrize("p", [24, 200, 300, 384, 700])  # blocked nb 32 / nb 16, unblocked
 def test_spd_whiten_rank_deficient_is_gelsy_basic_solution(K, p):
     """lstsq through the normal equations with dependent columns (alg.py:162-177 with a
     rank-deficient factor, e.g. a 2-bit L with an all-zero column): the dropped pivots give a
