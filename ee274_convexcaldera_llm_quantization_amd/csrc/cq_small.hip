@@ -308,9 +308,10 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
     double* A = A_all + b * (int64_t)p * p;
     double* Vt = Vt_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool want_v = V32 || V64;  // values only: no eigenvector rotations
     for (int i = wid; i < p; i += kSmallWaves)
         for (int c = lane; c < p; c += 64) {
-            Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
+            if (want_v) Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
             if (i < c) {  // symmetrise (Rayleigh-Ritz matrices carry rounding asymmetry)
                 const double s = 0.5 * (A[i * p + c] + A[c * p + i]);
                 A[i * p + c] = s;
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
             }
 
             // ---- Vt rows i, j of each active pair (coalesced along the row)
-            for (int q = wid; q < H; q += kSmallWaves) {
+            for (int q = wid; want_v && q < H; q += kSmallWaves) {
                 const double s = sn[q];
                 if (s == 0.0) continue;
                 const double c = cs[q];
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
         pi[i] = rank;
     }
     __syncthreads();
-    for (int i = wid; i < p; i += kSmallWaves) {
+    for (int i = wid; want_v && i < p; i += kSmallWaves) {
         const int rk = pi[i];
         for (int x = lane; x < p; x += 64) {  // component x of eigenvector i -> V[x][rk]
             const double v = Vt[i * p + x];

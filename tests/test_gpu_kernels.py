@@ -280,6 +280,9 @@ def test_jacobi_global_path_p384(K, near_diag):
         D = V.transpose(1, 2) @ S @ V
         off = D - torch.diag_embed(torch.diagonal(D, dim1=1, dim2=2))
         assert off.norm().item() <= 2 * tol * D.norm().item() + 1e-12 * nrm.max().item()
+        # values only: the same rotations of A without the eigenvector updates
+        ev2, V2, _, _ = K.jacobi_eigh(S.clone().to(DEV), tol=tol, want_vectors=False)
+        assert V2 is None and torch.equal(ev2.cpu(), ev.cpu())
 
 
 @pytest.mark.parametrize("p", [64, 128, 180, 192])
