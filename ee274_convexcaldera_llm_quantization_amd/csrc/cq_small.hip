@@ -361,40 +361,61 @@ __global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restric
             }
             __syncthreads();
             if (nact == 0) continue;
-            // ---- A <- J^T A J on 2x2 pair blocks (qa <= qb); wave strips over qb, balanced
-            for (int w = wid; w < H; w += kSmallWaves) {
-                // pair strips qb = w and qb = H-1-w alternate so every wave gets ~H/2 blocks
-                const int qb = (w & 1) ? (H - 1 - (w >> 1)) : (w >> 1);
-                const double cb = cs[qb], sb = sn[qb];
-                const int ib = pi[qb], jb = pj[qb];
-                const bool vb = jb < p;
-                for (int qa = lane; qa <= qb; qa += 64) {
-                    const double ca = cs[qa], sa = sn[qa];
-                    if (sa == 0.0 && sb == 0.0) continue;
-                    const int ia = pi[qa], ja = pj[qa];
-                    const bool va = ja < p;
-                    // upper-triangle element (r, c) of the symmetric A: half the stores
-                    const int u00 = ia < ib ? ia * p + ib : ib * p + ia;
-                    const int u01 = ia < jb ? ia * p + jb : jb * p + ia;
-                    const int u10 = ja < ib ? ja * p + ib : ib * p + ja;
-                    const int u11 = ja < jb ? ja * p + jb : jb * p + ja;
-                    const double x00 = A[u00];
-                    const double x01 = vb ? A[u01] : 0.0;
-                    const double x10 = va ? A[u10] : 0.0;
-                    const double x11 = (va && vb) ? A[u11] : 0.0;
-                    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                    const double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
-                    const double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
-                    if (qa == qb) {  // diagonal block: (ia, ja) is the annihilated pair
-                        A[u00] = z00;
-                        if (va && vb) A[u11] = z11;
-                        if (vb) A[u01] = 0.0;
-                    } else {
-                        A[u00] = z00;
-                        if (vb) A[u01] = z01;
-                        if (va) A[u10] = z10;
-                        if (va && vb) A[u11] = z11;
+            // ---- A <- J^T A J on 2x2 pair blocks (qa <= qb), upper triangle only.  The
+            // H(H+1)/2 blocks of a round are disjoint, so each thread takes JU blocks of the
+            // linear triangle enumeration and issues all their loads before any store (the
+            // scattered L2 round trips overlap instead of serialising block by block).
+            {
+                constexpr int JU = 4;
+                const int T = H * (H + 1) / 2;
+                for (int t0 = tid; t0 < T; t0 += JU * kSmallThreads) {
+                    int ua[JU][4];
+                    double xv[JU][4], cc[JU][2], ss[JU][2];
+                    bool act[JU], va[JU], vb[JU], dgb[JU];
+#pragma unroll
+                    for (int k = 0; k < JU; ++k) {
+                        const int t = t0 + k * kSmallThreads;
+                        act[k] = false;
+                        if (t >= T) continue;
+                        int qb = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+                        while ((qb + 1) * (qb + 2) / 2 <= t) ++qb;
+                        while (qb * (qb + 1) / 2 > t) --qb;
+                        const int qa = t - qb * (qb + 1) / 2;
+                        const double sa = sn[qa], sb = sn[qb];
+                        if (sa == 0.0 && sb == 0.0) continue;
+                        act[k] = true;
+                        dgb[k] = qa == qb;
+                        cc[k][0] = cs[qa]; ss[k][0] = sa; cc[k][1] = cs[qb]; ss[k][1] = sb;
+                        const int ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
+                        va[k] = ja < p; vb[k] = jb < p;
+                        ua[k][0] = ia < ib ? ia * p + ib : ib * p + ia;
+                        ua[k][1] = ia < jb ? ia * p + jb : jb * p + ia;
+                        ua[k][2] = ja < ib ? ja * p + ib : ib * p + ja;
+                        ua[k][3] = ja < jb ? ja * p + jb : jb * p + ja;
+                        xv[k][0] = A[ua[k][0]];
+                        xv[k][1] = vb[k] ? A[ua[k][1]] : 0.0;
+                        xv[k][2] = va[k] ? A[ua[k][2]] : 0.0;
+                        xv[k][3] = (va[k] && vb[k]) ? A[ua[k][3]] : 0.0;
+                    }
+#pragma unroll
+                    for (int k = 0; k < JU; ++k) {
+                        if (!act[k]) continue;
+                        const double ca = cc[k][0], sa = ss[k][0], cb = cc[k][1], sb = ss[k][1];
+                        const double x00 = xv[k][0], x01 = xv[k][1], x10 = xv[k][2], x11 = xv[k][3];
+                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                        const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                        const double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
+                        const double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
+                        if (dgb[k]) {  // diagonal block: (ia, ja) is the annihilated pair
+                            A[ua[k][0]] = z00;
+                            if (va[k] && vb[k]) A[ua[k][3]] = z11;
+                            if (vb[k]) A[ua[k][1]] = 0.0;
+                        } else {
+                            A[ua[k][0]] = z00;
+                            if (vb[k]) A[ua[k][1]] = z01;
+                            if (va[k]) A[ua[k][2]] = z10;
+                            if (va[k] && vb[k]) A[ua[k][3]] = z11;
+                        }
                     }
                 }
             }
