@@ -136,6 +136,11 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                            f"g.build()'` (hipcc --offload-arch=gfx950)")
+    if path == LIB_PATH and not os.environ.get("CQ_ALLOW_STALE_LIB"):
+        from . import build as _build
+        if _build.needs_build():  # never run kernels older than the sources in the tree
+            raise RuntimeError(f"{path} is stale (built from other sources than csrc/ now holds, or "
+                               f"unstamped): rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

@@ -2,6 +2,7 @@
 .so travels with the repo snapshot to the GPU box)."""
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -23,13 +24,36 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+STAMP = OUT + ".srchash"  # content hash of the sources the .so was built from
+
+
+def _deps():
+    return ([os.path.join(CSRC, s) for s in SOURCES + ["cq_common.h"]]
+            + [os.path.join(HERE, "..", "include", "caldera_hip.h")])
+
+
+def source_hash() -> str:
+    """SHA-256 over the kernel sources, the public header and the compile flags."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for d in _deps():
+        if os.path.exists(d):
+            with open(d, "rb") as f:
+                h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def built_hash() -> str | None:
+    try:
+        with open(STAMP) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def needs_build() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + ["cq_common.h"]]
-    deps.append(os.path.join(HERE, "..", "include", "caldera_hip.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    """Content-based (mtimes do not survive every copy): the .so is current iff the hash
+    stamped next to it at build time equals the hash of the sources now in the tree."""
+    return not os.path.exists(OUT) or built_hash() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -50,9 +74,12 @@ def build(force: bool = False, verbose: bool = True) -> str:
     failed = [src for p, src in procs if p.wait() != 0]
     if failed:
         raise RuntimeError(f"hipcc failed on {failed}")
+    digest = source_hash()
     tmp = OUT + ".tmp"
     subprocess.run([hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, OUT)
+    with open(STAMP, "w") as f:
+        f.write(digest + "\n")
     return OUT
 
 

@@ -469,6 +469,40 @@ class CalderaEngine:
         Wt32, _, info = K.spd_whiten(M64, rcond2=rc * rc)
         return Wt32, info
 
+    def lplr_L_step(self, R, Ysrc, wts: _Weights, L, tmp_mr=None):
+        """L step of the LPLR loop (alg.py:162-169), before quantisation:
+        L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T = (Y Rw^T)(Rw Rw^T)^{-1} with Rw = R H_sqrt
+        (data-aware; Ysrc = Y = res H_sqrt) or Rw = R, Ysrc = res (alg.py:167).  Normal
+        equations: fp64 Gram of Rw, rank-revealing SPD whitening at gelsy's rcond, fp32 GEMMs.
+        R (B, r, n), Ysrc (B, m, n), L (B, m, r) output."""
+        n = R.shape[-1]
+        if self.p.activation_aware_LR and wts.dense:
+            Rw = K.gemm(R, wts.Vs, C=torch.empty_like(R))  # R H_sqrt V
+        else:
+            Rw = K.scale_rc(R, colscale=wts.ycol) if (self.p.activation_aware_LR and wts.ycol is not None) else R
+        if tmp_mr is None:
+            tmp_mr = torch.empty_like(L)
+        Bm = K.gemm(Ysrc, Rw, tb=True, C=tmp_mr)            # m x r
+        Mr = K.gram_f64(Rw, Rw, ta=True, tb=True)          # r x r
+        Wr, _ = self._solve_normal(Mr, n)  # A = (R H_sqrt)^T: n x r
+        T1 = K.gemm(Bm, Wr, C=torch.empty_like(tmp_mr))     # (Y Rw^T) Wr
+        K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
+        return L
+
+    def lplr_R_step(self, L, res, R, tmp_rn=None):
+        """R step of the LPLR loop (alg.py:175-177), before quantisation:
+        R = lstsq(L, res) = (L^T L)^{-1} L^T res (unweighted, as the reference).
+        L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output."""
+        m = L.shape[1]
+        if tmp_rn is None:
+            tmp_rn = torch.empty_like(R)
+        Ml = K.gram_f64(L, L)                              # r x r
+        Wl, _ = self._solve_normal(Ml, m)  # A = L: m x r
+        Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
+        T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
+        K.gemm(Wl, T2, C=R)
+        return R
+
     def _lplr(self, st, Y, res, L0, R0, wts: _Weights):
         """Quantised-factor LPLR loop, alg.py:144-195 (data-aware lstsq in normal-equation form
         with fp64 Grams; quantise L^T and R as whole matrices, alg.py:171-180)."""
@@ -493,16 +527,8 @@ class CalderaEngine:
         Rn = torch.empty((B, r, n), dtype=torch.float32, device=dev)
         err = torch.empty(B, dtype=torch.float64, device=dev)
         for _ in range(p.lplr_iters):
-            # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T = (Y Rw^T)(Rw Rw^T)^{-1}   (alg.py:162-169)
-            if aware and wts.dense:
-                Rw = K.gemm(R, wts.Vs, C=torch.empty_like(R))  # R H_sqrt V
-            else:
-                Rw = K.scale_rc(R, colscale=wts.ycol) if (aware and wts.ycol is not None) else R
-            Bm = K.gemm(Ysrc, Rw, tb=True, C=tmp_mr)            # m x r
-            Mr = K.gram_f64(Rw, Rw, ta=True, tb=True)          # r x r
-            Wr, info = self._solve_normal(Mr, n)  # A = (R H_sqrt)^T: n x r
-            T1 = K.gemm(Bm, Wr, C=torch.empty_like(tmp_mr))     # (Y Rw^T) Wr
-            K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
+            # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T   (alg.py:162-169)
+            self.lplr_L_step(R, Ysrc, wts, L, tmp_mr)
             # --- quantise L^T as one block (alg.py:171-172)
             if cb:
                 Lt = K.transpose_split(L, out=torch.empty((B, r, m), dtype=torch.float32, device=dev))[0]
@@ -513,11 +539,7 @@ class CalderaEngine:
                 qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
                 L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
-            Ml = K.gram_f64(L, L)                              # r x r
-            Wl, info2 = self._solve_normal(Ml, m)  # A = L: m x r
-            Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
-            T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
-            K.gemm(Wl, T2, C=Rn)
+            self.lplr_R_step(L, res, Rn, tmp_rn)
             if cb:
                 itemsR, deqR = self._quantize_whole(Rn.view(B, r * n), p.method_LR, p.R_bits)
                 R = deqR.view(B, r, n)

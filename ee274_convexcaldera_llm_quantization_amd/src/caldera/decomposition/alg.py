@@ -29,7 +29,8 @@ def caldera(
 
     Computation always runs on the HIP device (device="cuda" on ROCm torch is the MI355X);
     output placement follows the reference: Q on W's device, L/R on `device`, W (scaled)
-    on the CPU.  H must be None or diagonal (what every reference caller passes)."""
+    on the CPU.  H may be None, diagonal (diag_embed(h), what main.py:163-165 passes: fused
+    column weights) or dense (one device eigendecomposition, then GEMM transforms)."""
     return _api.caldera_batch(quant_params, [W], H, device=device, use_tqdm=use_tqdm,
                               scale_W=scale_W, decomposition_cls=CalderaDecomposition)[0]
 

@@ -149,9 +149,12 @@ int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const fl
 
 /* ---------------------------------------------------------------------------------
  * Batched FP32 GEMM on gfx950 MFMA (v_mfma_f32_32x32x2_f32; exact f32 products).
- * Carries every dense product of the hot path: Gram Y Y^T, the filtered subspace
- * iteration G X, Ritz rotations X V, R = U^T Y, and the LPLR normal-equation products of
- * alg.py:162-182.  op(A) is M x K, op(B) is K x N.
+ * Carries the fp32 products of the hot path: Ritz rotations X V, the fp32 solver filter
+ * (fallback after an fp16 overflow, and k % 32 != 0 shapes), R = U^T Y / L = Y V where the
+ * split-fp16 path does not apply, the LPLR normal-equation products of alg.py:162-182, the
+ * fused residual (alg.py:262) and error (alg.py:182, :286-302) epilogues.  The Gram Y Y^T,
+ * the filter's G X and the Rayleigh-Ritz products run on cq_gemm_x3 (split-fp16 MFMA).
+ * op(A) is M x K, op(B) is K x N.
  *   epi = CQ_EPI_LINEAR:  C = alpha*op(A)op(B) + beta*C + gamma*D
  *   epi = CQ_EPI_RESID :  C = D - op(A)op(B) (D fp32, or fp16 if d_f16);
  *                          atomicMax(absmax_bits[b], |C|)     (alg.py:262 fused with :262 of quantization.py)

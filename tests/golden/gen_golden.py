@@ -14,10 +14,14 @@ Fixtures:
   e2e_nb.npz      notebook recipe RCR/caldera_playbook.ipynb cells 3-5 (summaries).
   trace_s.npz     teacher-forcing trace: every quantize_matrix / LR_init / update_LR /
                   activation_aware_error call of a small diag-H run, in call order.
+  lplr_mid.npz    teacher-forcing fixture of the quantised-factor LPLR loop (768x1280,
+                  r=64, L/R 4-bit, 10 lplr iterations, real-Hessian diag H): LR_init (L, R),
+                  per-iteration pre-quantisation inputs (sketches; full at iteration 0),
+                  codes, scales, near-tie indices and LPLR errors.
   sum_large.npz   configs 2, 3, 5 at full size: hashes, scalars, error lists and
                   float64 sketches (Q+LR)@Omega and (L1 R1)@Omega of the first LR step.
 
-Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [large]
+Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [lplr] [large]
 """
 import hashlib
 import json
@@ -248,6 +252,68 @@ def gen_trace(alg, q, CalderaParams):
 
 
 # ---------------------------------------------------------------------------
+def near_ties(A, bits, tol=1e-4):
+    """Flat indices of A whose scaled value x / max|A| * k (quantization.py:95, 266) lies
+    within `tol` code units of a rounding boundary: the only places where a code may flip
+    between two lstsq solutions that agree to ~1e-6 relative."""
+    a = A.detach().double().numpy().reshape(-1)
+    mx = max(np.abs(a).max(), 1e-8)
+    s = a / mx * (2 ** (bits - 1) - 1)
+    return np.nonzero(np.abs(np.abs(s - np.floor(s)) - 0.5) < tol)[0].astype(np.int32)
+
+
+def gen_lplr(alg, q, CalderaParams, tag="lplr_mid", m=768, n=1280, rank=64, lplr_iters=10):
+    """Teacher-forcing fixture for the quantised-factor LPLR loop (alg.py:160-188): the first
+    update_LR call of a diag-H run with 4-bit factors.  Recorded: the LR_init (L, R) and, per
+    LPLR iteration, the pre-quantisation L^T / R (full for iteration 0, a 16-column sketch
+    for all), their codes and scales, their near-tie indices, and ||(res - L R) H_sqrt||."""
+    torch.manual_seed(5)
+    W = (torch.randn(m, n) * 0.02).to(torch.float16)
+    h = resampled_h("language_model.model.layers.20.self_attn.q_proj", n, seed=2)
+    p = _params(CalderaParams, q, Q_bits=2, L_bits=4, R_bits=4, rank=rank, iters=2, lplr_iters=lplr_iters)
+    with Tracer(alg) as tr:
+        d = alg.caldera(p, W, torch.diag_embed(h), device="cpu", use_tqdm=False)
+    o = {"W_sha256": np.array(sha(W)), "h": h.numpy(), "global_scale": np.float64(d.global_scale),
+         "m": np.int64(m), "n": np.int64(n), "rank": np.int64(rank), "lplr_iters": np.int64(lplr_iters)}
+    kinds = [k for k, _ in tr.rec]
+    i0 = kinds.index("lr_init")
+    q1 = tr.rec[0][1]
+    o["firstQ_idxs_sha256"] = np.array(sha(q1["A_idxs"]))
+    o["firstQ_scale"] = q1["scale"].numpy()
+    ini = tr.rec[i0][1]
+    res, hs = ini["residual"], ini["H_sqrt_diag"]
+    o["residual_sha256"] = np.array(sha(res))
+    o["H_sqrt_diag"], o["L0"], o["R0"] = hs.numpy(), ini["L"].numpy(), ini["R"].numpy()
+    omL, omR = sketch_omega(m), sketch_omega(n)
+    errs, errs64 = [], []
+    for it in range(lplr_iters):
+        for side, j, om in (("L", i0 + 1 + 2 * it, omL), ("R", i0 + 2 + 2 * it, omR)):
+            kind, c = tr.rec[j]
+            assert kind == "quantize" and c["A"].shape == ((rank, m) if side == "L" else (rank, n))
+            A = c["A"]
+            if it == 0:
+                o[f"{side}{it}_A"] = A.numpy()
+            o[f"{side}{it}_sketch"] = A.double().numpy() @ om
+            o[f"{side}{it}_idxs"] = c["A_idxs"].numpy()
+            o[f"{side}{it}_scale"] = c["scale"].numpy()
+            o[f"{side}{it}_ties"] = near_ties(A, c["bits"])
+        Lh = tr.rec[i0 + 1 + 2 * it][1]["A_hat"].T
+        Rh = tr.rec[i0 + 2 + 2 * it][1]["A_hat"]
+        errs.append(float(torch.linalg.matrix_norm((res - Lh @ Rh) * hs)))   # as alg.py:182 (fp32)
+        errs64.append(float(torch.linalg.matrix_norm((res.double() - Lh.double() @ Rh.double()) * hs.double())))
+    o["lplr_err"] = np.array(errs)
+    o["lplr_err64"] = np.array(errs64)
+    upd = tr.rec[i0 + 1 + 2 * lplr_iters]
+    assert upd[0] == "update_lr"
+    o["best_L_idxs_sha256"] = np.array(sha(upd[1]["L_idxs"]))
+    o["best_R_idxs_sha256"] = np.array(sha(upd[1]["R_idxs"]))
+    for k, v in d.errors.items():
+        o["errors_" + k] = np.array(v, dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, tag + ".npz"), **o)
+    print(tag, "lplr errors", errs, "caldera errors", d.errors)
+
+
+# ---------------------------------------------------------------------------
 def run_large(alg, q, CalderaParams, tag, m, n, H, **kw):
     torch.manual_seed(0)
     W = (torch.randn(m, n) * 0.02).to(torch.float16)
@@ -300,7 +366,7 @@ def gen_large(alg, q, CalderaParams, which=("cfg2", "cfg5", "cfg3")):
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "large"]
+    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "lplr", "large"]
     alg, q, CP = _import_ref()
     cwd = os.getcwd()
     os.chdir(tempfile.mkdtemp())  # bbint appends outlier_log.csv to CWD (quantization.py:126-136)
@@ -313,6 +379,8 @@ if __name__ == "__main__":
             gen_nb(alg, q, CP)
         if "trace" in what:
             gen_trace(alg, q, CP)
+        if "lplr" in what:
+            gen_lplr(alg, q, CP)
         large = [w for w in what if w in ("cfg2", "cfg3", "cfg5")]
         if "large" in what:
             large = ["cfg2", "cfg5", "cfg3"]
