@@ -4,17 +4,24 @@
 H = I) on MI355X.  One "step" = one batched pass of the hot path (caldera() of
 alg.py:24-112) over B matrices resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload cfg2|cfg3|cfg5]
+                  [--no-cpu-baseline] [--no-parity] [--no-api-path]
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank decomposes
 its own batch (matrices are independent: weak scaling, no data-path collective); the
 timed region is bracketed by barrier + synchronize and the max over ranks is reported.
 
 Prints ONE JSON line (rank 0) with value = matrices/s over all ranks, the roofline of the
-dominant kernel (fp32 MFMA GEMM of the subspace filter, timed with HIP events on its
-stream inside the timed region), the relative Frobenius error of Q+LR against the CPU
-reference path on the same matrix, and the CPU baseline (the numpy/LAPACK oracle,
-oracle/caldera_oracle.py, timed on this host on one full decomposition).
+dominant kernel (timed with HIP events on its stream inside the timed region), parity of the
+LAST TIMED STEP's own results (matrices 0-3 of rank 0's batch, seeds 0-3, against the
+reference's golden sketches; matrix 0 also against the CPU baseline's output), the CPU
+baseline (the reference's torch-CPU op sequence, oracle/caldera_torch_cpu.py, on this host),
+and the drop-in API path (caldera_batch with the reference's output placement) timed on one
+extra step of the same batch.
+
+Workloads (BASELINE.json configs): cfg2 (default, the headline metric) 4096x4096, r 128, Q2,
+L/R 16, iters 5, H = I; cfg3 4096x11008, diag H (the golden fixture's resampled
+diag_Hessians.pt entry), r 128, Q2, L/R 16; cfg5 4096x4096, r 256, Q2, L/R 4, lplr 10.
 """
 import argparse
 import json
@@ -31,60 +38,100 @@ for _p in (ROOT, PKG):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-M = N = 4096
-RANK = 128
+WORKLOADS = {
+    "cfg2": dict(m=4096, n=4096, Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, lplr_iters=5, H=False,
+                 batch=256, desc="BASELINE configs[1]: 4096x4096 fp16, rank 128, Q_bits 2, L/R_bits 16, "
+                                 "iters 5, update_order [Q, LR], H = I"),
+    "cfg3": dict(m=4096, n=11008, Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, lplr_iters=5, H=True,
+                 batch=96, desc="BASELINE configs[2]: 4096x11008 fp16, activation-aware diag H (resampled "
+                                "diag_Hessians.pt down_proj entry), rank 128, Q_bits 2, L/R_bits 16, iters 5"),
+    "cfg5": dict(m=4096, n=4096, Q_bits=2, L_bits=4, R_bits=4, rank=256, iters=5, lplr_iters=10, H=False,
+                 batch=64, desc="BASELINE configs[4]: 4096x4096 fp16, rank 256, Q_bits 2, L/R_bits 4, "
+                                "lplr_iters 10, iters 5, H = I"),
+}
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 PEAK_F16_MFMA_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense fp16/bf16 MFMA)
 PEAK_HBM_GBS = 8000.0
 
 
-def make_params():
+def golden():
+    return np.load(os.path.join(ROOT, "tests", "golden", "sum_large.npz"), allow_pickle=False)
+
+
+def make_params(wl):
     from src.caldera.utils.dataclasses import CalderaParams
-    return CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=RANK, iters=5, lplr_iters=5,
-                         update_order=["Q", "LR"], sigma_reg=1e-8)
+    return CalderaParams(Q_bits=wl["Q_bits"], L_bits=wl["L_bits"], R_bits=wl["R_bits"], rank=wl["rank"],
+                         iters=wl["iters"], lplr_iters=wl["lplr_iters"], update_order=["Q", "LR"], sigma_reg=1e-8)
 
 
-def synth_batch(B, seed0, dev):
-    """B synthetic weights with the survey's recipe: per matrix
-    torch.manual_seed(seed); randn(4096, 4096) * 0.02 -> fp16 on the host generator (the
-    seed-0 matrix is the one the golden sketch pins).  Each matrix goes to `dev` as soon as it
-    is made, so host memory stays at one matrix per rank."""
-    out = torch.empty((B, M, N), dtype=torch.float16, device=dev)
+def make_h(wl):
+    """Diagonal of H (cfg3: the resampled real Hessian the golden run used) or None."""
+    return torch.from_numpy(golden()["cfg3_h"]).float() if wl["H"] else None
+
+
+def synth_W(wl, seed):
+    """The survey's recipe: torch.manual_seed(seed); randn(m, n) * 0.02 -> fp16
+    on the host generator (seeds 0-3 are the matrices the golden sketches pin)."""
+    torch.manual_seed(seed)
+    return (torch.randn(wl["m"], wl["n"]) * 0.02).to(torch.float16)
+
+
+def synth_batch(wl, B, seed0, dev):
+    """B synthetic weights; each goes to `dev` as soon as it is made (one matrix of host
+    memory per rank)."""
+    out = torch.empty((B, wl["m"], wl["n"]), dtype=torch.float16, device=dev)
     for i in range(B):
-        torch.manual_seed(seed0 + i)
-        out[i].copy_((torch.randn(M, N) * 0.02).to(torch.float16))
+        out[i].copy_(synth_W(wl, seed0 + i))
     return out
 
 
-def frob_vs_reference(dec_gpu, W_cpu, do_oracle):
-    """Relative Frobenius error of Q+LR (a) against the golden sketch of the reference run
-    (tests/golden/sum_large.npz, seed-0 matrix), (b) against the CPU oracle on the same W."""
+def _sketch(Q, L, R, n):
+    om = torch.from_numpy(np.random.default_rng(1234).standard_normal((n, 16))).to(Q.device)
+    return (Q.double() @ om + L.double() @ (R.double() @ om)).cpu().numpy()
+
+
+def parity_of_timed_step(name, decs, wl):
+    """Relative Frobenius error (16-column Gaussian sketch) of Q + L R of the timed step's
+    matrices 0-3 (seeds 0-3) against the reference's golden run of the same matrix."""
+    g = golden()
+    tags = {"cfg2": ["cfg2", "cfg2s1", "cfg2s2", "cfg2s3"], "cfg3": ["cfg3"], "cfg5": ["cfg5"]}[name]
     out = {}
-    QLR = (dec_gpu.Q.double() + dec_gpu.L.double() @ dec_gpu.R.double()).cpu().numpy()
-    g = np.load(os.path.join(ROOT, "tests", "golden", "sum_large.npz"), allow_pickle=False)
-    om = np.random.default_rng(1234).standard_normal((N, 16))
-    sk = QLR @ om
-    ref = g["cfg2_sketch_QLR"]
-    out["frob_err_vs_ref_sketch"] = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
-    cpu = None
-    if do_oracle:
-        from oracle import caldera_oracle as O  # CPU baseline leg only
-        nthreads = len(os.sched_getaffinity(0))
-        try:  # threads the BLAS/LAPACK backend actually uses (OMP/OPENBLAS limits apply)
-            from threadpoolctl import threadpool_info
-            nthreads = max(int(i.get("num_threads", 1)) for i in threadpool_info()) or nthreads
-        except Exception:
-            pass
-        t0 = time.perf_counter()
-        d = O.caldera(O.Params(Q_bits=2, L_bits=16, R_bits=16, rank=RANK, iters=5,
-                               update_order=["Q", "LR"], sigma_reg=1e-8), W_cpu.numpy())
-        el = time.perf_counter() - t0
-        exp = d.Q.astype(np.float64) + d.L.astype(np.float64) @ d.R.astype(np.float64)
-        out["frob_err_vs_ref"] = float(np.linalg.norm(QLR - exp) / np.linalg.norm(exp))
-        cpu = {"value": 1.0 / el, "unit": "matrices/s", "cores": nthreads, "kind": "port",
-               "sample": f"1 full cfg2 decomposition (seed-0 4096x4096, iters 5) by the numpy/"
-                         f"LAPACK oracle, {el:.1f} s on {nthreads} host threads"}
-    return out, cpu
+    for i, tag in enumerate(tags[:len(decs)]):
+        d = decs[i]
+        sk = _sketch(d["Q"], d["L"], d["R"], wl["n"])
+        ref = g[f"{tag}_sketch_QLR"]
+        out[f"seed{i}"] = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
+    if name == "cfg2":  # the reference's own spread on the same matrices (4 vs 8 CPU threads)
+        sp = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_spread_cfg2_seeds.json")))
+        out["reference_4_vs_8_threads"] = {f"seed{k}": v for k, v in sp["rel_frob_QLR_ref4_vs_ref8"].items()}
+    return out
+
+
+def cpu_baseline(name, wl, dec0):
+    """The reference's torch-CPU op sequence (oracle/caldera_torch_cpu.py) on the seed-0 matrix,
+    on this host's threads; a bounded sample (all `iters` outer iterations for cfg2/cfg3, one
+    outer iteration of cfg5's five, value scaled accordingly)."""
+    from oracle import caldera_torch_cpu as T  # CPU baseline leg only
+    W0 = synth_W(wl, 0)
+    h = make_h(wl)
+    iters = 1 if name == "cfg5" else wl["iters"]
+    t0 = time.perf_counter()
+    d = T.caldera(W0, None if h is None else torch.diag_embed(h), Q_bits=wl["Q_bits"], L_bits=wl["L_bits"],
+                  R_bits=wl["R_bits"], rank=wl["rank"], iters=iters, lplr_iters=wl["lplr_iters"],
+                  sigma_reg=1e-8)
+    el = time.perf_counter() - t0
+    per = el * wl["iters"] / iters
+    cpu = {"value": 1.0 / per, "unit": "matrices/s", "cores": torch.get_num_threads(), "kind": "port",
+           "sample": (f"seed-0 {wl['m']}x{wl['n']} matrix, {iters} of {wl['iters']} outer iterations of the "
+                      f"reference's torch-CPU op sequence (torch.linalg svd/lstsq on MKL, fp32), {el:.1f} s on "
+                      f"{torch.get_num_threads()} host threads" + ("" if iters == wl["iters"] else
+                                                                  f"; value = 1 / ({el:.1f} s x {wl['iters']})"))}
+    par = {}
+    if iters == wl["iters"] and dec0 is not None:
+        exp = d["Q"].double() + d["L"].double() @ d["R"].double()
+        got = (dec0["Q"].double() + dec0["L"].double() @ dec0["R"].double()).cpu()
+        par["frob_err_vs_cpu_baseline"] = float(torch.linalg.norm(got - exp) / torch.linalg.norm(exp))
+    return cpu, par
 
 
 def main():
@@ -92,12 +139,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=None, help="matrices per GPU (default: per workload)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-api-path", action="store_true")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -113,19 +163,22 @@ def main():
     from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     K.load()
-    qp = make_params()
+    qp = make_params(wl)
     ep = EngineParams.from_caldera_params(qp)
-    B = args.batch
-    Wb = synth_batch(B, 1000 * rank, dev)
+    B = args.batch or wl["batch"]
+    Wb = synth_batch(wl, B, 1000 * rank, dev)
+    h = make_h(wl)
+    h = None if h is None else h.to(dev)
     parts = max(1, args.streams or 1)
 
     def step():
         # the hot path: caldera() (alg.py:24-112) on B matrices resident in HBM, results
         # (packed Q codes + scale, L, R, dequantised Q, error history) left in HBM.  The
-        # drop-in API layer adds only output placement (alg.py:81 copies W to the host).
+        # drop-in API layer adds only output placement (alg.py:81 copies W to the host); it is
+        # timed separately below ("api_path").
         engines = [CalderaEngine(ep) for _ in range(parts)]
         bnd = [B * i // parts for i in range(parts + 1)]
-        outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], None, True) for i, e in enumerate(engines)], dev)
+        outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], h, True) for i, e in enumerate(engines)], dev)
         # no reference cycles: the previous step's buffers must be freed as soon as the
         # next step drops them, or the caching allocator grows and stalls on hipMalloc
         return [d for o in outs for d in o], engines[0]
@@ -165,8 +218,11 @@ def main():
         el = float(t.item())
     total = args.steps * B * world
     value = total / el
+    metric = ("weight matrices/sec (4096x4096, rank-128, Q=2-bit) + Frob err vs ref" if args.workload == "cfg2"
+              else f"weight matrices/sec ({wl['m']}x{wl['n']}, rank-{wl['rank']}, Q={wl['Q_bits']}-bit, "
+                   f"L/R={wl['L_bits']}-bit) + Frob err vs ref")
     result = {
-        "metric": "weight matrices/sec (4096x4096, rank-128, Q=2-bit) + Frob err vs ref",
+        "metric": metric,
         "value": value, "unit": "matrices/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32 (fp16 W in; fp32-grade split-fp16 MFMA products, fp64 small solves; int2 codes)",
@@ -189,7 +245,7 @@ def main():
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
             if (pm["config"]["batch"] == B // parts and pm["config"]["p"] == solver_p
-                    and pm["kernel"] == probe["kernel"]):
+                    and pm["config"].get("workload", "cfg2") == args.workload and pm["kernel"] == probe["kernel"]):
                 traffic = pm["hbm_bytes_per_launch"]
         ach_tf = flops / t / 1e12
         ach_gb = nbytes / t / 1e9
@@ -226,13 +282,34 @@ def main():
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
     result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0)}
-    if rank == 0 and world == 1 and not args.no_parity:
-        W0 = synth_batch(1, 0, "cpu")[0]
-        d0 = api.caldera_batch(qp, [W0.to(dev)], None, device=dev)[0]
-        par, cpu = frob_vs_reference(d0, W0, not args.no_cpu_baseline)
+    if rank == 0 and not args.no_parity:
+        # parity of the LAST TIMED STEP's own results (rank 0: batch positions 0-3 = seeds 0-3)
+        par = parity_of_timed_step(args.workload, decs, wl)
+        result["frob_err_vs_ref_sketch"] = par["seed0"]
+        result["parity_timed_step"] = {"vs": "reference golden run of the same matrix (tests/golden/sum_large.npz, "
+                                             "16-column Gaussian sketch of Q + L R)", **par}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, par = cpu_baseline(args.workload, wl, decs[0] if decs else None)
+        result["cpu_baseline"] = cpu
         result.update(par)
-        if cpu is not None:
-            result["cpu_baseline"] = cpu
+    decs = eng = None
+    if not args.no_api_path:
+        # the drop-in API (caldera_batch: the reference's output placement, W copied to the host
+        # as alg.py:81 does, dataclass assembly) on one extra step of the same resident batch
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = api.caldera_batch(qp, Wb, None if h is None else torch.diag_embed(h), device=dev)
+        torch.cuda.synchronize()
+        ta = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([ta], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ta = float(t.item())
+        del out
+        result["api_path"] = {"matrices_per_s": B * world / ta, "ms_per_step": 1000.0 * ta,
+                              "note": "one step through api.caldera_batch (drop-in layout, W to host)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

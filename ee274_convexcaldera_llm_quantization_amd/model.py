@@ -182,7 +182,7 @@ def apply_caldera_quantization(model: torch.nn.Module, hessians=None, quant_para
                                selection: LayerSelection | None = None, error_threshold: float = 0.99,
                                scale_W: bool = False, hadamard: bool = False, device="cuda",
                                max_batch: int = 16, keep_dtype: bool = True, decompose: Callable | None = None,
-                               log: Callable | None = None) -> QuantizationReport:
+                               log: Callable | None = None, hadamard_gate: bool = False) -> QuantizationReport:
     """main.py:135-251 on the MI355X engine.
 
     hessians: {module name: diagonal (n,) or dense (n, n)} — `Hall` (a missing name raises
@@ -190,6 +190,9 @@ def apply_caldera_quantization(model: torch.nn.Module, hessians=None, quant_para
     quant_params: CalderaParams (default `driver_params()`, main.py:167-182).
     keep_dtype: write `out` back in the weight's dtype (the reference assigns the fp32 `out`,
       main.py:199, which only matters for a non-fp32 model).
+    hadamard_gate: apply the 0.99 error gate and the bit accounting to the Hadamard branch
+      too (off by default: main.py:221-240 writes the recovered weight unconditionally and
+      counts nothing).
     decompose(quant_params, Ws, H) -> list of CalderaDecomposition: the engine
       (`api.caldera_batch`) unless given (tests pass a stand-in).
     Returns the QuantizationReport (counters + per-layer outcomes)."""
@@ -231,6 +234,13 @@ def apply_caldera_quantization(model: torch.nn.Module, hessians=None, quant_para
                     if hadamard:
                         out = hadamard_transform(out, inverse=True, original_shape=shapes[i]).contiguous()
                     err = _rel_error(W.to(dev), out)
+                    if hadamard and not hadamard_gate:
+                        # main.py:221-240: the Hadamard branch always writes the recovered
+                        # weight back, with no error gate and no parameter counting
+                        module.weight.data = out.to(W.dtype).to(W.device)
+                        say(f"Applied CALDERA (Hadamard) to {name}.weight, shape: {tuple(W.shape)}")
+                        outcomes[name] = LayerOutcome(name, tuple(W.shape), err, True, dict(dec.errors))
+                        continue
                     ok = err <= error_threshold
                     if ok:
                         module.weight.data = (out.to(W.dtype) if keep_dtype else out).to(W.device)

@@ -3,30 +3,39 @@
 The reference decomposes a model's linear layers one after another in one process
 (main.py:135-251, `apply_CALDERA_quantization`).  The units are independent (no state is
 shared between `caldera()` calls), so here every rank (one process per GPU)
-decomposes the matrices i with i % world == rank, batching same-shape matrices in lockstep
-on its GPU, and the only collective is the final gather of the packed results to rank 0
-(torch.distributed `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo" on CPU).
+decomposes the matrices i with i % world == rank, batching same-shape, same-H matrices in
+lockstep on its GPU, and the only collective is the final gather of the packed results to
+rank 0 (torch.distributed `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo" on
+CPU tests).
 
 Result payload (also the on-disk format, §8f item 2): one uint8 tensor per rank =
-  [u64 little-endian meta length][meta JSON][blob]
+  [u64 little-endian meta length][meta JSON][pad to 16][blob]
 with, per matrix, int2/int4 offset-binary packed Q codes (or int8/int16 codes for 8/16 bits),
-fp32 L (m x r) and R (r x n), and in the JSON its name, shape, scales, global scale and
-error history.  Packing first keeps the 224-matrix Llama-2-7B gather at ~2.9 GB instead of
-~7.4 GB with the reference's unpacked int8 codes.
+fp32 L (m x r) and R (r x n), each 16-byte aligned, and in the JSON its name, shape, scales,
+global scale, error history and array offsets.  The payload is assembled where the results
+live: on the GPU the blob is concatenated in HBM (only the few-KB JSON crosses PCIe), the
+RCCL gather moves it HBM -> HBM over xGMI, and rank 0 unpacks it into device views.
+Packing keeps the 224-matrix Llama-2-7B gather at ~2.9 GB instead of ~7.4 GB with the
+reference's unpacked int8 codes.
+
+Resume (main.py:135-251 decomposes layer after layer; a crash loses everything): with
+`resume_path`, names already in that results file are skipped and the file is rewritten
+(atomically) with everything done so far after this rank's batches finish.
 """
 from __future__ import annotations
 
 import json
+import os
 import struct
 from dataclasses import dataclass, field
 
-import numpy as np
 import torch
 
 LLAMA2_7B_PROJS = (("self_attn.q_proj", 4096, 4096), ("self_attn.k_proj", 4096, 4096),
                    ("self_attn.v_proj", 4096, 4096), ("self_attn.o_proj", 4096, 4096),
                    ("mlp.gate_proj", 11008, 4096), ("mlp.up_proj", 11008, 4096),
                    ("mlp.down_proj", 4096, 11008))
+_ALIGN = 16
 
 
 def llama2_7b_matrices(n_layers: int = 32):
@@ -58,45 +67,55 @@ class MatrixResult:
     R: torch.Tensor              # (r, n) fp32
     global_scale: float
     errors: dict = field(default_factory=dict)
-    extra: dict = field(default_factory=dict)
+    extra: dict = field(default_factory=dict)  # e.g. n_padded: codes on an (m, n_padded) grid
 
 
-def _np(t: torch.Tensor) -> np.ndarray:
-    return t.detach().cpu().contiguous().numpy()
+def _pad(nbytes: int) -> int:
+    return (-nbytes) % _ALIGN
 
 
-def pack_results(results: list[MatrixResult]) -> torch.Tensor:
-    """Serialise results into one uint8 tensor (CPU)."""
-    metas, blobs, off = [], [], 0
+def _as_bytes(t: torch.Tensor, dev) -> torch.Tensor:
+    return t.detach().contiguous().reshape(-1).view(torch.uint8).to(dev)
+
+
+def pack_results(results: list[MatrixResult], device=None) -> torch.Tensor:
+    """Serialise results into one uint8 tensor on `device` (default: the CPU).  On a HIP
+    device the arrays never leave HBM: they are concatenated there, only the JSON is
+    uploaded."""
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    metas, parts, off = [], [], 0
     for r in results:
         entry = {"name": r.name, "m": r.m, "n": r.n, "rank": r.rank, "Q_bits": r.Q_bits,
                  "Q_scale": float(r.Q_scale), "global_scale": float(r.global_scale),
                  "errors": r.errors, "extra": r.extra, "arrays": {}}
         for key, t in (("codes", r.codes), ("L", r.L), ("R", r.R)):
-            a = _np(t)
-            b = a.tobytes()
-            entry["arrays"][key] = {"offset": off, "nbytes": len(b), "dtype": str(a.dtype),
-                                    "shape": list(a.shape)}
-            blobs.append(b)
-            off += len(b)
+            b = _as_bytes(t, dev)
+            entry["arrays"][key] = {"offset": off, "nbytes": b.numel(), "dtype": str(t.dtype).split(".")[-1],
+                                    "shape": list(t.shape)}
+            parts.append(b)
+            pad = _pad(b.numel())
+            if pad:
+                parts.append(torch.zeros(pad, dtype=torch.uint8, device=dev))
+            off += b.numel() + pad
         metas.append(entry)
     meta = json.dumps(metas).encode()
-    buf = struct.pack("<Q", len(meta)) + meta + b"".join(blobs)
-    return torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+    head = struct.pack("<Q", len(meta)) + meta
+    head += b"\0" * _pad(len(head))
+    head_t = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(dev)
+    return torch.cat([head_t] + parts)
 
 
 def unpack_results(buf: torch.Tensor) -> list[MatrixResult]:
-    raw = bytes(buf.cpu().numpy().tobytes())
-    (mlen,) = struct.unpack("<Q", raw[:8])
-    metas = json.loads(raw[8:8 + mlen].decode())
-    base = 8 + mlen
+    """Inverse of pack_results; arrays are views of `buf` on its device."""
+    (mlen,) = struct.unpack("<Q", bytes(buf[:8].cpu().numpy().tobytes()))
+    metas = json.loads(bytes(buf[8:8 + mlen].cpu().numpy().tobytes()).decode())
+    base = 8 + mlen + _pad(8 + mlen)
     out = []
     for e in metas:
         arrs = {}
         for key, d in e["arrays"].items():
-            a = np.frombuffer(raw, dtype=np.dtype(d["dtype"]), count=int(np.prod(d["shape"])) if d["shape"] else 1,
-                              offset=base + d["offset"]).reshape(d["shape"]).copy()
-            arrs[key] = torch.from_numpy(a)
+            s = base + d["offset"]
+            arrs[key] = buf[s:s + d["nbytes"]].view(getattr(torch, d["dtype"])).view(d["shape"])
         out.append(MatrixResult(e["name"], e["m"], e["n"], e["rank"], e["Q_bits"], arrs["codes"],
                                 e["Q_scale"], arrs["L"], arrs["R"], e["global_scale"], e["errors"],
                                 e.get("extra", {})))
@@ -104,8 +123,11 @@ def unpack_results(buf: torch.Tensor) -> list[MatrixResult]:
 
 
 def save_results(path: str, results: list[MatrixResult]):
-    with open(path, "wb") as f:
-        f.write(bytes(pack_results(results).numpy().tobytes()))
+    """Write the packed payload (host copy) atomically."""
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(pack_results(results).numpy().tobytes())
+    os.replace(tmp, path)
 
 
 def load_results(path: str) -> list[MatrixResult]:
@@ -113,10 +135,11 @@ def load_results(path: str) -> list[MatrixResult]:
         return unpack_results(torch.frombuffer(bytearray(f.read()), dtype=torch.uint8))
 
 
-def gather_to_rank0(payload: torch.Tensor, group=None, device=None):
+def gather_to_rank0(payload: torch.Tensor, group=None, device=None, to_host: bool = False):
     """Gather every rank's uint8 payload to rank 0 (padded to the max size).  Returns the
-    list of per-rank payloads on rank 0, None elsewhere.  device: where the collective
-    runs (a HIP device for "nccl" = RCCL over xGMI, CPU for "gloo")."""
+    list of per-rank payloads on rank 0 (on `device`, i.e. in HBM for "nccl"; host copies
+    with to_host), None elsewhere.  device: where the collective runs (a HIP device for
+    "nccl" = RCCL over xGMI, CPU for "gloo")."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -131,31 +154,46 @@ def gather_to_rank0(payload: torch.Tensor, group=None, device=None):
     dist.gather(buf, gather_list=gl, dst=0, group=group)
     if rank != 0:
         return None
-    return [g[: int(s.item())].cpu() for g, s in zip(gl, sizes)]
+    out = [g[: int(s.item())] for g, s in zip(gl, sizes)]
+    return [o.cpu() for o in out] if to_host else out
 
 
 def decompose_sharded(items, decompose_batch, *, rank: int, world: int, max_batch: int = 16,
-                      group=None, gather: bool = True, device=None):
+                      group=None, gather: bool = True, device=None, h_key=None, resume_path=None):
     """items: list of (name, m, n, seed).  decompose_batch(list_of_items) -> list of
-    MatrixResult (the GPU engine on MI355X; a stub in the CPU gloo tests).  Same-shape
-    matrices of this rank's shard run together in batches of <= max_batch."""
+    MatrixResult (the GPU engine on MI355X; a stub in the CPU gloo tests).  Matrices of this
+    rank's shard that share shape AND Hessian (h_key(name), default: all the same) run
+    together in batches of <= max_batch.  resume_path: per-rank results file; names in it
+    are not decomposed again, and it is rewritten with this rank's results at the end."""
     mine = [items[i] for i in shard_indices(len(items), world, rank)]
-    by_shape: dict[tuple, list] = {}
+    done = []
+    if resume_path is not None and os.path.exists(resume_path):
+        names = {it[0] for it in mine}
+        done = [r for r in load_results(resume_path) if r.name in names]
+        have = {r.name for r in done}
+        mine = [it for it in mine if it[0] not in have]
+    groups: dict[tuple, list] = {}
     for it in mine:
-        by_shape.setdefault((it[1], it[2]), []).append(it)
-    batches = [group_items[s:s + max_batch] for group_items in by_shape.values()
-               for s in range(0, len(group_items), max_batch)]
+        groups.setdefault((it[1], it[2], None if h_key is None else h_key(it[0])), []).append(it)
+    batches = [g[s:s + max_batch] for g in groups.values() for s in range(0, len(g), max_batch)]
     results = []
-    if hasattr(decompose_batch, "run_all"):  # all batches at once (interleaved on HIP streams)
-        results = decompose_batch.run_all(batches)
-    else:
-        for b in batches:
-            results.extend(decompose_batch(b))
+    if batches:
+        if hasattr(decompose_batch, "run_all"):  # all batches at once (interleaved on HIP streams)
+            results = decompose_batch.run_all(batches)
+        else:
+            for b in batches:
+                results.extend(decompose_batch(b))
+    dev = device if device is not None else (results[0].L.device if results else torch.device("cpu"))
+    if done:
+        results.extend(MatrixResult(r.name, r.m, r.n, r.rank, r.Q_bits, r.codes.to(dev), r.Q_scale, r.L.to(dev),
+                                    r.R.to(dev), r.global_scale, r.errors, r.extra) for r in done)
     order = {it[0]: i for i, it in enumerate(items)}
     results.sort(key=lambda r: order[r.name])
+    if resume_path is not None and batches:
+        save_results(resume_path, results)
     if not gather or world == 1:
         return results
-    payloads = gather_to_rank0(pack_results(results), group=group, device=device)
+    payloads = gather_to_rank0(pack_results(results, device=dev), group=group, device=dev)
     if payloads is None:
         return None
     allres = [r for pl in payloads for r in unpack_results(pl)]
@@ -165,7 +203,8 @@ def decompose_sharded(items, decompose_batch, *, rank: int, world: int, max_batc
 
 def engine_decompose_batch(quant_params, device, H_of=None):
     """decompose_batch for the MI355X engine: synthetic fp16 weights randn*0.02 per seed
-    (random-init model, no checkpoint access), H_of(name) -> diagonal or None."""
+    (random-init model, no checkpoint access), H_of(name) -> diagonal (n,) or None.  Every
+    matrix of a batch must have the same H (decompose_sharded groups by h_key; this checks)."""
     from .engine import CalderaEngine, EngineParams
     from .overlap import run_interleaved
 
@@ -176,10 +215,24 @@ def engine_decompose_batch(quant_params, device, H_of=None):
             ws.append((torch.randn(m, n) * 0.02).to(torch.float16))
         return torch.stack(ws).to(device)
 
+    def h_of(batch_items):
+        if H_of is None:
+            return None
+        hs = [H_of(it[0]) for it in batch_items]
+        h0 = hs[0]
+        for h in hs[1:]:
+            if h is not h0 and not (h is not None and h0 is not None and torch.equal(h, h0)):
+                raise ValueError("engine_decompose_batch: matrices of one batch need the same H "
+                                 "(pass h_key to decompose_sharded)")
+        return h0
+
     def results(batch_items, eng):
-        return [MatrixResult(name, m, n, d["L"].shape[1], quant_params.Q_bits, d["codes"], d["Q_scale"], d["L"],
-                             d["R"], d["global_scale"], d["errors"])
-                for (name, m, n, seed), d in zip(batch_items, eng.last_packed)]
+        out = []
+        for (name, m, n, seed), d in zip(batch_items, eng.last_packed):
+            extra = {"n_padded": d["n_padded"]} if "n_padded" in d else {}
+            out.append(MatrixResult(name, m, n, d["L"].shape[1], quant_params.Q_bits, d["codes"], d["Q_scale"],
+                                    d["L"], d["R"], d["global_scale"], d["errors"], extra))
+        return out
 
     def run_all(batches):
         """Every batch (one per shape class) on its own engine and HIP stream, interleaved at
@@ -187,9 +240,10 @@ def engine_decompose_batch(quant_params, device, H_of=None):
         the 256 CUs to the other batches' GEMMs (config 4 share of one rank at 8 GPUs:
         0.43 s vs 0.78 s one batch after another, tools/bench_model.py)."""
         Ws = [weights(b) for b in batches]
+        hs = [h_of(b) for b in batches]
         engines = [CalderaEngine(EngineParams.from_caldera_params(quant_params)) for _ in batches]
-        run_interleaved([e.run_iter(W, H_of(b[0][0]) if H_of is not None else None)
-                         for e, W, b in zip(engines, Ws, batches)], torch.device(device))
+        run_interleaved([e.run_iter(W, None if h is None else h.to(device))
+                         for e, W, h in zip(engines, Ws, hs)], torch.device(device))
         return [r for b, e in zip(batches, engines) for r in results(b, e)]
 
     def run(batch_items):

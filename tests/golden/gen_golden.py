@@ -21,7 +21,7 @@ Fixtures:
   sum_large.npz   configs 2, 3, 5 at full size: hashes, scalars, error lists and
                   float64 sketches (Q+LR)@Omega and (L1 R1)@Omega of the first LR step.
 
-Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [lplr] [large]
+Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [lplr] [seeds] [large]
 """
 import hashlib
 import json
@@ -314,8 +314,8 @@ def gen_lplr(alg, q, CalderaParams, tag="lplr_mid", m=768, n=1280, rank=64, lplr
 
 
 # ---------------------------------------------------------------------------
-def run_large(alg, q, CalderaParams, tag, m, n, H, **kw):
-    torch.manual_seed(0)
+def run_large(alg, q, CalderaParams, tag, m, n, H, seed=0, **kw):
+    torch.manual_seed(seed)
     W = (torch.randn(m, n) * 0.02).to(torch.float16)
     p = _params(CalderaParams, q, **kw)
     t = time.time()
@@ -365,8 +365,22 @@ def gen_large(alg, q, CalderaParams, which=("cfg2", "cfg5", "cfg3")):
     np.savez_compressed(path, **o)
 
 
+def gen_seeds(alg, q, CalderaParams, seeds=(1, 2, 3)):
+    """Config 2 on the bench's other seeds (bench.py synth_batch: seed i -> matrix i): the
+    Q+LR sketch, norm and error lists the bench and the B = 256 batch test pin."""
+    path = os.path.join(OUT, "sum_large.npz")
+    o = dict(np.load(path))
+    for s in seeds:
+        r = run_large(alg, q, CalderaParams, f"cfg2s{s}", 4096, 4096, None, seed=s,
+                      Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5)
+        keep = ("_W_sha256", "_global_scale", "_sketch_QLR", "_norm_QLR", "_errors_Q", "_errors_LR",
+                "_firstQ_idxs_sha256", "_seconds")
+        o.update({k: v for k, v in r.items() if k.endswith(keep)})
+    np.savez_compressed(path, **o)
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "lplr", "large"]
+    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "lplr", "large", "seeds"]
     alg, q, CP = _import_ref()
     cwd = os.getcwd()
     os.chdir(tempfile.mkdtemp())  # bbint appends outlier_log.csv to CWD (quantization.py:126-136)
@@ -381,6 +395,8 @@ if __name__ == "__main__":
             gen_trace(alg, q, CP)
         if "lplr" in what:
             gen_lplr(alg, q, CP)
+        if "seeds" in what:
+            gen_seeds(alg, q, CP)
         large = [w for w in what if w in ("cfg2", "cfg3", "cfg5")]
         if "large" in what:
             large = ["cfg2", "cfg5", "cfg3"]

@@ -174,6 +174,11 @@ def test_caller_threshold_and_hadamard():
     names = [j[0] for j in select_layers(m)[0]]
     W0 = {n: dict(m.named_modules())[n].weight.data.clone() for n in names}
     rep = apply_caldera_quantization(m, None, _params(), hadamard=True)
+    # main.py:221-240: the Hadamard branch writes back unconditionally and counts nothing
+    skipped_only = select_layers(_tiny_model(1))[1].unquantized_language_param_count
+    assert rep.quantized_param_count == 0 and rep.unquantized_language_param_count == skipped_only
+    rep_gate0 = apply_caldera_quantization(_tiny_model(1), None, _params(), hadamard=True, error_threshold=0.0)
+    assert all(o.applied for o in rep_gate0.layers) and rep_gate0.quantized_param_count == 0
     for o in rep.layers:
         assert o.applied and 0.0 < o.rel_error < 0.99
         if o.shape == (512, 512):  # no padding: the orthogonal transform keeps the error

@@ -98,3 +98,55 @@ def test_gather_world2_gloo():
     for name, codes, L, R, qs, errs in got:
         assert torch.equal(torch.from_numpy(codes), ref[name].codes) and torch.equal(torch.from_numpy(L), ref[name].L)
         assert torch.equal(torch.from_numpy(R), ref[name].R) and qs == ref[name].Q_scale and errs == ref[name].errors
+
+
+def test_batches_group_by_hessian():
+    """Same-shape matrices of different layers carry different diagonal Hessians: a batch
+    (one engine run, one H) must never mix them (decompose_sharded h_key)."""
+    items = _items()
+    seen = []
+
+    def rec(batch_items):
+        seen.append([it[0] for it in batch_items])
+        return _stub(batch_items)
+
+    layer_of = lambda name: name.split(".")[2]  # noqa: E731  (one Hessian per layer here)
+    res = S.decompose_sharded(items, rec, rank=0, world=1, max_batch=8, h_key=layer_of)
+    assert [r.name for r in res] == [it[0] for it in items]
+    for b in seen:
+        assert len({layer_of(n) for n in b}) == 1, b
+    # without h_key, same-shape matrices of different layers share batches
+    seen.clear()
+    S.decompose_sharded(items, rec, rank=0, world=1, max_batch=8)
+    assert any(len({layer_of(n) for n in b}) > 1 for b in seen)
+
+
+def test_resume_skips_finished_matrices(tmp_path):
+    items = _items()
+    path = str(tmp_path / "rank0.bin")
+    first = S.decompose_sharded(items[:10], _stub, rank=0, world=1, max_batch=4, resume_path=path)
+    calls = []
+
+    def rec(batch_items):
+        calls.extend(it[0] for it in batch_items)
+        return _stub(batch_items)
+
+    res = S.decompose_sharded(items, rec, rank=0, world=1, max_batch=4, resume_path=path)
+    assert sorted(calls) == sorted(it[0] for it in items[10:])  # only the unfinished ones ran
+    assert [r.name for r in res] == [it[0] for it in items]
+    ref = {r.name: r for r in _stub(items)}
+    for r in res:
+        assert torch.equal(r.codes, ref[r.name].codes) and torch.equal(r.L, ref[r.name].L)
+    assert [r.name for r in S.load_results(path)] == [it[0] for it in items]
+    assert [r.name for r in first] == [it[0] for it in items[:10]]
+
+
+def test_pack_keeps_padded_grid_and_alignment():
+    """n % 4 != 0: packed codes stay on the (m, n_padded) grid; extra["n_padded"] travels
+    with them, and every array starts 16-byte aligned (device views need it)."""
+    r = S.MatrixResult("x", 5, 7, 2, 2, torch.arange(10, dtype=torch.uint8), 0.5, torch.randn(5, 2),
+                       torch.randn(2, 7), 1.0, {"Q": [1.0]}, {"n_padded": 8})
+    buf = S.pack_results([r, r])
+    back = S.unpack_results(buf)
+    assert back[1].extra == {"n_padded": 8} and torch.equal(back[1].codes, r.codes)
+    assert torch.equal(back[1].R, r.R) and back[1].R.data_ptr() % 16 == 0
