@@ -226,9 +226,8 @@ def main():
         "value": value, "unit": "matrices/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32 (fp16 W in; fp32-grade split-fp16 MFMA products, fp64 small solves; int2 codes)",
-        "data": "synthetic: W = randn(4096,4096)*0.02 -> fp16, seed per matrix",
-        "config": {"workload": "BASELINE configs[1]: 4096x4096 fp16, rank 128, Q_bits 2, L/R_bits 16, "
-                               "iters 5, update_order [Q, LR], H = I",
+        "data": f"synthetic: W = randn({wl['m']},{wl['n']})*0.02 -> fp16, seed per matrix",
+        "config": {"workload": wl["desc"], "name": args.workload,
                    "batch_per_gpu": B, "matrices_per_step": B * world, "parallelism": f"dp{world} (matrix-sharded)"},
     }
     if probe["count"]:

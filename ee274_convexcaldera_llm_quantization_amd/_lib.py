@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcaldera_hip.so")
 
-CQ_F32, CQ_F16, CQ_BF16 = 0, 1, 2
+CQ_F32, CQ_F16, CQ_BF16, CQ_F64 = 0, 1, 2, 3
 EPI_LINEAR, EPI_RESID, EPI_WERR = 0, 1, 2
 CQ_EINVAL, CQ_EHIP, CQ_EWORKSPACE = -1, -2, -3
 
@@ -119,6 +119,7 @@ _SIGS = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_batched_dot": (c_int, [c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_act_sqsum_workspace": (c_size, [c_i64, c_i64]),
     "cq_act_sqsum_cols": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp, c_size, c_vp]),
     "cq_act_sqsum_rows": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp]),
@@ -220,6 +221,21 @@ def weighted_sqsum(x: torch.Tensor, w: torch.Tensor | None, ncols: int) -> torch
     ws = workspace(lib.cq_rms_scale_workspace(B, numel), x.device)
     _check(lib.cq_weighted_sqsum(dt, _p(x), B, numel, _p(w), ncols, _p(out), _p(ws), ws.numel(),
                                  _stream(x.device)), "cq_weighted_sqsum")
+    return out
+
+
+def batched_dot(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """out[b] = <x[b], y[b]> in fp64 (x, y (B, ...) fp32 or fp64, same shape, contiguous)."""
+    _require_hip(x, y)
+    assert x.shape == y.shape and x.dtype == y.dtype and x.is_contiguous() and y.is_contiguous()
+    dt = {torch.float32: CQ_F32, torch.float64: CQ_F64}[x.dtype]
+    B = x.shape[0]
+    numel = x[0].numel()
+    out = torch.empty(B, dtype=torch.float64, device=x.device)
+    lib = load()
+    ws = workspace(lib.cq_rms_scale_workspace(B, numel), x.device)
+    _check(lib.cq_batched_dot(dt, _p(x), _p(y), B, numel, _p(out), _p(ws), ws.numel(), _stream(x.device)),
+           "cq_batched_dot")
     return out
 
 

@@ -70,7 +70,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
     streams = max(1, min(int(streams), B))
     bounds = [B * i // streams for i in range(streams + 1)]
     engines = [CalderaEngine(params, **(engine_kwargs or {})) for _ in range(streams)]
-    gens = [e.run_iter(W[bounds[i]:bounds[i + 1]], h, scale_W, use_tqdm and i == 0)
+    gens = [e.run_iter(W[bounds[i]:bounds[i + 1]], h, scale_W, use_tqdm and i == 0, w_to_host=True)
             for i, e in enumerate(engines)]
     res = [d for part in run_interleaved(gens, comp) for d in part]
     eng = engines[0]
@@ -78,12 +78,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
         eng.parts = engines
     out = []
     lr_dev = dev_req if dev_req.type == "cpu" else comp
-    # alg.py:81 keeps W on the host: one batched copy into pinned memory instead of B
-    # pageable copies
-    W_host = torch.empty((B, m, n), dtype=res[0]["W"].dtype, pin_memory=True)
-    for b, d in enumerate(res):
-        W_host[b].copy_(d["W"], non_blocking=True)
-    torch.cuda.current_stream(comp).synchronize()
+    # alg.py:81 keeps W on the host: the engines copied it there while they ran (w_to_host)
     for b, d in enumerate(res):
         dec = decomposition_cls(
             Q=d["Q"].to(w_dev),
@@ -93,7 +88,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
         dec.scaleWH = None
         dec.SU = torch.ones(n, dtype=w_dtype, device=w_dev)
         dec.SV = torch.ones(m, dtype=w_dtype, device=w_dev)
-        dec.W = W_host[b]
+        dec.W = d["W"]
         for f in ("Q_idxs", "L_idxs", "R_idxs"):
             v = d[f]
             setattr(dec, f, v.to(lr_dev if f != "Q_idxs" else w_dev) if v is not None else None)

@@ -1,0 +1,424 @@
+// Block Jacobi symmetric eigensolver spread over many workgroups per matrix, for the
+// Rayleigh-Ritz matrices that do not fit one CU's LDS (p > 192: rank 256 at config 5,
+// p = 384; rank 200 in main.py:176, p = 288).  Replaces the one-CU global-memory Jacobi
+// (cq_small.hip jacobi_kernel), which serialised a p = 384 solve on one CU at ~77 ms.
+//
+// The p indices are cut into nblk blocks of NB = 32.  A sweep is nblk - 1 steps of the
+// round-robin pairing of blocks; in a step every pair (a, c) forms a 64 x 64 subproblem:
+//   bj_solve_kernel   (one workgroup per pair): the subproblem A[P, P] (P = a u c) lives in
+//                     LDS and is diagonalised by cyclic two-sided Jacobi (threshold rotations,
+//                     the same rule as the one-CU kernels); it writes back the diagonalised
+//                     block and V_P (64 x 64, fp64);
+//   bj_update_kernel  (one workgroup per off-diagonal pair-block (P, Q), plus one per pair
+//                     for the eigenvector rows): A[P, Q] <- V_P^T A[P, Q] V_Q, Vt[P, :] <-
+//                     V_P^T Vt[P, :].  Blocks whose pairs did not rotate are left alone.
+// Both kernels also leave per-block off-diagonal / diagonal square sums; bj_check_kernel
+// turns them into the per-matrix stop test off^2 <= tol^2 sum a_ii^2 after every sweep
+// (the host reads the flags once per sweep and stops when every matrix has converged;
+// converged matrices' workgroups exit at entry).  Everything is fp64.
+#include "cq_common.h"
+
+namespace cq {
+namespace {
+
+constexpr int NB = 32;        // block size
+constexpr int D = 2 * NB;     // subproblem dimension
+constexpr int LDP = D + 1;    // padded LDS row (fp64): column walks hit different banks
+constexpr int BT = 256;       // threads per workgroup
+#ifndef CQ_BJ_INNER
+#define CQ_BJ_INNER 1
+#endif
+constexpr int kInnerMax = CQ_BJ_INNER;  // inner sweeps per subproblem and step (partial solves: see DESIGN.md)
+
+// round-robin pairing of n (even) items, round rd, slot q: (i < j)
+__device__ __forceinline__ void rr(int n, int rd, int q, int& i, int& j) {
+    const int n1 = n - 1;
+    if (q == 0) { i = n1; j = rd; }
+    else {
+        i = rd + q; if (i >= n1) i -= n1;
+        j = rd - q; if (j < 0) j += n1;
+    }
+    if (i > j) { const int t = i; i = j; j = t; }
+}
+
+// global index of subproblem row u for the pair (a, c) of blocks; -1 past p (or a virtual
+// block when nblk was rounded up to even)
+__device__ __forceinline__ int gidx(int a, int c, int u, int p) {
+    const int g = (u < NB ? a : c) * NB + (u & (NB - 1));
+    return g < p ? g : -1;
+}
+
+__device__ __forceinline__ void rot_params(double aii, double ajj, double aij, double thr, double& c, double& s) {
+    c = 1.0; s = 0.0;
+    if (fabs(aij) > 1e-300 && fabs(aij) > thr * sqrt(fabs(aii * ajj))) {
+        const double th = (ajj - aii) / (2.0 * aij);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
+        c = 1.0 / sqrt(1.0 + t * t);
+        s = t * c;
+    }
+}
+
+__global__ __launch_bounds__(BT) void bj_init_kernel(double* __restrict__ A_all, int p, double* __restrict__ Vt_all,
+                                                     int* __restrict__ done, int* __restrict__ sweeps,
+                                                     double tol) {
+    const int64_t b = blockIdx.x;
+    double* A = A_all + b * (int64_t)p * p;
+    __shared__ double red[16];
+    double off = 0.0, dg = 0.0;
+    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += BT) {
+        const int i = (int)(t / p), c = (int)(t % p);
+        if (Vt_all) Vt_all[b * (int64_t)p * p + t] = (i == c) ? 1.0 : 0.0;
+        if (i < c) {  // symmetrise (Rayleigh-Ritz matrices carry rounding asymmetry)
+            const double s = 0.5 * (A[(int64_t)i * p + c] + A[(int64_t)c * p + i]);
+            A[(int64_t)i * p + c] = s;
+            A[(int64_t)c * p + i] = s;
+            off += 2.0 * s * s;
+        } else if (i == c) {
+            const double v = A[(int64_t)i * p + i];
+            dg += v * v;
+        }
+    }
+    const double offs = block_sum_f64(off, red);
+    const double dgs = block_sum_f64(dg, red);
+    if (threadIdx.x == 0) {
+        done[b] = (offs <= tol * tol * dgs) ? 1 : 0;
+        sweeps[b] = 0;
+    }
+}
+
+// One workgroup per (pair q, matrix b): diagonalise the 64 x 64 subproblem in LDS.
+__global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all, int p, int nblk, int step,
+                                                      double thr, double* __restrict__ Vs_all,
+                                                      int* __restrict__ rot_all, const int* __restrict__ done,
+                                                      double* __restrict__ part_off, double* __restrict__ part_dg,
+                                                      int nslots) {
+    const int q = blockIdx.x, npair = nblk / 2;
+    const int64_t b = blockIdx.y;
+    if (done[b]) return;
+    __shared__ double As[D * LDP];
+    __shared__ double Vsm[D * LDP];
+    __shared__ double cs[NB], sn[NB];
+    __shared__ int pi_[NB], pj_[NB];
+    __shared__ int gi[D];
+    __shared__ int any_rot;
+    __shared__ double red[16];
+    const int tid = threadIdx.x;
+    double* A = A_all + b * (int64_t)p * p;
+    int a, c;
+    rr(nblk, step, q, a, c);
+    if (tid < D) gi[tid] = gidx(a, c, tid, p);
+    __syncthreads();
+    for (int t = tid; t < D * D; t += BT) {
+        const int u = t / D, v = t % D;
+        const int gu = gi[u], gv = gi[v];
+        As[u * LDP + v] = (gu >= 0 && gv >= 0) ? A[(int64_t)gu * p + gv] : 0.0;
+        Vsm[u * LDP + v] = (u == v) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    int rotated = 0;
+    for (int inner = 0; inner < kInnerMax; ++inner) {
+        if (tid == 0) any_rot = 0;
+        __syncthreads();
+        for (int rd = 0; rd < D - 1; ++rd) {
+            if (tid < NB) {
+                int i, j;
+                rr(D, rd, tid, i, j);
+                double cc, ss;
+                rot_params(As[i * LDP + i], As[j * LDP + j], As[i * LDP + j], thr, cc, ss);
+                if (ss != 0.0) any_rot = 1;
+                cs[tid] = cc; sn[tid] = ss; pi_[tid] = i; pj_[tid] = j;
+            }
+            __syncthreads();
+            // A <- J^T A J on the 32 x 32 pair-blocks (each element belongs to one block)
+            for (int t = tid; t < NB * NB; t += BT) {
+                const int qa = t / NB, qb = t % NB;
+                const double sa = sn[qa], sb = sn[qb];
+                if (sa == 0.0 && sb == 0.0) continue;
+                const double ca = cs[qa], cb = cs[qb];
+                const int ia = pi_[qa], ja = pj_[qa], ib = pi_[qb], jb = pj_[qb];
+                const double x00 = As[ia * LDP + ib], x01 = As[ia * LDP + jb];
+                const double x10 = As[ja * LDP + ib], x11 = As[ja * LDP + jb];
+                const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
+                double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
+                if (qa == qb) { z01 = 0.0; z10 = 0.0; }  // the annihilated pair
+                As[ia * LDP + ib] = z00; As[ia * LDP + jb] = z01;
+                As[ja * LDP + ib] = z10; As[ja * LDP + jb] = z11;
+            }
+            // V <- V J (columns i, j of every row)
+            for (int t = tid; t < D * NB; t += BT) {
+                const int u = t / NB, qq = t % NB;
+                const double ss = sn[qq];
+                if (ss == 0.0) continue;
+                const double cc = cs[qq];
+                const int i = pi_[qq], j = pj_[qq];
+                const double vi = Vsm[u * LDP + i], vj = Vsm[u * LDP + j];
+                Vsm[u * LDP + i] = cc * vi - ss * vj;
+                Vsm[u * LDP + j] = ss * vi + cc * vj;
+            }
+            __syncthreads();
+        }
+        const int anyr = any_rot;
+        __syncthreads();
+        if (!anyr) break;
+        rotated = 1;
+    }
+    // write back the (block-)diagonalised subproblem, its V, and its square sums
+    double off = 0.0, dg = 0.0;
+    for (int t = tid; t < D * D; t += BT) {
+        const int u = t / D, v = t % D;
+        const int gu = gi[u], gv = gi[v];
+        if (gu < 0 || gv < 0) continue;
+        const double x = As[u * LDP + v];
+        if (rotated) A[(int64_t)gu * p + gv] = x;
+        if (u == v) dg += x * x; else off += x * x;
+    }
+    double* Vs = Vs_all + (b * npair + q) * (int64_t)(D * D);
+    if (rotated)
+        for (int t = tid; t < D * D; t += BT) Vs[t] = Vsm[(t / D) * LDP + (t % D)];
+    const double offs = block_sum_f64(off, red);
+    const double dgs = block_sum_f64(dg, red);
+    if (tid == 0) {
+        rot_all[b * npair + q] = rotated;
+        part_off[b * nslots + q] = offs;
+        part_dg[b * npair + q] = dgs;
+    }
+}
+
+// 4 x 4 register tile per thread of a 64 x 64 fp64 product C = op(X) Y from LDS.
+// transX: C[u][v] = sum_k X[k][u] Y[k][v]; else C[u][v] = sum_k X[u][k] Y[k][v].
+template <bool transX>
+__device__ __forceinline__ void mm64(const double* X, const double* Y, double acc[4][4], int tu, int tv) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+    for (int k = 0; k < D; ++k) {
+        double xa[4], yb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xa[i] = transX ? X[k * LDP + tu + 16 * i] : X[(tu + 16 * i) * LDP + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yb[j] = Y[k * LDP + tv + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fma(xa[i], yb[j], acc[i][j]);
+    }
+}
+
+__device__ __forceinline__ void load_v(double* dst, const double* Vs, bool rotated, int tid) {
+    for (int t = tid; t < D * D; t += BT) {
+        const int u = t / D, v = t % D;
+        dst[u * LDP + v] = rotated ? Vs[t] : (u == v ? 1.0 : 0.0);
+    }
+}
+
+// Workgroups [0, npair*(npair-1)): off-diagonal pair-block (P, Q), A[P,Q] <- V_P^T A[P,Q] V_Q.
+// Workgroups [npair*(npair-1), + npair) (with eigenvectors): Vt[P, :] <- V_P^T Vt[P, :].
+__global__ __launch_bounds__(BT) void bj_update_kernel(double* __restrict__ A_all, int p, int nblk, int step,
+                                                       const double* __restrict__ Vs_all,
+                                                       const int* __restrict__ rot_all, const int* __restrict__ done,
+                                                       double* __restrict__ Vt_all, double* __restrict__ part_off,
+                                                       int nslots) {
+    const int npair = nblk / 2, noff = npair * (npair - 1);
+    const int w = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    if (done[b]) return;
+    __shared__ double Xs[D * LDP];
+    __shared__ double Ys[D * LDP];
+    __shared__ double Ms[D * LDP];
+    __shared__ int gP[D], gQ[D];
+    __shared__ double red[16];
+    const int tid = threadIdx.x, tu = tid / 16, tv = tid % 16;
+    double* A = A_all + b * (int64_t)p * p;
+    const int* rot = rot_all + b * npair;
+    const double* Vs = Vs_all + b * npair * (int64_t)(D * D);
+    if (w < noff) {
+        const int P = w / (npair - 1);
+        int Q = w % (npair - 1);
+        if (Q >= P) ++Q;
+        int a, c, e, f;
+        rr(nblk, step, P, a, c);
+        rr(nblk, step, Q, e, f);
+        if (tid < D) { gP[tid] = gidx(a, c, tid, p); gQ[tid] = gidx(e, f, tid, p); }
+        __syncthreads();
+        const bool rp = rot[P] != 0, rq = rot[Q] != 0;
+        for (int t = tid; t < D * D; t += BT) {
+            const int u = t / D, v = t % D;
+            const int gu = gP[u], gv = gQ[v];
+            Ms[u * LDP + v] = (gu >= 0 && gv >= 0) ? A[(int64_t)gu * p + gv] : 0.0;
+        }
+        double off = 0.0;
+        if (rp || rq) {
+            load_v(Xs, Vs + (int64_t)P * D * D, rp, tid);
+            load_v(Ys, Vs + (int64_t)Q * D * D, rq, tid);
+            __syncthreads();
+            double acc[4][4];
+            mm64<true>(Xs, Ms, acc, tu, tv);       // T = V_P^T A_PQ
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) Ms[(tu + 16 * i) * LDP + tv + 16 * j] = acc[i][j];
+            __syncthreads();
+            mm64<false>(Ms, Ys, acc, tu, tv);      // T V_Q
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int u = tu + 16 * i, v = tv + 16 * j;
+                    const int gu = gP[u], gv = gQ[v];
+                    if (gu >= 0 && gv >= 0) {
+                        A[(int64_t)gu * p + gv] = acc[i][j];
+                        off += acc[i][j] * acc[i][j];
+                    }
+                }
+        } else {
+            __syncthreads();
+            for (int t = tid; t < D * D; t += BT) {
+                const double x = Ms[(t / D) * LDP + (t % D)];
+                off += x * x;
+            }
+        }
+        const double offs = block_sum_f64(off, red);
+        if (tid == 0) part_off[b * nslots + npair + w] = offs;
+        return;
+    }
+    // eigenvector rows of pair P
+    const int P = w - noff;
+    if (!Vt_all || !rot[P]) return;
+    int a, c;
+    rr(nblk, step, P, a, c);
+    if (tid < D) gP[tid] = gidx(a, c, tid, p);
+    load_v(Xs, Vs + (int64_t)P * D * D, true, tid);
+    double* Vt = Vt_all + b * (int64_t)p * p;
+    for (int x0 = 0; x0 < p; x0 += D) {
+        __syncthreads();
+        for (int t = tid; t < D * D; t += BT) {
+            const int u = t / D, l = t % D;
+            const int gu = gP[u];
+            Ms[u * LDP + l] = (gu >= 0 && x0 + l < p) ? Vt[(int64_t)gu * p + x0 + l] : 0.0;
+        }
+        __syncthreads();
+        double acc[4][4];
+        mm64<true>(Xs, Ms, acc, tu, tv);           // V_P^T Vt[P, x0:x0+64]
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int u = tu + 16 * i, l = tv + 16 * j;
+                const int gu = gP[u];
+                if (gu >= 0 && x0 + l < p) Vt[(int64_t)gu * p + x0 + l] = acc[i][j];
+            }
+    }
+}
+
+__global__ void bj_check_kernel(const double* __restrict__ part_off, const double* __restrict__ part_dg, int nslots,
+                                int npair, double tol, int* __restrict__ done, int* __restrict__ sweeps) {
+    const int64_t b = blockIdx.x;
+    if (done[b]) return;
+    __shared__ double red[16];
+    double off = 0.0, dg = 0.0;
+    for (int i = threadIdx.x; i < nslots; i += blockDim.x) off += part_off[b * nslots + i];
+    for (int i = threadIdx.x; i < npair; i += blockDim.x) dg += part_dg[b * npair + i];
+    const double offs = block_sum_f64(off, red);
+    const double dgs = block_sum_f64(dg, red);
+    if (threadIdx.x == 0) {
+        sweeps[b] += 1;
+        if (offs <= tol * tol * dgs) done[b] = 1;
+    }
+}
+
+// Descending eigenvalues by rank counting (ties by index); column rank(i) of V = Vt row i.
+__global__ __launch_bounds__(BT) void bj_finish_kernel(const double* __restrict__ A_all, int p,
+                                                       const double* __restrict__ Vt_all, double* __restrict__ evals,
+                                                       float* __restrict__ V32, double* __restrict__ V64,
+                                                       const int* __restrict__ sweeps, int* __restrict__ sweeps_out,
+                                                       int* __restrict__ rank_ws) {
+    const int64_t b = blockIdx.x;
+    const double* A = A_all + b * (int64_t)p * p;
+    int* rk = rank_ws + b * (int64_t)p;
+    for (int i = threadIdx.x; i < p; i += BT) {
+        const double di = A[(int64_t)i * p + i];
+        int r = 0;
+        for (int j = 0; j < p; ++j) {
+            const double dj = A[(int64_t)j * p + j];
+            r += (dj > di) || (dj == di && j < i);
+        }
+        evals[b * p + r] = di;
+        rk[i] = r;
+    }
+    if (threadIdx.x == 0 && sweeps_out) sweeps_out[b] = sweeps[b];
+    if (!Vt_all) return;
+    __syncthreads();
+    const double* Vt = Vt_all + b * (int64_t)p * p;
+    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += BT) {
+        const int i = (int)(t / p), x = (int)(t % p);
+        const double v = Vt[t];
+        if (V32) V32[b * (int64_t)p * p + (int64_t)x * p + rk[i]] = (float)v;
+        if (V64) V64[b * (int64_t)p * p + (int64_t)x * p + rk[i]] = v;
+    }
+}
+
+}  // namespace
+
+size_t bj_workspace(int64_t p, int64_t batch) {
+    const int64_t nblk = ceil_div(p, NB) + (ceil_div(p, NB) & 1);
+    const int64_t npair = nblk / 2;
+    const int64_t nslots = npair + npair * (npair - 1);
+    size_t s = align_up((size_t)batch * p * p * sizeof(double), 256);           // Vt
+    s += align_up((size_t)batch * npair * D * D * sizeof(double), 256);           // V_P
+    s += align_up((size_t)batch * nslots * sizeof(double), 256);                  // off partials
+    s += align_up((size_t)batch * npair * sizeof(double), 256);                   // dg partials
+    s += align_up((size_t)batch * npair * sizeof(int), 256);                      // rotated
+    s += align_up((size_t)batch * sizeof(int), 256) * 2;                          // done, sweeps
+    s += align_up((size_t)batch * p * sizeof(int), 256);                          // ranks
+    return s;
+}
+
+// Block-Jacobi eigensolver (host loop; one stream synchronisation per sweep to read the
+// per-matrix convergence flags).
+int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
+            double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (ws_bytes < bj_workspace(p, batch)) return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
+    const int nblk = (int)(ceil_div(p, NB) + (ceil_div(p, NB) & 1));
+    const int npair = nblk / 2, noff = npair * (npair - 1), nslots = npair + noff;
+    const bool want_v = V32 || V64;
+    char* w = reinterpret_cast<char*>(ws);
+    auto take = [&](size_t bytes) { char* r = w; w += align_up(bytes, 256); return r; };
+    double* Vt = reinterpret_cast<double*>(take((size_t)batch * p * p * sizeof(double)));
+    double* Vs = reinterpret_cast<double*>(take((size_t)batch * npair * D * D * sizeof(double)));
+    double* poff = reinterpret_cast<double*>(take((size_t)batch * nslots * sizeof(double)));
+    double* pdg = reinterpret_cast<double*>(take((size_t)batch * npair * sizeof(double)));
+    int* rot = reinterpret_cast<int*>(take((size_t)batch * npair * sizeof(int)));
+    int* done = reinterpret_cast<int*>(take((size_t)batch * sizeof(int)));
+    int* sweeps = reinterpret_cast<int*>(take((size_t)batch * sizeof(int)));
+    int* ranks = reinterpret_cast<int*>(take((size_t)batch * p * sizeof(int)));
+    const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
+    bj_init_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
+    int* flags = new int[batch];
+    for (int sw = 0; sw < max_sweeps; ++sw) {
+        if (hipMemcpyAsync(flags, done, batch * sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            delete[] flags;
+            return check_launch("cq_jacobi_eigh (block Jacobi flags)");
+        }
+        bool all = true;
+        for (int64_t i = 0; i < batch && all; ++i) all = flags[i] != 0;
+        if (all) break;
+        for (int st = 0; st < nblk - 1; ++st) {
+            bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
+                                                                                   done, poff, pdg, nslots);
+            bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair : 0)), (unsigned)batch), BT, 0, s>>>(
+                A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
+        }
+        bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
+    }
+    delete[] flags;
+    bj_finish_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64, sweeps,
+                                                     sweeps_out, ranks);
+    return check_launch("cq_jacobi_eigh (block Jacobi)");
+}
+
+}  // namespace cq

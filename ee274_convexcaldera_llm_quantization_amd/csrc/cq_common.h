@@ -107,6 +107,12 @@ __device__ __forceinline__ float quant_code_r(float x, float s, float ys, float 
 }
 __device__ __forceinline__ float dequant_r(float c, float k, float yk, float s) { return div_rn(c, k, yk) * s; }
 
+// block-Jacobi eigensolver (cq_bjacobi.hip) behind cq_jacobi_eigh for p > kBlockJacobiMinP
+constexpr int64_t kBlockJacobiMinP = 192;
+size_t bj_workspace(int64_t p, int64_t batch);
+int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
+            double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s);
+
 }  // namespace cq
 
 #define CQ_REQUIRE(cond, ...)                                  \

@@ -133,6 +133,22 @@ __global__ __launch_bounds__(kThreads) void wsq_partial_kernel(const void* __res
     if (threadIdx.x == 0) part[b * gridDim.x + blockIdx.x] = s;
 }
 
+// out[b] = sum_i x[b][i] y[b][i] (fp32 or fp64 inputs, fp64 accumulation), per-block partials
+template <typename T>
+__global__ __launch_bounds__(kThreads) void dot_partial_kernel(const T* __restrict__ X, const T* __restrict__ Y,
+                                                                int64_t numel, double* part) {
+    __shared__ double lds[16];
+    const int64_t b = blockIdx.y;
+    const T* x = X + b * numel;
+    const T* y = Y + b * numel;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < numel; i += stride)
+        acc += (double)x[i] * (double)y[i];
+    const double s = block_sum_f64(acc, lds);
+    if (threadIdx.x == 0) part[b * gridDim.x + blockIdx.x] = s;
+}
+
 __global__ void sum_parts_kernel(const double* part, int nparts, double* out, int accumulate) {
     const int64_t b = blockIdx.x;
     if (threadIdx.x != 0) return;
@@ -490,6 +506,26 @@ int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel, co
     else wsq_partial_kernel<CQ_F32><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part);
     sum_parts_kernel<<<batch, 64, 0, s>>>(part, g, out, 0);
     return check_launch("cq_weighted_sqsum");
+}
+
+int cq_batched_dot(int dtype, const void* x, const void* y, int64_t batch, int64_t numel, double* out, void* ws,
+                   size_t ws_bytes, void* stream) {
+    CQ_REQUIRE(x && y && out && batch > 0 && numel > 0, "cq_batched_dot: bad args");
+    CQ_REQUIRE(dtype == CQ_F32 || dtype == CQ_F64, "cq_batched_dot: dtype must be CQ_F32 or CQ_F64");
+    const int g = grid_for(numel, batch);
+    if (ws_bytes < (size_t)batch * g * sizeof(double) || !ws)
+        return set_error(CQ_EWORKSPACE, "cq_batched_dot: workspace too small");
+    hipStream_t s = as_stream(stream);
+    double* part = reinterpret_cast<double*>(ws);
+    dim3 grid(g, batch);
+    if (dtype == CQ_F64)
+        dot_partial_kernel<double><<<grid, kThreads, 0, s>>>(reinterpret_cast<const double*>(x),
+                                                             reinterpret_cast<const double*>(y), numel, part);
+    else
+        dot_partial_kernel<float><<<grid, kThreads, 0, s>>>(reinterpret_cast<const float*>(x),
+                                                            reinterpret_cast<const float*>(y), numel, part);
+    sum_parts_kernel<<<batch, 64, 0, s>>>(part, g, out, 0);
+    return check_launch("cq_batched_dot");
 }
 
 size_t cq_quantize_workspace(int64_t batch, int64_t numel, int64_t block_size) {

@@ -1148,6 +1148,7 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
 }
 
 size_t cq_jacobi_workspace(int64_t p, int64_t batch) {
+    if (p > kBlockJacobiMinP) return cq::bj_workspace(p, batch);
     return (size_t)batch * p * p * sizeof(double);
 }
 
@@ -1162,6 +1163,8 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     hipStream_t s = as_stream(stream);
     double* Vt = reinterpret_cast<double*>(ws);
     const size_t l32 = jacobi_lds_bytes((int)p, 4), lreg = jacobi_reg_bytes((int)p);
+    if (p > kBlockJacobiMinP)  // A does not fit one CU's LDS: block Jacobi over many workgroups
+        return cq::bj_eigh(A, p, batch, max_sweeps, tol, evals, V32, V64, sweeps_out, ws, ws_bytes, s);
     if (p <= 192 && lreg <= 160 * 1024) {
         // fp64 A in LDS, V in registers (no per-round memory traffic for V)
         if (p <= 64)

@@ -239,6 +239,8 @@ class CalderaEngine:
         self.profile = profile
         self.timings = {}
         self.solver = None
+        self.lplr_fused_err = True   # LPLR error from the normal-equation pieces (False: error GEMM)
+        self.lplr_trace = None       # list -> per-LPLR-iteration errors are appended (diagnostics)
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
                 raise NotImplementedError(f"Quantization method '{meth}' not supported yet.")
@@ -432,7 +434,7 @@ class CalderaEngine:
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
                 K.scale_rc(V, trans=True, rowscale=sq, out=R)
         if quantized:
-            L, R = yield from self._lplr(st, Y, res, L, R, wts)
+            L, R = yield from self._lplr(st, Y, res, L, R, wts, ysq=ysq)
         st.L, st.R = L, R
         st.has_LR = True
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
@@ -469,43 +471,65 @@ class CalderaEngine:
         Wt32, _, info = K.spd_whiten(M64, rcond2=rc * rc)
         return Wt32, info
 
+    def _lplr_rw(self, R, wts: _Weights):
+        """R H_sqrt as the L step's lstsq operand (alg.py:163): R V diag(sqrt lam) for dense H,
+        R * sqrt(h) for diagonal H, R itself for H = I or non-data-aware (alg.py:167)."""
+        if self.p.activation_aware_LR and wts.dense:
+            return K.gemm(R, wts.Vs, C=torch.empty_like(R))  # R H_sqrt V
+        if self.p.activation_aware_LR and wts.ycol is not None:
+            return K.scale_rc(R, colscale=wts.ycol)
+        return R
+
+    def lplr_rhs(self, R, Ysrc, wts: _Weights, Bm):
+        """The L step's normal-equation pieces for the current R: Bm = Y Rw^T (m x r, fp32
+        GEMM, into Bm) and Mr = Rw Rw^T (r x r, fp64 Gram)."""
+        Rw = self._lplr_rw(R, wts)
+        K.gemm(Ysrc, Rw, tb=True, C=Bm)                    # m x r
+        return Bm, K.gram_f64(Rw, Rw, ta=True, tb=True)     # r x r
+
+    def lplr_L_from(self, Bm, Mr, n, L):
+        """L = Bm Mr^{-1} through the whitening Wr Wr^T = Mr^{-1} (rank-revealing at gelsy's
+        rcond for A = (R H_sqrt)^T, n x r).  Mr is overwritten."""
+        Wr, _ = self._solve_normal(Mr, n)
+        T1 = K.gemm(Bm, Wr, C=torch.empty_like(L))          # (Y Rw^T) Wr
+        K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
+        return L
+
     def lplr_L_step(self, R, Ysrc, wts: _Weights, L, tmp_mr=None):
         """L step of the LPLR loop (alg.py:162-169), before quantisation:
         L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T = (Y Rw^T)(Rw Rw^T)^{-1} with Rw = R H_sqrt
         (data-aware; Ysrc = Y = res H_sqrt) or Rw = R, Ysrc = res (alg.py:167).  Normal
         equations: fp64 Gram of Rw, rank-revealing SPD whitening at gelsy's rcond, fp32 GEMMs.
         R (B, r, n), Ysrc (B, m, n), L (B, m, r) output."""
-        n = R.shape[-1]
-        if self.p.activation_aware_LR and wts.dense:
-            Rw = K.gemm(R, wts.Vs, C=torch.empty_like(R))  # R H_sqrt V
-        else:
-            Rw = K.scale_rc(R, colscale=wts.ycol) if (self.p.activation_aware_LR and wts.ycol is not None) else R
-        if tmp_mr is None:
-            tmp_mr = torch.empty_like(L)
-        Bm = K.gemm(Ysrc, Rw, tb=True, C=tmp_mr)            # m x r
-        Mr = K.gram_f64(Rw, Rw, ta=True, tb=True)          # r x r
-        Wr, _ = self._solve_normal(Mr, n)  # A = (R H_sqrt)^T: n x r
-        T1 = K.gemm(Bm, Wr, C=torch.empty_like(tmp_mr))     # (Y Rw^T) Wr
-        K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
-        return L
+        Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty_like(L) if tmp_mr is None else tmp_mr)
+        return self.lplr_L_from(Bm, Mr, R.shape[-1], L)
 
-    def lplr_R_step(self, L, res, R, tmp_rn=None):
+    def lplr_R_step(self, L, res, R, tmp_rn=None, Ml=None):
         """R step of the LPLR loop (alg.py:175-177), before quantisation:
         R = lstsq(L, res) = (L^T L)^{-1} L^T res (unweighted, as the reference).
-        L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output."""
+        L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output.  Returns (R, L^T L)."""
         m = L.shape[1]
         if tmp_rn is None:
             tmp_rn = torch.empty_like(R)
-        Ml = K.gram_f64(L, L)                              # r x r
-        Wl, _ = self._solve_normal(Ml, m)  # A = L: m x r
+        if Ml is None:
+            Ml = K.gram_f64(L, L)                          # r x r
+        Wl, _ = self._solve_normal(Ml.clone(), m)  # A = L: m x r (the whitening overwrites its input)
         Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
         T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
         K.gemm(Wl, T2, C=R)
-        return R
+        return R, Ml
 
-    def _lplr(self, st, Y, res, L0, R0, wts: _Weights):
+    def _lplr(self, st, Y, res, L0, R0, wts: _Weights, ysq=None):
         """Quantised-factor LPLR loop, alg.py:144-195 (data-aware lstsq in normal-equation form
-        with fp64 Grams; quantise L^T and R as whole matrices, alg.py:171-180)."""
+        with fp64 Grams; quantise L^T and R as whole matrices, alg.py:171-180).
+
+        Data-aware with diagonal H (the callers' case, main.py:163-196): the iteration error
+        ||(res - L R) H_sqrt||^2 = ||Y - L Rw||^2 (alg.py:182) is assembled from pieces the
+        loop needs anyway -- ||Y||^2 - 2 <L, Y Rw^T> + <L^T L, Rw Rw^T>, where Y Rw^T and
+        Rw Rw^T of the new R are the next L step's normal equations and L^T L is the R step's
+        -- instead of a separate m x n x r error GEMM.  Best-iterate bookkeeping (strict <,
+        alg.py:184-188) stays on the device (no host sync per LPLR iteration) for uniform
+        quantisers."""
         p = self.p
         B, m, n = st.B, st.m, st.n
         r = R0.shape[1]
@@ -521,14 +545,17 @@ class CalderaEngine:
                     Rc=torch.zeros((B, r * n), dtype=K.code_dtype(p.R_bits), device=dev),
                     Ls=torch.zeros(B, device=dev), Rs=torch.zeros(B, device=dev))
         Ysrc = Y if aware else res
-        tmp_mr = torch.empty((B, m, r), dtype=torch.float32, device=dev)
+        fused_err = aware and not wts.dense and self.lplr_fused_err
         L = torch.empty((B, m, r), dtype=torch.float32, device=dev)
         tmp_rn = torch.empty((B, r, n), dtype=torch.float32, device=dev)
         Rn = torch.empty((B, r, n), dtype=torch.float32, device=dev)
         err = torch.empty(B, dtype=torch.float64, device=dev)
+        Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty((B, m, r), dtype=torch.float32, device=dev))
+        if fused_err and ysq is None:
+            ysq = K.weighted_sqsum(Ysrc, None, n)
         for _ in range(p.lplr_iters):
             # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T   (alg.py:162-169)
-            self.lplr_L_step(R, Ysrc, wts, L, tmp_mr)
+            self.lplr_L_from(Bm, Mr, n, L)
             # --- quantise L^T as one block (alg.py:171-172)
             if cb:
                 Lt = K.transpose_split(L, out=torch.empty((B, r, m), dtype=torch.float32, device=dev))[0]
@@ -539,20 +566,19 @@ class CalderaEngine:
                 qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
                 L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
-            self.lplr_R_step(L, res, Rn, tmp_rn)
+            _, Ml = self.lplr_R_step(L, res, Rn, tmp_rn)
             if cb:
                 itemsR, deqR = self._quantize_whole(Rn.view(B, r * n), p.method_LR, p.R_bits)
                 R = deqR.view(B, r, n)
             else:
                 qR = K.quantize_uniform(Rn.view(B, r * n), r * n, p.R_bits, codes=True, deq=True)
                 R = qR["deq"].view(B, r, n)
-            # --- error ||(res - L R) H_sqrt||_F  (alg.py:182)
-            if aware:
-                if wts.dense:
-                    Rw2 = K.gemm(R, wts.Vs, C=torch.empty_like(R))
-                else:
-                    Rw2 = K.scale_rc(R, colscale=wts.ycol) if wts.ycol is not None else R
-                K.gemm(L, Rw2, D=Y, epi=K.EPI_WERR, err_out=err)
+            # --- the next L step's normal equations; error ||(res - L R) H_sqrt||_F  (alg.py:182)
+            Bm, Mr = self.lplr_rhs(R, Ysrc, wts, Bm)
+            if fused_err:
+                err = (ysq - 2.0 * K.batched_dot(L, Bm) + K.batched_dot(Ml, Mr)).clamp_min(0.0)
+            elif aware:  # dense H (or the A/B switch lplr_fused_err off): the error GEMM
+                K.gemm(L, self._lplr_rw(R, wts), D=Y, epi=K.EPI_WERR, err_out=err)
             else:
                 if wts.dense:  # ||(res - L R) H||^2 with H_sqrt = H (alg.py:47-49, :182)
                     if resH is None:
@@ -561,21 +587,27 @@ class CalderaEngine:
                 else:
                     K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.lplr, err_out=err)
             e32 = torch.sqrt(err).float().double()  # torch.linalg.matrix_norm in fp32
-            better = e32 < best_err
+            if self.lplr_trace is not None:
+                self.lplr_trace.append(e32.clone())
+            better = e32 < best_err                  # strict <, NaN never better (alg.py:184)
+            if not cb:
+                # device-side selection: no host round trip per LPLR iteration
+                bm = better.view(B, 1)
+                best["L"] = torch.where(bm.view(B, 1, 1), L, best["L"])
+                best["R"] = torch.where(bm.view(B, 1, 1), R, best["R"])
+                best["Lc"] = torch.where(bm, qL["codes"].view(B, m, r).transpose(1, 2).reshape(B, m * r),
+                                         best["Lc"])  # L^T order
+                best["Rc"] = torch.where(bm, qR["codes"].view(B, r * n), best["Rc"])
+                best["Ls"] = torch.where(better, qL["scale"].view(B), best["Ls"])
+                best["Rs"] = torch.where(better, qR["scale"].view(B), best["Rs"])
+                best_err = torch.where(better, e32, best_err)
+                continue
             yield
-            better = better.tolist()
-            sel = [b for b in range(B) if better[b]]
+            sel = [b for b, ok in enumerate(better.tolist()) if ok]
             for b in sel:
                 best["L"][b].copy_(L[b])
                 best["R"][b].copy_(R[b])
-                if cb:
-                    best_items[b] = (itemsL[b], itemsR[b])
-                    best_err[b] = e32[b]
-                    continue
-                best["Lc"][b].copy_(qL["codes"][b].view(m, r).t().reshape(-1))  # L^T order
-                best["Rc"][b].copy_(qR["codes"][b])
-                best["Ls"][b] = qL["scale"][b, 0]
-                best["Rs"][b] = qR["scale"][b, 0]
+                best_items[b] = (itemsL[b], itemsR[b])
                 best_err[b] = e32[b]
         if cb:
             st.L_idxs = [it[0][0] if it else None for it in best_items]
@@ -595,9 +627,13 @@ class CalderaEngine:
         return run_to_end(self.run_iter(W, h, scale_W, use_tqdm))
 
     def run_iter(self, W: torch.Tensor, h: torch.Tensor | None = None, scale_W: bool = True,
-                 use_tqdm: bool = False):
+                 use_tqdm: bool = False, w_to_host: bool = False):
         """Generator form of run(): yields before each host synchronisation, so several
-        engines can be interleaved on their own streams (overlap.run_interleaved)."""
+        engines can be interleaved on their own streams (overlap.run_interleaved).
+
+        w_to_host: the results' "W" is a host copy of the scaled W (alg.py:81 keeps
+        best_decomp.W on the CPU), copied by a helper thread on a side stream while the
+        decomposition runs (the D2H transfer overlaps the kernels instead of following them)."""
         p = self.p
         if W.dim() == 2:
             W = W.unsqueeze(0)
@@ -616,6 +652,7 @@ class CalderaEngine:
             qlog.check_method_bits(p.method_LR, p.R_bits)
         gs, Ws = K.rms_scale(W, scale_W)  # on the true numel (alg.py:38-42)
         Ws_out = Ws
+        host_copy = self._start_host_copy(Ws) if w_to_host else None
         self._n_true = n
         if pad:
             # ragged n: zero columns up to a multiple of 4 (the kernels' vector width).  Zeros
@@ -692,6 +729,8 @@ class CalderaEngine:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         self._yh = self._yl = None
         self._yth = self._ytl = None
+        if host_copy is not None:
+            Ws_out = host_copy()  # joins the copy thread: the host tensor
         out = self._finalize(best, st, W, Ws_out, gs, errors, wts, spare=(work, res))
         if pad:
             out = [self._cut_columns(d, m, n, n_true) for d in out]
@@ -699,6 +738,37 @@ class CalderaEngine:
                 lp["R"] = lp["R"][:, :n_true]
                 lp["n_padded"] = n
         return out
+
+    @staticmethod
+    def _start_host_copy(Ws: torch.Tensor):
+        """Copy Ws (B, m, n) to a pageable host tensor on a side stream from a helper thread
+        (a pageable D2H copy blocks its calling thread, not the device); returns a join()
+        that yields the host tensor."""
+        import threading
+        dev = Ws.device
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
+        side = torch.cuda.Stream(dev)
+        host = torch.empty(Ws.shape, dtype=Ws.dtype)
+        err = []
+
+        def work():
+            try:
+                with torch.cuda.device(dev), torch.cuda.stream(side):
+                    side.wait_event(ready)
+                    host.copy_(Ws)
+            except BaseException as e:  # re-raised on join
+                err.append(e)
+
+        t = threading.Thread(target=work, daemon=True)
+        t.start()
+
+        def join():
+            t.join()
+            if err:
+                raise err[0]
+            return host
+        return join
 
     @staticmethod
     def _cut_columns(d, m, n_pad, n):

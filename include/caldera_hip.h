@@ -39,6 +39,7 @@ extern "C" {
 #define CQ_F32 0
 #define CQ_F16 1
 #define CQ_BF16 2
+#define CQ_F64 3
 
 int cq_abi_version(void);
 const char* cq_last_error(void);
@@ -340,6 +341,12 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
 int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel,
                       const float* w, int64_t ncols, double* out, void* ws, size_t ws_bytes,
                       void* stream);
+/* out[b] = sum_i x[b][i] * y[b][i], fp64 accumulation; dtype CQ_F32 | CQ_F64.  Workspace
+ * as cq_weighted_sqsum (cq_rms_scale_workspace(batch, numel)).  Replaces the separate
+ * m x n x r error GEMM of the LPLR loop (alg.py:182): with Y R^T and the r x r Grams
+ * already at hand, ||Y - L R||^2 = ||Y||^2 - 2 <L, Y R^T> + <L^T L, R R^T>. */
+int cq_batched_dot(int dtype, const void* x, const void* y, int64_t batch, int64_t numel, double* out,
+                   void* ws, size_t ws_bytes, void* stream);
 /* Y[b][i][j] = op(X[b])[i][j] * rowscale[b*rss + i] * colscale[b*css + j]
  * (op(X)[i][j] = X[i*ldx + j], or X[j*ldx + i] if trans_x; a NULL scale is 1;
  *  a stride of 0 shares the scale vector across the batch). rows x cols is op(X)'s shape. */

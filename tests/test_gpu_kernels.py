@@ -237,8 +237,8 @@ def test_ritz_residual(K):
     assert torch.allclose(out.double(), ref, rtol=1e-5)
 
 
-def test_jacobi_fp32_lds_path_p256(K):
-    """p = 256 runs the fp32-LDS Jacobi (not used by the solver for its final extraction):
+def test_jacobi_block_path_p256(K):
+    """p = 256 (> 192) runs the multi-workgroup block Jacobi (cq_bjacobi.hip, fp64):
     eigenvalues to ~1e-5 relative of ||T||, V orthogonal."""
     torch.manual_seed(9)
     p = 256
@@ -257,9 +257,9 @@ def test_jacobi_fp32_lds_path_p256(K):
 
 @pytest.mark.parametrize("near_diag", [False, True])
 def test_jacobi_global_path_p384(K, near_diag):
-    """p = 384 (rank-256 Rayleigh-Ritz, config 5) runs the global-memory threshold Jacobi:
-    pairs below tol / (2 sqrt p) of sqrt|a_ii a_jj| are skipped, which must not stop the
-    off-norm test from passing (cold and warm / near-diagonal matrices)."""
+    """p = 384 (rank-256 Rayleigh-Ritz, config 5) runs the block Jacobi over many workgroups
+    with threshold rotations: pairs below tol / (2 sqrt p) of sqrt|a_ii a_jj| are skipped,
+    which must not stop the off-norm test from passing (cold and warm / near-diagonal)."""
     torch.manual_seed(10)
     p = 384
     X = torch.randn(1, 2048, p, dtype=torch.float64)
@@ -283,6 +283,28 @@ def test_jacobi_global_path_p384(K, near_diag):
         # values only: the same rotations of A without the eigenvector updates
         ev2, V2, _, _ = K.jacobi_eigh(S.clone().to(DEV), tol=tol, want_vectors=False)
         assert V2 is None and torch.equal(ev2.cpu(), ev.cpu())
+
+
+@pytest.mark.parametrize("p", [200, 288, 300])
+def test_jacobi_block_path_ragged_batch(K, p):
+    """Block Jacobi on p not a multiple of its 32-wide blocks (a partial last block, an odd
+    block count rounded up with a virtual block; p = 288 is main.py's rank 200), in a batch
+    whose matrices converge after different sweep counts (cold, near-diagonal, diagonal)."""
+    torch.manual_seed(p)
+    X = torch.randn(3, 1024, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    _, U = torch.linalg.eigh(S[1])
+    Qp, _ = torch.linalg.qr(U + 1e-5 * torch.randn_like(U))
+    S[1] = 0.5 * ((Qp.T @ S[1] @ Qp) + (Qp.T @ S[1] @ Qp).T)
+    S[2] = torch.diag(torch.rand(p, dtype=torch.float64) + 0.5)
+    ref = torch.linalg.eigvalsh(S).flip(-1)
+    ev, V32, V64, sw = K.jacobi_eigh(S.clone().to(DEV), tol=1e-12, want64=True)
+    assert int(sw[2]) == 0 and int(sw[1]) <= int(sw[0]) < 30
+    assert ((ev.cpu() - ref).abs() / ref[:, 0:1]).max().item() < 1e-12
+    V = V64.cpu()
+    assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 1e-12
+    res = S @ V - V * ev.cpu().unsqueeze(1)
+    assert res.abs().max().item() < 1e-10 * ref.max().item()
 
 
 @pytest.mark.parametrize("p", [64, 128, 180, 192])
