@@ -119,6 +119,7 @@ _SIGS = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_ritz_product_error": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_batched_dot": (c_int, [c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_act_sqsum_workspace": (c_size, [c_i64, c_i64]),
     "cq_act_sqsum_cols": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp, c_size, c_vp]),
@@ -503,6 +504,18 @@ def ritz_residual(X, Z, theta, r):
     ws = workspace(lib.cq_ritz_workspace(k, r, B), X.device)
     _check(lib.cq_ritz_residual(_p(X), _p(Z), _p(theta), k, p, r, B, _p(out), _p(ws), ws.numel(),
                                 _stream(X.device)), "cq_ritz_residual")
+    return out
+
+
+def ritz_product_error(X, Z, theta, r, ysq):
+    """Per-matrix estimate of the relative error of the rank-r projection (cq_ritz_product_error)."""
+    _require_hip(X, Z, theta, ysq)
+    B, k, p = X.shape
+    out = torch.empty(B, dtype=torch.float32, device=X.device)
+    lib = load()
+    ws = workspace(lib.cq_ritz_workspace(k, r, B), X.device)
+    _check(lib.cq_ritz_product_error(_p(X), _p(Z), _p(theta), k, p, r, B, _p(ysq), _p(out), _p(ws), ws.numel(),
+                                     _stream(X.device)), "cq_ritz_product_error")
     return out
 
 

@@ -1084,6 +1084,34 @@ __global__ void ritz_final_kernel(const double* part, int nchunks, int64_t p, in
     }
 }
 
+// Product-error estimate of the rank-r projection from the Ritz pairs (see cq_ritz_product_error):
+// vector i's residual e_i tilts it toward eigenvectors outside the block by ~||e_i|| / gap_i
+// (gap_i = theta_i - theta_{p-1}, the block's smallest Ritz value bounding the unconverged
+// complement), which moves the projection of Y by that angle times sigma_i = sqrt(theta_i).
+__global__ void ritz_prod_final_kernel(const double* part, int nchunks, int64_t p, int64_t r,
+                                       const double* theta, const double* ysq, float* out) {
+    __shared__ double red[16];
+    const int64_t b = blockIdx.x;
+    const double t0 = fabs(theta[b * p]), tp = theta[b * p + p - 1];
+    double acc = 0.0;
+    for (int64_t c = threadIdx.x; c < r; c += blockDim.x) {
+        double s = 0.0;
+        for (int t = 0; t < nchunks; ++t) s += part[(b * nchunks + t) * r + c];
+        const double th = fmax(theta[b * p + c], 0.0);
+        const double gap = fmax(th - tp, 1e-3 * t0);
+        acc += s * th / (gap * gap);
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[i];
+        const double y2 = ysq[b];
+        out[b] = (float)(y2 > 0 ? sqrt(a / y2) : sqrt(a));
+    }
+}
+
 }  // namespace cq
 
 using namespace cq;
@@ -1202,6 +1230,21 @@ int cq_ritz_residual(const float* X, const float* Z, const double* theta, int64_
     ritz_partial_kernel<<<dim3((unsigned)nch, (unsigned)batch), 256, 0, s>>>(X, Z, theta, k, p, r, rows_per, part);
     ritz_final_kernel<<<(unsigned)batch, 256, 0, s>>>(part, (int)nch, p, r, theta, out);
     return check_launch("cq_ritz_residual");
+}
+
+int cq_ritz_product_error(const float* X, const float* Z, const double* theta, int64_t k, int64_t p, int64_t r,
+                          int64_t batch, const double* ysq, float* out, void* ws, size_t ws_bytes, void* stream) {
+    CQ_REQUIRE(X && Z && theta && ysq && out && k > 0 && p > 0 && r > 0 && r < p,
+               "cq_ritz_product_error: bad args");
+    if (!ws || ws_bytes < cq_ritz_workspace(k, r, batch))
+        return set_error(CQ_EWORKSPACE, "cq_ritz_product_error: workspace too small");
+    hipStream_t s = as_stream(stream);
+    const int64_t nch = std::min<int64_t>(64, std::max<int64_t>(1, k / 64));
+    const int64_t rows_per = ceil_div(k, nch);
+    double* part = reinterpret_cast<double*>(ws);
+    ritz_partial_kernel<<<dim3((unsigned)nch, (unsigned)batch), 256, 0, s>>>(X, Z, theta, k, p, r, rows_per, part);
+    ritz_prod_final_kernel<<<(unsigned)batch, 256, 0, s>>>(part, (int)nch, p, r, theta, ysq, out);
+    return check_launch("cq_ritz_product_error");
 }
 
 }  // extern "C"

@@ -127,11 +127,17 @@ FILTER_MAX_AMP = 2.0e5  # bound on T_d(t0): config 2's degree-12 steps (T_12(1.6
 MAX_OUTER = 40  # outer iterations per solve (the schedule's last degree repeats until converged)
 
 
+JACOBI_MAX_SWEEPS = 30
+STALL_RATIO = 0.85
+
+
 class SolverStats:
     def __init__(self):
         self.outer = 0
         self.matvecs = 0
         self.x3_fallbacks = 0
+        self.jacobi_unconverged = 0  # Rayleigh-Ritz eigensolves that used all JACOBI_MAX_SWEEPS
+        self.stalls = 0              # calls ended at the products' precision floor
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
@@ -139,6 +145,7 @@ class SolverStats:
 
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
+                    jacobi_unconverged=self.jacobi_unconverged, stalls=self.stalls,
                     max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks)
 
 
@@ -149,7 +156,7 @@ class RankRSolver:
                  tol: float = 1e-5, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 7, 6, 6, 6, 6),
                  seed: int = 0x5EED, jacobi_tol: float = 1e-7, filter_precision: str = "f16x3",
                  cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool = False,
-                 jacobi_tol_values: float = 1e-2):
+                 jacobi_tol_values: float = 1e-2, criterion: str = "product"):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -165,6 +172,9 @@ class RankRSolver:
         self.direct = p >= self.k or self.k <= 256  # small problem: Jacobi on the full Gram
         self.p = self.k if self.direct else p
         self.tol = tol
+        if criterion not in ("product", "theta0"):
+            raise ValueError(f"criterion must be 'product' or 'theta0', got {criterion!r}")
+        self.criterion = criterion
         self.deg_cold, self.deg_warm = tuple(deg_cold), tuple(deg_warm)
         self.device = device
         self.seed = seed
@@ -290,9 +300,12 @@ class RankRSolver:
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps
-            theta, _, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol_values, want_vectors=False)
+            theta, _, _, sw = K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=self.jacobi_tol_values,
+                                            want_vectors=False)
+            self._last_sw = sw
             return theta, X, None
-        theta, V32, _, _ = K.jacobi_eigh(T, tol=self.jacobi_tol)
+        theta, V32, _, sw = K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=self.jacobi_tol)
+        self._last_sw = sw
         Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
         Zo = self._free(X, Z, Xo, *keep)
@@ -441,6 +454,7 @@ class RankRSolver:
             self._y_halves = (yh, yl, ys)
             if ysq is None:
                 ysq = K.weighted_sqsum(Y, None, Y.shape[2])
+            self._ysq = ysq
             K.gemm_x3(yh, yl, yh, yl, yinv, None, tri=True, a_blocked=True, b_blocked=True,
                       out_h=self._Gh, out_l=self._Gl, out_scale=X3_SCALE, sym_bound=ysq,
                       scale_out=self._gscale, inv_out=self._ginv)
@@ -448,6 +462,8 @@ class RankRSolver:
         elif not self.x3:
             self._fill_G(Y)  # Y Y^T (upper tiles + mirror) or Y^T Y
         self._active.fill_(1)
+        if not g_split:
+            self._ysq = K.weighted_sqsum(Y, None, Y.shape[2])  # trace(G) for the product-error test
         if self.x3:
             if not g_split:
                 if self._G is None:
@@ -513,13 +529,24 @@ class RankRSolver:
                 Xb, _ = self._cholqr(Xa, X)
                 theta_n, Xn, Zn = self._rr(Xb, X, single=cheap, values_only=cheap)
                 # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
-                res = (K.ritz_residual(Xn, Zn, theta_n, self.r).double() if not cheap
-                       else torch.full((B,), math.inf, dtype=torch.float64, device=dev))
+                # stopping test: estimated relative error of the rank-r projection of Y (a
+                # residual relative to theta_0 over-converges flat spectra and under-converges
+                # activation-weighted ones); "theta0": the max Ritz residual / theta_0
+                if cheap:
+                    res = torch.full((B,), math.inf, dtype=torch.float64, device=dev)
+                elif self.criterion == "product" and self.r < p:
+                    res = K.ritz_product_error(Xn, Zn, theta_n, self.r, self._ysq).double()
+                else:
+                    res = K.ritz_residual(Xn, Zn, theta_n, self.r).double()
                 ovf = (self._ovf.max().double() if self.x3 and self._x3f
                        else torch.zeros((), dtype=torch.float64, device=dev))
-                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res])
+                # matrices whose Jacobi ran out of sweeps (read back with the residuals)
+                unconv = (self._last_sw >= JACOBI_MAX_SWEEPS).sum().double().view(1)
+                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res, unconv])
                 yield
                 chk = chk.cpu().numpy()
+                self.stats.jacobi_unconverged += int(chk[-1])
+                chk = chk[:-1]
                 if self.x3 and self._x3f and chk[0] != 0:
                     # an fp16 half overflowed (a Ritz value far below the true top of the
                     # spectrum, cold start): redo this outer iteration with the fp32 filter
@@ -544,6 +571,12 @@ class RankRSolver:
             self.stats.resid_hist.append(mr)
             used.append(d)
             if mr <= self.tol:
+                break
+            # precision floor (split-fp16 products: ~2e-7 theta_0): a test that has stopped
+            # improving over two outer iterations ends the call instead of running to MAX_OUTER
+            fin = [v for v in self.stats.resid_hist if math.isfinite(v)]
+            if len(fin) >= 3 and fin[-1] > STALL_RATIO * min(fin[-3], fin[-2]):
+                self.stats.stalls += 1
                 break
         if Z is None:  # left the loop on a values-only iteration (MAX_OUTER): rotate once
             theta, X, Z = self._rr(X)

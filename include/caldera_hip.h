@@ -227,6 +227,15 @@ size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch);
 int cq_ritz_residual(const float* X, const float* Z, const double* theta, int64_t k,
                      int64_t p, int64_t r, int64_t batch, float* out, void* ws,
                      size_t ws_bytes, void* stream);
+/* The rank-r solver's stopping test (replaces the full SVD's exactness, alg.py:217): an
+ * estimate of ||(P_r - P_r*) Y||_F / ||Y||_F, the relative error of the rank-r projection of
+ * Y from the Ritz pairs:  out[b] = sqrt(sum_{i<r} ||e_i||^2 theta_i / gap_i^2 / ysq[b]),
+ * e_i = Z[:,i] - theta_i X[:,i], gap_i = max(theta_i - theta_{p-1}, 1e-3 theta_0), ysq[b] =
+ * ||Y||_F^2 = trace(G).  Spectra with a wide spread (activation-weighted Y) need much smaller
+ * residuals than flat ones for the same product accuracy; a residual relative to theta_0
+ * cannot tell them apart.  r < p.  Workspace: cq_ritz_workspace. */
+int cq_ritz_product_error(const float* X, const float* Z, const double* theta, int64_t k, int64_t p, int64_t r,
+                          int64_t batch, const double* ysq, float* out, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Split-fp16 ("f16x3") products with a symmetric Gram, fp32-grade accuracy on the fp16

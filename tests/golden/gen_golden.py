@@ -21,7 +21,10 @@ Fixtures:
   sum_large.npz   configs 2, 3, 5 at full size: hashes, scalars, error lists and
                   float64 sketches (Q+LR)@Omega and (L1 R1)@Omega of the first LR step.
 
-Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [lplr] [seeds] [large]
+  main_caller.npz the primary caller's configuration (main.py:163-196): rank 200, L/R 16,
+                  scale_W=False, real layer-20 diag Hessians, 896x4864 / 4864x896 / 896x896.
+
+Usage:  python tests/golden/gen_golden.py [kat] [cfg1] [nb] [trace] [lplr] [seeds] [main] [tall] [large]
 """
 import hashlib
 import json
@@ -314,13 +317,13 @@ def gen_lplr(alg, q, CalderaParams, tag="lplr_mid", m=768, n=1280, rank=64, lplr
 
 
 # ---------------------------------------------------------------------------
-def run_large(alg, q, CalderaParams, tag, m, n, H, seed=0, **kw):
+def run_large(alg, q, CalderaParams, tag, m, n, H, seed=0, scale_W=True, **kw):
     torch.manual_seed(seed)
     W = (torch.randn(m, n) * 0.02).to(torch.float16)
     p = _params(CalderaParams, q, **kw)
     t = time.time()
     with Tracer(alg) as tr:
-        d = alg.caldera(p, W, H, device="cpu", use_tqdm=False)
+        d = alg.caldera(p, W, H, device="cpu", use_tqdm=False, scale_W=scale_W)
     el = time.time() - t
     om = sketch_omega(n)
     o = {}
@@ -365,6 +368,37 @@ def gen_large(alg, q, CalderaParams, which=("cfg2", "cfg5", "cfg3")):
     np.savez_compressed(path, **o)
 
 
+MAIN_LAYERS = (("main_down", "language_model.model.layers.20.mlp.down_proj", 896, 4864, 11),
+               ("main_up", "language_model.model.layers.20.mlp.up_proj", 4864, 896, 12),
+               ("main_o", "language_model.model.layers.20.self_attn.o_proj", 896, 896, 13))
+
+
+def gen_main(alg, q, CalderaParams):
+    """The primary caller's real configuration (main.py:163-196): rank 200, L/R 16, Q 2,
+    iters 5, scale_W=False, H = diag_embed(Hall[name]) with the REAL diag_Hessians.pt entries
+    of layer 20 (down_proj's h spans 2.7e-5 .. 24.6), on synthetic fp16 weights of the
+    layers' shapes (the model's weights are not in the reference)."""
+    path = os.path.join(OUT, "main_caller.npz")
+    Hall = torch.load(HESS, weights_only=True)
+    o = {}
+    for tag, name, m, n, seed in MAIN_LAYERS:
+        h = Hall[name].to(torch.float32)
+        o[tag + "_h"] = h.numpy()
+        o[tag + "_name"] = np.array(name)
+        o.update(run_large(alg, q, CalderaParams, tag, m, n, torch.diag_embed(h), seed=seed, scale_W=False,
+                           Q_bits=2, L_bits=16, R_bits=16, rank=200, iters=5, lplr_iters=5))
+    np.savez_compressed(path, **o)
+
+
+def gen_tall(alg, q, CalderaParams):
+    """Config 4's tall gate/up projection shape 11008 x 4096 (H = I, r 128, Q2, iters 5)."""
+    path = os.path.join(OUT, "sum_large.npz")
+    o = dict(np.load(path))
+    o.update(run_large(alg, q, CalderaParams, "cfg4t", 11008, 4096, None, seed=4,
+                       Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5))
+    np.savez_compressed(path, **o)
+
+
 def gen_seeds(alg, q, CalderaParams, seeds=(1, 2, 3)):
     """Config 2 on the bench's other seeds (bench.py synth_batch: seed i -> matrix i): the
     Q+LR sketch, norm and error lists the bench and the B = 256 batch test pin."""
@@ -380,7 +414,7 @@ def gen_seeds(alg, q, CalderaParams, seeds=(1, 2, 3)):
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "lplr", "large", "seeds"]
+    what = sys.argv[1:] or ["kat", "cfg1", "nb", "trace", "lplr", "large", "seeds", "main", "tall"]
     alg, q, CP = _import_ref()
     cwd = os.getcwd()
     os.chdir(tempfile.mkdtemp())  # bbint appends outlier_log.csv to CWD (quantization.py:126-136)
@@ -397,6 +431,10 @@ if __name__ == "__main__":
             gen_lplr(alg, q, CP)
         if "seeds" in what:
             gen_seeds(alg, q, CP)
+        if "main" in what:
+            gen_main(alg, q, CP)
+        if "tall" in what:
+            gen_tall(alg, q, CP)
         large = [w for w in what if w in ("cfg2", "cfg3", "cfg5")]
         if "large" in what:
             large = ["cfg2", "cfg5", "cfg3"]
