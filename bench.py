@@ -4,7 +4,7 @@
 H = I) on MI355X.  One "step" = one batched pass of the hot path (caldera() of
 alg.py:24-112) over B matrices resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload cfg2|cfg3|cfg5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload cfg2|cfg3|cfg5|model]
                   [--no-cpu-baseline] [--no-parity] [--no-api-path]
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank decomposes
@@ -21,7 +21,10 @@ extra step of the same batch.
 
 Workloads (BASELINE.json configs): cfg2 (default, the headline metric) 4096x4096, r 128, Q2,
 L/R 16, iters 5, H = I; cfg3 4096x11008, diag H (the golden fixture's resampled
-diag_Hessians.pt entry), r 128, Q2, L/R 16; cfg5 4096x4096, r 256, Q2, L/R 4, lplr 10.
+diag_Hessians.pt entry), r 128, Q2, L/R 16; cfg5 4096x4096, r 256, Q2, L/R 4, lplr 10;
+model = BASELINE configs[3]: all 224 Llama-2-7B linear weights sharded round-robin over the
+ranks (same-shape batches interleaved on HIP streams), packed on the device and gathered to
+rank 0 over RCCL -- strong scaling (the model is fixed), timed end to end including the gather.
 """
 import argparse
 import json
@@ -134,19 +137,112 @@ def cpu_baseline(name, wl, dec0):
     return cpu, par
 
 
+def run_model(args):
+    """BASELINE configs[3]: the 224 Llama-2-7B linear weights (random-init fp16, one device RNG
+    seed per matrix, resident in HBM before the timed region), rank i % world decomposing
+    matrix i (sharding.decompose_sharded: same-shape batches of <= 16 interleaved on their own
+    HIP streams), results packed in HBM and gathered to rank 0 over RCCL.  One step = the
+    whole model."""
+    from ee274_convexcaldera_llm_quantization_amd import sharding as S
+    from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
+    from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    K.load()
+    wl = WORKLOADS["cfg2"]
+    qp = make_params(wl)
+    items = S.llama2_7b_matrices(32)
+    mine = [items[i] for i in S.shard_indices(len(items), world, rank)]
+    Wd = {}
+    for name, m, n, seed in mine:
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        Wd[name] = (torch.randn(m, n, generator=g, device=dev) * 0.02).to(torch.float16)
+    ep = EngineParams.from_caldera_params(qp)
+
+    def run_all(batches):
+        # up to 4 shape batches interleaved on their own HIP streams at a time (a rank's share
+        # at 8 GPUs is 3 batches; the whole model on one GPU is 14, whose scratch would not fit)
+        res = []
+        for g0 in range(0, len(batches), 4):
+            grp = batches[g0:g0 + 4]
+            engines = [CalderaEngine(ep) for _ in grp]
+            run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)], dev)
+            res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"], d["R"],
+                                   d["global_scale"], d["errors"])
+                    for b, e in zip(grp, engines) for (name, m, n, _), d in zip(b, e.last_packed)]
+        return res
+
+    def decompose(batch_items):
+        return run_all([batch_items])
+    decompose.run_all = run_all
+
+    def step():
+        return S.decompose_sharded(items, decompose, rank=rank, world=world, max_batch=16, device=dev)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = None
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        assert out is not None and [r.name for r in out] == [it[0] for it in items], "gather incomplete"
+        result = {
+            "metric": "weight matrices/sec (Llama-2-7B linear weights, rank-128, Q=2-bit, whole model)",
+            "value": len(items) * args.steps / el, "unit": "matrices/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32 (fp16 W in; fp32-grade split-fp16 MFMA products, fp64 small solves; int2 codes)",
+            "data": "synthetic: 224 random-init fp16 Llama-2-7B-shaped weights (randn*0.02, device RNG per seed)",
+            "config": {"workload": "BASELINE configs[3]: 224 Llama-2-7B linear weights (32 x q,k,v,o 4096x4096, "
+                                   "gate,up 11008x4096, down 4096x11008), r 128, Q2, L/R 16, iters 5, H = I; "
+                                   "round-robin matrix sharding, RCCL gather of the packed (Q, L, R) to rank 0",
+                       "name": "model", "matrices_per_step": len(items), "matrices_on_rank0": len(mine),
+                       "parallelism": f"dp{world} (matrix-sharded)"},
+            "gathered_bytes": int(sum(r.codes.numel() * r.codes.element_size() + r.L.numel() * 4 + r.R.numel() * 4
+                                      for r in out)),
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=None, help="matrices per GPU (default: per workload)")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS) + ["model"], default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-api-path", action="store_true")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     args = ap.parse_args()
+    if args.workload == "model":
+        return run_model(args)
     wl = WORKLOADS[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
