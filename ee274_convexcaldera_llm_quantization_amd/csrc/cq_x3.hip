@@ -1676,6 +1676,276 @@ __global__ __launch_bounds__(256) void transpose_split_kernel(const float* __res
     }
 }
 
+
+// ------------------------------------------------------------------ row-panel fused Q update
+// Same two passes and per-element arithmetic as q_update_v_kernel (res = W - L R on
+// split-fp16 MFMAs, absmax pass, quantise pass), organised for K = r <= 256: a workgroup owns
+// a panel of QP_WAVES * 16 * RB rows of W and walks its columns in chunks of 32.  Each wave
+// keeps its L rows' fragments (hi and lo, all of K) in VGPRs for the whole panel, so L is
+// read once per panel; the chunk's R^T rows are staged once per workgroup in LDS by LDS-DMA
+// (double buffer) and shared by every wave.  Per output element the load path then carries
+// 2 B of W plus 512 B / (rows per panel) of R^T halves (1 B at 512 rows) instead of ~4 B of
+// operand tiles with the 192 x 384 tiles.  Transposed MFMA (A = R^T, B = L) with the R^T rows
+// of a chunk permuted so each lane owns 8 consecutive columns of one W row: 16-byte fp16 W
+// loads, one 16-bit store of 8 two-bit codes.
+constexpr int QP_WAVES = 8;               // default waves per workgroup (template parameter NW)
+constexpr int QP_BN = 32;                 // columns per chunk (two 16-column MFMA blocks)
+constexpr int QP_KMAX = 256;              // largest r
+constexpr int QP_ROW = QP_KMAX;           // LDS row of one R^T column (halves, 512 B)
+constexpr int QP_STAGE = 2 * QP_BN * QP_ROW;  // halves per stage (hi rows, then lo rows)
+
+// 16-B chunk swizzle of an LDS row: the 16 rows one MFMA fragment read touches (rows
+// 8 a + b + 4 c, a, b < 4) land on 16 different chunk positions mod 16 (bank-conflict free)
+__device__ __forceinline__ int qp_swz(int row) { return (row & 3) | (((row >> 3) & 3) << 2); }
+
+// LDS-DMA of chunk n0's R^T rows (both halves) into a stage: 32 wave-instructions of 2 rows
+// x 512 B, 32 / NW per wave; lane slot (lane & 31) holds logical chunk slot ^ swz(row)
+template <int NW>
+__device__ __forceinline__ void qp_issue_r(const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl,
+                                           int64_t n0, int K, _Float16* stage, int wid, int lane) {
+#pragma unroll
+    for (int u = 0; u < 32 / NW; ++u) {
+        const int I = wid * (32 / NW) + u;         // 0..31
+        const int half = I >> 4, row = 2 * (I & 15) + (lane >> 5);
+        const int logical = (lane & 31) ^ qp_swz(row);
+        const int kc = 8 * logical < K ? 8 * logical : 0;   // past K: any valid address (unused)
+        const uint16_t* src = (half ? Rl : Rh) + (n0 + row) * (int64_t)K + kc;
+        _Float16* dst = stage + (half * QP_BN + 2 * (I & 15)) * QP_ROW;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ f16x8g qp_frag(const _Float16* stage, int half, int row, int chunk) {
+    return *reinterpret_cast<const f16x8g*>(stage + (half * QP_BN + row) * QP_ROW + 8 * (chunk ^ qp_swz(row)));
+}
+
+// RB row-blocks of 16 rows per wave; K = r <= 32 KSMAX.  FAST (pass 1): the scale is a
+// finite normal number and |res| <= scale, so x / s and c / k take the branch-free correctly
+// rounded division (div_fast; same results as IEEE division), and 2-bit dequantisation is
+// c * s (k = 1: (c / 1) * s is exactly c * s).
+template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, int NW>
+__device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
+                                        const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl, int K,
+                                        int panels, _Float16* smem) {
+    constexpr int ROWS = NW * 16 * RB;
+    constexpr int WV = DT == CQ_F16 ? 1 : 2;        // uint4 per lane-run of 8 W elements
+    const int64_t m = q.m, n = q.n, MN = m * n;
+    // XCD-aware order: the panels of one matrix run on one XCD (R^T chunks shared in its L2)
+    const int64_t total = (int64_t)panels * q.x.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
+    const int64_t b = lin / panels, panel = lin % panels;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int KS = K / 32;
+    const uint16_t* Lhb = Lh + b * m * (int64_t)K;
+    const uint16_t* Llb = Ll + b * m * (int64_t)K;
+    const uint16_t* Rhb = Rh + b * n * (int64_t)K;
+    const uint16_t* Rlb = Rl + b * n * (int64_t)K;
+    const int64_t row0 = panel * ROWS + wid * 16 * RB;   // this wave's first W row
+
+    // this wave's L fragments: row block rb, K step ks, lane (l16 row, lq chunk)
+    f16x8g lh[RB][KSMAX], ll[RB][KSMAX];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        const int64_t row = row0 + 16 * rb + l16;
+#pragma unroll
+        for (int ks = 0; ks < KSMAX; ++ks) {
+            if (ks < KS && row < m) {
+                const int64_t o = row * K + 32 * ks + 8 * lq;
+                lh[rb][ks] = *reinterpret_cast<const f16x8g*>(Lhb + o);
+                ll[rb][ks] = *reinterpret_cast<const f16x8g*>(Llb + o);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) { lh[rb][ks][e] = (_Float16)0.f; ll[rb][ks][e] = (_Float16)0.f; }
+            }
+        }
+    }
+    const float sc = q.x.inv_scale[b];
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN;
+    const float* Wf = reinterpret_cast<const float*>(q.W) + b * MN;
+    constexpr float kq = (float)((1 << (BITS - 1)) - 1);
+    float s = 0.f;
+    if (PASS == 1) s = quant_scale(q.absmax[b], q.eps);
+    const float ys = 1.f / s, yk = 1.f / kq;
+    uint32_t mx = 0;
+    double err = 0.0;
+    // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
+    // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
+    const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
+    const int64_t nchunks = n / QP_BN;
+    uint4 wr[RB][WV], wn[RB][WV];
+    auto load_w = [&](int64_t n0, uint4 (&dst)[RB][WV]) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int64_t row = row0 + 16 * rb + l16;
+            const int64_t e = (row < m ? row : m - 1) * n + n0 + 8 * lq;
+            if (DT == CQ_F16) {
+                dst[rb][0] = *reinterpret_cast<const uint4*>(Wh + e);
+            } else {
+                dst[rb][0] = *reinterpret_cast<const uint4*>(Wf + e);
+                dst[rb][WV - 1] = *reinterpret_cast<const uint4*>(Wf + e + 4);
+            }
+        }
+    };
+    qp_issue_r<NW>(Rhb, Rlb, 0, K, smem, wid, lane);
+    load_w(0, wr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t ch = 0; ch < nchunks; ++ch) {
+        const int64_t n0 = ch * QP_BN;
+        if (ch + 1 < nchunks) {  // next chunk's R^T (LDS-DMA) and W in flight during this chunk
+            qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
+            load_w(n0 + QP_BN, wn);
+        }
+        const _Float16* st = smem + (ch & 1) * QP_STAGE;
+        f32x4v acc[RB][2];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) acc[rb][c] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KSMAX; ++ks) {
+            if (ks < KS) {
+                f16x8g ah[2], al[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    ah[c] = qp_frag(st, 0, acol0 + 4 * c, 4 * ks + lq);
+                    al[c] = qp_frag(st, 1, acol0 + 4 * c, 4 * ks + lq);
+                }
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
+                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[c], ll[rb][ks], acc[rb][c], 0, 0, 0);
+                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
+                    }
+            }
+        }
+        // epilogue: acc[rb][c][i] is (W row row0 + 16 rb + l16, column n0 + 8 lq + 4 c + i)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int64_t row = row0 + 16 * rb + l16;
+            if (row >= m) continue;
+            const int64_t e = row * n + n0 + 8 * lq;
+            float v[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int u = 4 * c + i;
+                    float w;
+                    if (DT == CQ_F16) {
+                        const uint32_t pr = (&wr[rb][0].x)[u >> 1];
+                        w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
+                    } else {
+                        w = __uint_as_float((&wr[rb][(u >> 2) & (WV - 1)].x)[u & 3]);
+                    }
+                    v[u] = w - acc[rb][c][i] * sc;   // res = W - L R (alg.py:262)
+                }
+            if (PASS == 0) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) mx = max(mx, abs_bits(v[u]));
+                continue;
+            }
+            int cq8[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float e4[4];
+                float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
+                if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + n0 + 8 * lq + 4 * h);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float x = v[4 * h + i];
+                    float c, dq;
+                    if (FAST) {
+                        c = rintf(div_fast(x, s, ys) * kq);
+                        dq = BITS == 2 ? c * s : div_fast(c, kq, yk) * s;
+                    } else {
+                        c = quant_code_r(x, s, ys, kq);
+                        dq = dequant_r(c, kq, yk, s);
+                    }
+                    const float d = dq - x;
+                    e4[i] = (d * d) * (&wv.x)[i];
+                    cq8[4 * h + i] = (int)c;
+                }
+                err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
+            }
+            if (BITS == 2 && q.packed) {  // bytes: codes 0-3, 4-7, MSB-first offset binary (c + 1)
+                uint32_t w16 = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    w16 |= (((uint32_t)(cq8[4 * h] + 1) << 6) | ((uint32_t)(cq8[4 * h + 1] + 1) << 4) |
+                            ((uint32_t)(cq8[4 * h + 2] + 1) << 2) | (uint32_t)(cq8[4 * h + 3] + 1)) << (8 * h);
+                *reinterpret_cast<uint16_t*>(q.packed + (b * MN + e) / 4) = (uint16_t)w16;
+            } else if (BITS == 4 && q.packed) {
+                uint32_t w32 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    w32 |= (((uint32_t)(cq8[2 * j] + 7) << 4) | (uint32_t)(cq8[2 * j + 1] + 7)) << (8 * j);
+                *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 2) = w32;
+            }
+            if (q.codes) {
+                if (BITS <= 8) {
+                    uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        c0 |= (uint32_t)(uint8_t)(int8_t)cq8[j] << (8 * j);
+                        c1 |= (uint32_t)(uint8_t)(int8_t)cq8[4 + j] << (8 * j);
+                    }
+                    *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) = make_uint2(c0, c1);
+                } else {
+                    int16_t* cp = reinterpret_cast<int16_t*>(q.codes) + b * MN + e;
+                    *reinterpret_cast<short4*>(cp) = make_short4((short)cq8[0], (short)cq8[1], (short)cq8[2], (short)cq8[3]);
+                    *reinterpret_cast<short4*>(cp + 4) = make_short4((short)cq8[4], (short)cq8[5], (short)cq8[6], (short)cq8[7]);
+                }
+            }
+        }
+        if (ch + 1 < nchunks) {
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int w = 0; w < WV; ++w) wr[rb][w] = wn[rb][w];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
+    }
+    if (PASS == 0) {
+        mx = wave_max_u32(mx);
+        if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
+    } else if (q.part) {
+        __shared__ double red[16];
+        const double tsum = block_sum_f64(err, red);
+        if (tid == 0) q.part[b * panels + panel] = tsum;
+    }
+}
+
+template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uint16_t* __restrict__ Lh,
+                                                                   const uint16_t* __restrict__ Ll,
+                                                                   const uint16_t* __restrict__ Rh,
+                                                                   const uint16_t* __restrict__ Rl, int K,
+                                                                   int panels) {
+    extern __shared__ __attribute__((aligned(16))) char qp_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(qp_smem_raw);
+    if (PASS == 0) {
+        qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+        return;
+    }
+    // which matrix this workgroup serves (same mapping as qp_body) decides the division path
+    const int64_t total = (int64_t)panels * q.x.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
+    const float sb = quant_scale(q.absmax[lin / panels], q.eps);
+    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    else qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+}
+constexpr size_t QP_LDS_BYTES = (size_t)2 * QP_STAGE * sizeof(_Float16);  // 64 KB
+
 }  // namespace cq
 
 using namespace cq;
@@ -1815,6 +2085,42 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
         return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
     }
     const unsigned grid = (unsigned)(tiles * batch);
+    // row-panel kernel (q_update_p_kernel): K <= 256, m % 16 == 0, n % 32 == 0, 16-B aligned
+    static const char* qu_env = getenv("CQ_QU_KERNEL");
+    const bool pk = r > 0 && r <= QP_KMAX && m % 16 == 0 && n % QP_BN == 0 && vk && al16(Lh) && al16(Ll) &&
+                    al16(Rth) && al16(Rtl) && !(qu_env && qu_env[0] == 'v');
+    if (pk && !known) {
+        // pass 0 (absmax) and pass 1 (quantise + packing, more live values) may use different
+        // panel geometries: every 16 x 16 output block runs the same MFMA sequence whatever
+        // the geometry, so both passes see identical res.  8 waves; 4 (pass 0) / 3 (pass 1)
+        // row blocks per wave for K <= 128 and fp16 W (VGPR budget), 2 otherwise.
+        const bool f16 = dtype == CQ_F16;
+        const bool small = r <= 128;
+        const int rb0 = (small && f16) ? 4 : 2, rb1 = (small && f16) ? 3 : 2;
+        const int64_t p0 = ceil_div(m, (int64_t)QP_WAVES * 16 * rb0), p1 = ceil_div(m, (int64_t)QP_WAVES * 16 * rb1);
+        CQ_REQUIRE(p0 * batch < (1ll << 31), "cq_q_update_x3: grid too large");
+        q.x.batch = batch;
+        const uint16_t *lh = Lh, *ll = Ll, *rh = Rth, *rl = Rtl;
+        const int Ki = (int)r;
+        const unsigned g0 = (unsigned)(p0 * batch), g1 = (unsigned)(p1 * batch);
+#define CQ_QP(PS, B, DTV, RBV, KSV, G, P) \
+        q_update_p_kernel<PS, B, DTV, RBV, KSV, QP_WAVES><<<G, QP_WAVES * 64, QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)P)
+#define CQ_QP_B(B) do { \
+            if (f16 && small) { CQ_QP(0, B, CQ_F16, 4, 4, g0, p0); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
+            else if (f16) { CQ_QP(0, B, CQ_F16, 2, 8, g0, p0); CQ_QP(1, B, CQ_F16, 2, 8, g1, p1); } \
+            else if (small) { CQ_QP(0, B, CQ_F32, 2, 4, g0, p0); CQ_QP(1, B, CQ_F32, 2, 4, g1, p1); } \
+            else { CQ_QP(0, B, CQ_F32, 2, 8, g0, p0); CQ_QP(1, B, CQ_F32, 2, 8, g1, p1); } } while (0)
+        switch (bits) {
+            case 2: CQ_QP_B(2); break;
+            case 4: CQ_QP_B(4); break;
+            case 8: CQ_QP_B(8); break;
+            default: CQ_QP_B(16); break;
+        }
+#undef CQ_QP_B
+#undef CQ_QP
+        q_update_finalize_kernel<<<(unsigned)batch, 64, 0, s>>>(q.absmax, q.part, p1, batch, eps, scale_out, err_out);
+        return check_launch("cq_q_update_x3");
+    }
     if (known && vk) {  // r = 0 with max|W| known: one streaming pass over W
         const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(tiles, ceil_div(m * n / 16, 256)));
         CQ_REQUIRE(batch < 65536, "cq_q_update_x3: batch too large");

@@ -534,28 +534,43 @@ def _near_tie(x64, scale64, bits, tol=1e-4):
     return (torch.abs(torch.abs(s - torch.floor(s)) - 0.5) < tol)
 
 
-def test_q_update_x3_with_lr_matches_fp64_residual(K):
-    """r = 64: codes of res = W - L R equal those of the exact (fp64) residual everywhere
-    except where the exact value lies within 1e-4 code units of a rounding boundary; scale
-    to fp32 rounding; error to 1e-4 relative."""
-    g = torch.Generator(device=DEV).manual_seed(3)
-    B, m, n, r = 2, 300, 520, 64
-    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.02).half()
+@pytest.mark.parametrize("m,n,r,bits,dt", [
+    (300, 520, 64, 2, torch.float16),    # m % 16 != 0: the 192 x 384 tile kernel
+    (320, 544, 96, 2, torch.float16),    # row-panel kernel: partial panel, K = 96 (3 of 4 MFMA steps)
+    (640, 1024, 128, 4, torch.float16),  # row-panel kernel, 4-bit packing
+    (336, 512, 256, 2, torch.float16),   # row-panel kernel, K = 256 (2 row blocks per wave)
+    (320, 544, 64, 8, torch.float32),    # fp32 W, int8 codes
+    (320, 544, 128, 16, torch.float32),  # fp32 W, int16 codes
+])
+def test_q_update_x3_with_lr_matches_fp64_residual(K, m, n, r, bits, dt):
+    """Codes of res = W - L R equal those of the exact (fp64) residual everywhere except where
+    the exact value lies within 1e-4 code units of a rounding boundary; scale to fp32
+    rounding; the weighted error to 1e-4 relative."""
+    g = torch.Generator(device=DEV).manual_seed(3 + m + r)
+    B = 2
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.02).to(dt)
     L = torch.linalg.qr(torch.randn(B, m, r, device=DEV, generator=g))[0].contiguous()
     R = (torch.randn(B, r, n, device=DEV, generator=g) * 0.01).contiguous()
-    packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=DEV)
+    packed = torch.empty(B, m * n * bits // 8, dtype=torch.uint8, device=DEV) if bits <= 4 else None
+    codes = torch.empty(B, m * n, dtype=K.code_dtype(bits), device=DEV)
     scale = torch.empty(B, device=DEV)
     err = torch.empty(B, dtype=torch.float64, device=DEV)
     w = torch.rand(n, device=DEV, generator=g) + 0.5
-    K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_w=w, err_out=err)
+    K.q_update_x3(W, L, R, bits, packed=packed, codes=codes, scale=scale, err_w=w, err_out=err)
     res = W.double() - L.double() @ R.double()
     s64 = res.abs().amax((1, 2))
     assert torch.allclose(scale.double(), s64, rtol=1e-6, atol=0)
-    c = K.unpack_codes(packed, m * n, 2).view(B, m, n).double()
-    c_ref = torch.round(res / s64.view(B, 1, 1))
+    k = float(2 ** (bits - 1) - 1)
+    c = codes.view(B, m, n).double()
+    if packed is not None:
+        assert torch.equal(K.unpack_codes(packed, m * n, bits).view(B, m, n).double(), c)
+    c_ref = torch.round(res / s64.view(B, 1, 1) * k)
     flips = c != c_ref
-    assert not (flips & ~_near_tie(res, s64.view(B, 1, 1), 2)).any()
-    deq = c * scale.double().view(B, 1, 1)
+    # near-tie width in code units: 1e-4, or an fp32-grade residual's ~4e-6 relative error
+    # expressed in code units at high bit widths (k = 32767 at 16 bits)
+    tol = max(1e-4, 4e-6 * k)
+    assert not (flips & ~_near_tie(res, s64.view(B, 1, 1), bits, tol)).any(), int(flips.sum())
+    deq = c / k * scale.double().view(B, 1, 1)
     e_ref = (((deq - res) ** 2) * w.double()).sum((1, 2))
     assert torch.allclose(err, e_ref, rtol=1e-4, atol=0)
 
