@@ -287,6 +287,7 @@ def main():
     # time the dominant kernel (the G X filter GEMMs) with HIP events on its stream
     solver.EVENT_PROBE.enable(True)
     solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * max(1, args.streams or 1))
+    solver.LPLR_PROBE.enable(wl["L_bits"] < 16, max_pairs=64)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -308,6 +309,8 @@ def main():
     probe = solver.EVENT_PROBE.summary()
     qprobe = solver.QUANT_PROBE.summary()
     solver.QUANT_PROBE.enable(False)
+    lprobe = solver.LPLR_PROBE.summary()
+    solver.LPLR_PROBE.enable(False)
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -374,6 +377,23 @@ def main():
                        else "q_update_v_kernel<0|1, bits> (cq_q_update_x3)")}
     if qroof:
         result["roofline_quantise"] = qroof
+    if lprobe:
+        # the quantised-factor LPLR loop's m x n x r products (alg.py:162-177): split-fp16
+        # (3 fp16 MFMA products per fp32-grade product) when Y is unweighted, else fp32 MFMA GEMMs.
+        # achieved_tflops counts the algorithmic 2 m n r; frac_mfma prices the MFMA work actually
+        # issued against its own dense peak (3 x fp16 products vs the fp16 peak for the split path)
+        lx3 = eng.lplr_x3 and not wl["H"]
+        result["roofline_lplr"] = {}
+        for kind, g in lprobe.items():
+            ach = g["flops_per_launch"] / (g["avg_ms"] * 1e-3) / 1e12
+            result["roofline_lplr"][kind] = {
+                "bound": "mfma", "achieved_tflops": ach,
+                "peak_tflops": PEAK_F16_MFMA_TFLOPS / 3 if lx3 else PEAK_FP32_MFMA_TFLOPS,
+                "frac_mfma": ach / (PEAK_F16_MFMA_TFLOPS / 3 if lx3 else PEAK_FP32_MFMA_TFLOPS),
+                "frac_of_fp32_peak": ach / PEAK_FP32_MFMA_TFLOPS,
+                "launches_timed": g["count"], "avg_call_ms": g["avg_ms"], "flops_per_call": g["flops_per_launch"],
+                "kernel": ("x3 split-fp16 kernel (cq_gemm_x3, 3 x v_mfma_f32_16x16x32_f16)" if lx3
+                           else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")}
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
     result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0)}

@@ -27,7 +27,7 @@ from . import _lib as K
 from . import qlog
 from .overlap import run_to_end
 from . import scratch
-from .solver import QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
+from .solver import LPLR_PROBE, QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
 
 
 @dataclass
@@ -243,6 +243,7 @@ class CalderaEngine:
         self.timings = {}
         self.solver = None
         self.lplr_fused_err = True   # LPLR error from the normal-equation pieces (False: error GEMM)
+        self.lplr_x3 = True          # LPLR m x n x r products on split-fp16 MFMAs where the halves exist
         self.lplr_trace = None       # list -> per-LPLR-iteration errors are appended (diagnostics)
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
@@ -341,6 +342,12 @@ class CalderaEngine:
         dev = Ws.device
         quantized = p.L_bits < 16 or p.R_bits < 16
         weighted = p.activation_aware_LR and (wts.ycol is not None or wts.dense)
+        if self._w_finite is None:  # once per run (one small read-back)
+            self._w_finite = bool(torch.isfinite(self._wmax).all().item())
+        if not self._w_finite:
+            # the reference's LR_init SVD (alg.py:217 / :232) raises on a non-finite residual
+            raise torch.linalg.LinAlgError("linalg.svd: The algorithm failed to converge because the input "
+                                           "matrix contained non-finite values.")
         if self.solver is None and p.rand_svd:  # torch.svd_lowrank branch (alg.py:213-216, :228-231)
             self.solver = RandSVD(B, m, n, p.rank, dev)
         if self.solver is None:
@@ -356,6 +363,7 @@ class CalderaEngine:
         sv = self.solver
         y_split = None
         ysq = None
+        lplr_halves = None
         if st.dense_q and st.has_Q:
             qsrc, qsc, qbits = st.Qd, st.Qbound, 32
         else:
@@ -379,7 +387,10 @@ class CalderaEngine:
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
             halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)
             x3_r = sv.left and not quantized and p.activation_aware_LR
-            if x3_r:
+            # quantised factors with unweighted Y (= res): the LPLR loop's m x n x r products run
+            # on split-fp16 MFMAs from these halves (Y for Y R^T, res^T = Y^T for L^T res)
+            x3_lplr = sv.left and quantized and not weighted and self.lplr_x3
+            if x3_r or x3_lplr:
                 if self._yth is None:
                     self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
                     self._ytl = scratch.get("lr.ytl", (B, n, m), torch.float16, dev)
@@ -389,6 +400,8 @@ class CalderaEngine:
                              res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
                              scale=self._ys, sq=ysq, **halves)
             y_split = (self._yh, self._yl, self._ys, ysq)
+            if x3_lplr:
+                lplr_halves = dict(yh=self._yh, yl=self._yl, ys=self._ys, yth=self._yth, ytl=self._ytl)
         else:
             K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
@@ -442,7 +455,7 @@ class CalderaEngine:
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
                 K.scale_rc(V, trans=True, rowscale=sq, out=R)
         if quantized:
-            L, R = yield from self._lplr(st, Y, res, L, R, wts, ysq=ysq)
+            L, R = yield from self._lplr(st, Y, res, L, R, wts, ysq=ysq, halves=lplr_halves)
         st.L, st.R = L, R
         st.has_LR = True
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
@@ -488,11 +501,26 @@ class CalderaEngine:
             return K.scale_rc(R, colscale=wts.ycol)
         return R
 
-    def lplr_rhs(self, R, Ysrc, wts: _Weights, Bm):
-        """The L step's normal-equation pieces for the current R: Bm = Y Rw^T (m x r, fp32
-        GEMM, into Bm) and Mr = Rw Rw^T (r x r, fp64 Gram)."""
+    def lplr_rhs(self, R, Ysrc, wts: _Weights, Bm, halves=None):
+        """The L step's normal-equation pieces for the current R: Bm = Y Rw^T (m x r, into Bm)
+        and Mr = Rw Rw^T (r x r, fp64 Gram).  halves (unweighted Y): Y's K-blocked split-fp16
+        halves from cq_residual_split; the product then runs on split-fp16 MFMAs (fp32-grade,
+        3 fp16 products) instead of the fp32 MFMA GEMM."""
         Rw = self._lplr_rw(R, wts)
-        K.gemm(Ysrc, Rw, tb=True, C=Bm)                    # m x r
+        B_, m, n = Ysrc.shape
+        r = R.shape[1]
+        ev = LPLR_PROBE.start("Y_Rw^T", 2.0 * B_ * m * n * r, 4.0 * B_ * (m * n + n * r + m * r))
+        if ev is not None:
+            ev[0].record()
+        if halves is not None:
+            sR = K.pow2_scale(Rw, 14)
+            rh, rl = K.split_f16(Rw, sR, hi=halves["rwh"], lo=halves["rwl"], blocked=True)
+            K.gemm_x3(halves["yh"], halves["yl"], rh, rl, 1.0 / (halves["ys"] * sR), Bm, a_blocked=True,
+                      b_blocked=True)
+        else:
+            K.gemm(Ysrc, Rw, tb=True, C=Bm)                # m x r
+        if ev is not None:
+            ev[1].record()
         return Bm, K.gram_f64(Rw, Rw, ta=True, tb=True)     # r x r
 
     def lplr_L_from(self, Bm, Mr, n, L):
@@ -512,7 +540,7 @@ class CalderaEngine:
         Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty_like(L) if tmp_mr is None else tmp_mr)
         return self.lplr_L_from(Bm, Mr, R.shape[-1], L)
 
-    def lplr_R_step(self, L, res, R, tmp_rn=None, Ml=None):
+    def lplr_R_step(self, L, res, R, tmp_rn=None, Ml=None, halves=None):
         """R step of the LPLR loop (alg.py:175-177), before quantisation:
         R = lstsq(L, res) = (L^T L)^{-1} L^T res (unweighted, as the reference).
         L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output.  Returns (R, L^T L)."""
@@ -522,12 +550,26 @@ class CalderaEngine:
         if Ml is None:
             Ml = K.gram_f64(L, L)                          # r x r
         Wl, _ = self._solve_normal(Ml.clone(), m)  # A = L: m x r (the whitening overwrites its input)
-        Ct = K.gemm(L, res, ta=True, C=tmp_rn)             # r x n
+        B_, _, n = res.shape
+        r = L.shape[2]
+        ev = LPLR_PROBE.start("L^T_res", 2.0 * B_ * m * n * r, 4.0 * B_ * (m * n + n * r + m * r))
+        if ev is not None:
+            ev[0].record()
+        if halves is not None:  # L^T res on split-fp16 MFMAs: A = L^T halves, B = res^T halves
+            sL = K.pow2_scale(L, 14)
+            K.transpose_split(L, hi=halves["lth"], lo=halves["ltl"], scale=sL, blocked=True)
+            K.gemm_x3(halves["lth"], halves["ltl"], halves["yth"], halves["ytl"], 1.0 / (sL * halves["ys"]),
+                      tmp_rn, a_blocked=True, b_blocked=True)
+            Ct = tmp_rn
+        else:
+            Ct = K.gemm(L, res, ta=True, C=tmp_rn)         # r x n
+        if ev is not None:
+            ev[1].record()
         T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
         K.gemm(Wl, T2, C=R)
         return R, Ml
 
-    def _lplr(self, st, Y, res, L0, R0, wts: _Weights, ysq=None):
+    def _lplr(self, st, Y, res, L0, R0, wts: _Weights, ysq=None, halves=None):
         """Quantised-factor LPLR loop, alg.py:144-195 (data-aware lstsq in normal-equation form
         with fp64 Grams; quantise L^T and R as whole matrices, alg.py:171-180).
 
@@ -558,7 +600,13 @@ class CalderaEngine:
         tmp_rn = torch.empty((B, r, n), dtype=torch.float32, device=dev)
         Rn = torch.empty((B, r, n), dtype=torch.float32, device=dev)
         err = torch.empty(B, dtype=torch.float64, device=dev)
-        Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty((B, m, r), dtype=torch.float32, device=dev))
+        if halves is not None:
+            f16 = torch.float16
+            halves = dict(halves, rwh=torch.empty((B, r, n), dtype=f16, device=dev),
+                          rwl=torch.empty((B, r, n), dtype=f16, device=dev),
+                          lth=torch.empty((B, r, m), dtype=f16, device=dev),
+                          ltl=torch.empty((B, r, m), dtype=f16, device=dev))
+        Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty((B, m, r), dtype=torch.float32, device=dev), halves)
         if fused_err and ysq is None:
             ysq = K.weighted_sqsum(Ysrc, None, n)
         for _ in range(p.lplr_iters):
@@ -574,7 +622,7 @@ class CalderaEngine:
                 qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
                 L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
-            _, Ml = self.lplr_R_step(L, res, Rn, tmp_rn)
+            _, Ml = self.lplr_R_step(L, res, Rn, tmp_rn, halves=halves)
             if cb:
                 itemsR, deqR = self._quantize_whole(Rn.view(B, r * n), p.method_LR, p.R_bits)
                 R = deqR.view(B, r, n)
@@ -582,7 +630,7 @@ class CalderaEngine:
                 qR = K.quantize_uniform(Rn.view(B, r * n), r * n, p.R_bits, codes=True, deq=True)
                 R = qR["deq"].view(B, r, n)
             # --- the next L step's normal equations; error ||(res - L R) H_sqrt||_F  (alg.py:182)
-            Bm, Mr = self.lplr_rhs(R, Ysrc, wts, Bm)
+            Bm, Mr = self.lplr_rhs(R, Ysrc, wts, Bm, halves)
             if fused_err:
                 err = (ysq - 2.0 * K.batched_dot(L, Bm) + K.batched_dot(Ml, Mr)).clamp_min(0.0)
             elif aware:  # dense H (or the A/B switch lplr_fused_err off): the error GEMM
@@ -676,6 +724,7 @@ class CalderaEngine:
                 h = torch.cat([h, h.max().expand(pad)])
         wts = _Weights(h, n, p, dev)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
+        self._w_finite = None
         self._yh = self._yl = self._ys = None
         self._yth = self._ytl = None
         if wts.dense:  # den = tr(W H W^T) (alg.py:298)

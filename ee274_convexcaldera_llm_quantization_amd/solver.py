@@ -120,6 +120,7 @@ class _GroupProbe:
 
 
 QUANT_PROBE = _GroupProbe()
+LPLR_PROBE = _GroupProbe()  # the LPLR loop's m x n x r GEMMs (alg.py:162-177), bench roofline_lplr
 
 
 X3_SCALE = 2.0 ** 6  # power-of-two scale of the filter iterates' fp16 halves (entries <= ~1)

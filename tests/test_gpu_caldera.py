@@ -284,3 +284,20 @@ def test_update_orders_and_flags_vs_oracle(api, order, aware, cq, clr):
     exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
     den = max(np.linalg.norm(exp), 1e-30)
     assert np.linalg.norm(out - exp) / den < 1e-4
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_non_finite_weight_raises_like_reference(api, bad):
+    """A NaN / Inf weight: the reference's first LR_init SVD raises torch.linalg.LinAlgError
+    ("... contained non-finite values", alg.py:217); the drop-in raises the same error at the
+    same point instead of iterating on NaNs.  A Q-only run (no SVD) returns, as the
+    reference's does."""
+    caldera, CP, _ = api
+    torch.manual_seed(0)
+    W = (torch.randn(64, 128) * 0.02).half()
+    W[3, 5] = bad
+    with pytest.raises(torch.linalg.LinAlgError, match="non-finite"):
+        caldera(CP(Q_bits=2, L_bits=16, R_bits=16, rank=8, iters=2, update_order=["Q", "LR"], sigma_reg=1e-8),
+                W.to(DEV), None, device=DEV, use_tqdm=False)
+    d = caldera(CP(Q_bits=2, rank=8, iters=1, update_order=["Q"]), W.to(DEV), None, device=DEV, use_tqdm=False)
+    assert not math.isfinite(d.errors["Q"][0])
