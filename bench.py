@@ -49,7 +49,7 @@ WORKLOADS = {
                  batch=96, desc="BASELINE configs[2]: 4096x11008 fp16, activation-aware diag H (resampled "
                                 "diag_Hessians.pt down_proj entry), rank 128, Q_bits 2, L/R_bits 16, iters 5"),
     "cfg5": dict(m=4096, n=4096, Q_bits=2, L_bits=4, R_bits=4, rank=256, iters=5, lplr_iters=10, H=False,
-                 batch=64, desc="BASELINE configs[4]: 4096x4096 fp16, rank 256, Q_bits 2, L/R_bits 4, "
+                 batch=256, desc="BASELINE configs[4]: 4096x4096 fp16, rank 256, Q_bits 2, L/R_bits 4, "
                                 "lplr_iters 10, iters 5, H = I"),
 }
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak

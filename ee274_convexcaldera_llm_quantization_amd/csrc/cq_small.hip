@@ -98,9 +98,12 @@ __global__ void gram_reduce_kernel(const double* __restrict__ part, int64_t MN, 
 // accumulation: the same arithmetic contract as gram_f64_kernel).  64 x 64 tile per
 // workgroup, 4 waves of 32 x 32 (2 x 2 blocks), GK-deep LDS slices filled by float4 loads
 // with a one-slice register prefetch.  sym (A == B): tiles below the block diagonal are
-// skipped and mirrored by the reduction.
+// skipped and mirrored by the reduction.  TK: both operands transposed (C = A B^T with A: M x K,
+// B: N x K row-major, K contiguous -- the LPLR loop's R H_sqrt (R H_sqrt)^T): float4 loads run
+// along K and are transposed into the same LDS slice layout.
 using f64x4v = __attribute__((ext_vector_type(4))) double;
 
+template <bool TK>
 __global__ __launch_bounds__(kGramThreads) void gram_f64_mfma_kernel(
     int64_t M, int64_t N, int64_t K, int64_t kchunk, int splits, const float* __restrict__ A,
     int64_t lda, int64_t sa, const float* __restrict__ B, int64_t ldb, int64_t sb, int sym,
@@ -117,6 +120,8 @@ __global__ __launch_bounds__(kGramThreads) void gram_f64_mfma_kernel(
     const int wi = wid >> 1, wj = wid & 1;  // wave block: rows 32 wi, cols 32 wj
     // slice loader: GK rows x 64 columns of A and of B, 2 float4 per thread each
     const int lr = t >> 4, lc = (t & 15) * 4;  // rows lr and lr + 16, columns lc .. lc+3
+    // TK: 64 operand rows x GK along K, 2 float4 per thread each: rows tr and tr + 32, K tk .. tk+3
+    const int tr = t >> 3, tk = (t & 7) * 4;
     const int64_t kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
     auto ld4 = [&](const float* base, int64_t ld, int64_t lim, int64_t k, int64_t c0) -> float4 {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -137,18 +142,45 @@ __global__ __launch_bounds__(kGramThreads) void gram_f64_mfma_kernel(
 #pragma unroll
         for (int v = 0; v < 2; ++v) acc[u][v] = f64x4v{0.0, 0.0, 0.0, 0.0};
     float4 ra[2], rb[2];
+    // TK loads: row `row` of a K-contiguous operand, K elements k .. k+3 (zero past kend / lim)
+    auto ld4t = [&](const float* base, int64_t ld, int64_t lim, int64_t row, int64_t k) -> float4 {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < lim && k < kend) {
+            const float* src = base + row * ld + k;
+            if (k + 3 < kend) v = *reinterpret_cast<const float4*>(src);
+            else {
+                v.x = src[0];
+                if (k + 1 < kend) v.y = src[1];
+                if (k + 2 < kend) v.z = src[2];
+            }
+        }
+        return v;
+    };
     auto fetch = [&](int64_t k0) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            ra[h] = ld4(Ab, lda, M, k0 + lr + 16 * h, i0 + lc);
-            rb[h] = ld4(Bb, ldb, N, k0 + lr + 16 * h, j0 + lc);
+            if constexpr (TK) {
+                ra[h] = ld4t(Ab, lda, M, i0 + tr + 32 * h, k0 + tk);
+                rb[h] = ld4t(Bb, ldb, N, j0 + tr + 32 * h, k0 + tk);
+            } else {
+                ra[h] = ld4(Ab, lda, M, k0 + lr + 16 * h, i0 + lc);
+                rb[h] = ld4(Bb, ldb, N, k0 + lr + 16 * h, j0 + lc);
+            }
         }
     };
     auto stash = [&](int buf) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            *reinterpret_cast<float4*>(&As[buf][lr + 16 * h][lc]) = ra[h];
-            *reinterpret_cast<float4*>(&Bs[buf][lr + 16 * h][lc]) = rb[h];
+            if constexpr (TK) {
+                const int c = tr + 32 * h;
+                As[buf][tk + 0][c] = ra[h].x; As[buf][tk + 1][c] = ra[h].y;
+                As[buf][tk + 2][c] = ra[h].z; As[buf][tk + 3][c] = ra[h].w;
+                Bs[buf][tk + 0][c] = rb[h].x; Bs[buf][tk + 1][c] = rb[h].y;
+                Bs[buf][tk + 2][c] = rb[h].z; Bs[buf][tk + 3][c] = rb[h].w;
+            } else {
+                *reinterpret_cast<float4*>(&As[buf][lr + 16 * h][lc]) = ra[h];
+                *reinterpret_cast<float4*>(&Bs[buf][lr + 16 * h][lc]) = rb[h];
+            }
         }
     };
     const int nsl = (int)ceil_div(kend - kbeg, GK);
@@ -1135,10 +1167,16 @@ int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, 
     dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT), (unsigned)(batch * splits));
     const int64_t tot = batch * M * N;
     const unsigned rgrid = (unsigned)std::min<int64_t>(ceil_div(tot, 256), 4096);
-    if (!trans_a && !trans_b && lda % 4 == 0 && ldb % 4 == 0 && stride_a % 4 == 0 && stride_b % 4 == 0) {
+    const bool al4 = lda % 4 == 0 && ldb % 4 == 0 && stride_a % 4 == 0 && stride_b % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0;
+    if (al4 && trans_a == trans_b) {
         const int sym = (A == B && lda == ldb && stride_a == stride_b && M == N) ? 1 : 0;
-        gram_f64_mfma_kernel<<<grid, kGramThreads, 0, s>>>(M, N, K, kchunk, splits, A, lda, stride_a, B, ldb,
-                                                           stride_b, sym, reinterpret_cast<double*>(ws));
+        if (trans_a)
+            gram_f64_mfma_kernel<true><<<grid, kGramThreads, 0, s>>>(M, N, K, kchunk, splits, A, lda, stride_a, B,
+                                                                     ldb, stride_b, sym, reinterpret_cast<double*>(ws));
+        else
+            gram_f64_mfma_kernel<false><<<grid, kGramThreads, 0, s>>>(M, N, K, kchunk, splits, A, lda, stride_a, B,
+                                                                      ldb, stride_b, sym, reinterpret_cast<double*>(ws));
         if (sym)
             gram_reduce_sym_kernel<<<rgrid, 256, 0, s>>>(reinterpret_cast<double*>(ws), M, splits, batch, C);
         else

@@ -454,10 +454,18 @@ class CalderaEngine:
                 K.gemm(Ysrc, V, C=L)
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
                 K.scale_rc(V, trans=True, rowscale=sq, out=R)
+        self._lplr_err2 = None
         if quantized:
             L, R = yield from self._lplr(st, Y, res, L, R, wts, ysq=ysq, halves=lplr_halves)
         st.L, st.R = L, R
         st.has_LR = True
+        if self._lplr_err2 is not None and wts.identity and wts.err_unit:
+            # H = I: the activation-aware numerator ||res - L R||^2 (alg.py:286-302) of the kept
+            # iterate is the LPLR loop's own fused error of that iterate (alg.py:182) -- no
+            # separate m x n x r error GEMM.  Small errors (cancellation in ||Y||^2 - 2<L, Y R^T>
+            # + <L^T L, R R^T>) are recomputed directly by run_iter, as for the Pythagorean form.
+            self._pyth = True
+            return self._lplr_err2
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
         if wts.dense:
             return self._state_error(st, Ws, res, wts)
@@ -609,6 +617,8 @@ class CalderaEngine:
         Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty((B, m, r), dtype=torch.float32, device=dev), halves)
         if fused_err and ysq is None:
             ysq = K.weighted_sqsum(Ysrc, None, n)
+        # fp64 fused error of the kept iterate; L = R = 0 (nothing kept) leaves ||Y||^2
+        best_err2 = ysq.clone() if fused_err and not cb else None
         for _ in range(p.lplr_iters):
             # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T   (alg.py:162-169)
             self.lplr_L_from(Bm, Mr, n, L)
@@ -643,6 +653,8 @@ class CalderaEngine:
                 else:
                     K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.lplr, err_out=err)
             e32 = torch.sqrt(err).float().double()  # torch.linalg.matrix_norm in fp32
+            if fused_err and not cb:
+                best_err2 = torch.where(e32 < best_err, err, best_err2)
             if self.lplr_trace is not None:
                 self.lplr_trace.append(e32.clone())
             better = e32 < best_err                  # strict <, NaN never better (alg.py:184)
@@ -673,6 +685,7 @@ class CalderaEngine:
         else:
             st.L_idxs, st.R_idxs = best["Lc"], best["Rc"]
             st.L_scale, st.R_scale = best["Ls"], best["Rs"]
+        self._lplr_err2 = best_err2
         return best["L"], best["R"]
 
     # ------------------------------------------------------------------ driver

@@ -167,15 +167,19 @@ def test_gram_f64(K, ta, tb):
     assert (C.cpu() - ref).abs().max().item() < 1e-9
 
 
-@pytest.mark.parametrize("M,N,Kd,sym", [(192, 192, 4096, True), (130, 96, 1000, False), (190, 190, 333, True)])
-def test_gram_f64_mfma_paths(K, M, N, Kd, sym):
-    """Non-transposed Grams (fp64 MFMA path; symmetric X^T X skips and mirrors lower tiles)."""
+@pytest.mark.parametrize("tk", [False, True])
+@pytest.mark.parametrize("M,N,Kd,sym", [(192, 192, 4096, True), (130, 96, 1000, False), (190, 190, 333, True),
+                                        (256, 256, 4096, True), (64, 200, 1004, False)])
+def test_gram_f64_mfma_paths(K, M, N, Kd, sym, tk):
+    """Grams on the fp64 MFMA path, both operand orientations (tk: C = A B^T with K contiguous,
+    the LPLR loop's R R^T); symmetric Grams skip and mirror the lower tiles.  Ragged K (not a
+    multiple of the 32-deep slice or of 4) included."""
     g = torch.Generator().manual_seed(M + Kd)
-    A = torch.randn(3, Kd, M, generator=g)
-    Bm = A if sym else torch.randn(3, Kd, N, generator=g)
+    A = torch.randn(3, M, Kd, generator=g) if tk else torch.randn(3, Kd, M, generator=g)
+    Bm = A if sym else (torch.randn(3, N, Kd, generator=g) if tk else torch.randn(3, Kd, N, generator=g))
     Ad = A.to(DEV)
-    C = K.gram_f64(Ad, Ad if sym else Bm.to(DEV))
-    ref = A.double().transpose(1, 2) @ Bm.double()
+    C = K.gram_f64(Ad, Ad if sym else Bm.to(DEV), ta=tk, tb=tk)
+    ref = (A.double() @ Bm.double().transpose(1, 2)) if tk else (A.double().transpose(1, 2) @ Bm.double())
     assert ((C.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-13
     if sym:
         assert torch.equal(C, C.transpose(1, 2))
