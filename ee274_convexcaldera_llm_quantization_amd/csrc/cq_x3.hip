@@ -795,6 +795,88 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
     }
 }
 
+// Single-product (hi x hi) K loop on a 4-slot ring: only the hi halves are loaded, so a
+// stage is 36 KB (A hi 192 x 32 | B hi 384 x 32) and four fit the 144 KB the 2-stage split
+// ring uses.  Loads of steps t+1..t+3 are issued while step t computes (counted vmcnt
+// across the raw s_barrier: 3 LDS-DMA wave-instructions per wave and step): a hi-only step
+// has a third of the split product's MFMA work, too little to cover an HBM round trip with
+// one stage ahead.  Same fragments, MFMAs and accumulation order as xv_mainloop<false, true>.
+constexpr int XV1_NS = 4;
+constexpr int XV1_STAGE = XW_APART + XW_BPART;  // halves
+static_assert((size_t)XV1_NS * XV1_STAGE * sizeof(_Float16) <= XW_LDS_BYTES, "single-product ring fits the LDS");
+
+__device__ __forceinline__ void xv1_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                          const uint32_t (&off)[XW1_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW1_PER_WAVE; ++u) {
+        const int I = wid * XW1_PER_WAVE + u;
+        const bool isA = I < 12;
+        const int sub = isA ? I : I - 12;
+        const _Float16* base = isA ? a.Ah + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
+                                   : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
+        _Float16* dst = stage + (isA ? 0 : XW_APART) + (16 * sub) * XW_BK;
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
+                                         16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void xv1_wait(int64_t after) {
+    // this wave's loads of the stages issued after step t (at most XV1_NS - 2 = 2 at the wait,
+    // step t + 3 being issued after it) may stay in flight
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
+                                             _Float16* smem, int wid, int lane, int wm, int wn,
+                                             f32x4v (&acc)[6][4]) {
+    static_assert(XV1_NS == 4 && XW1_PER_WAVE == 3, "xv1_wait's counts");
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    wid = __builtin_amdgcn_readfirstlane(wid);
+    uint32_t off[XW1_PER_WAVE];
+    if (nt > 0) {
+        xw1_plan(a, m0, n0, wid, lane, off);
+        for (int64_t s = 0; s < XV1_NS - 1 && s < nt; ++s) xv1_issue(a, b, s * XW_BK, smem + s * XV1_STAGE, wid, off);
+    }
+    const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
+    uint32_t live = (a.noskip || (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0))) ? 1u : 0u;
+    live = __builtin_amdgcn_readfirstlane(live);
+    if (!live) {  // dead 96 x 64 block: its share of the loads and barriers only
+        for (int64_t t = 0; t < nt; ++t) {
+            xv1_wait(nt - 1 - t);
+            __builtin_amdgcn_s_barrier();
+            if (t + XV1_NS - 1 < nt)
+                xv1_issue(a, b, (t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE, wid,
+                          off);
+        }
+        return;
+    }
+    for (int64_t t = 0; t < nt; ++t) {
+        xv1_wait(nt - 1 - t);
+        __builtin_amdgcn_s_barrier();  // stage t landed everywhere; the slot of t - 1 fully read
+        // slot (t + 3) % 4 last held step t - 1, whose reads every wave finished before this barrier
+        if (t + XV1_NS - 1 < nt)
+            xv1_issue(a, b, (t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE, wid, off);
+        const _Float16* sA = smem + (t & (XV1_NS - 1)) * XV1_STAGE;
+        const _Float16* sB = sA + XW_APART;
+        f16x8 bh[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bh[j] = xg_frag(sB, 64 * wn + 16 * j + l16, lq);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const f16x8 ah = xg_frag(sA, 96 * wm + 16 * i + l16, lq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+        }
+    }
+}
+
 template <bool X1>
 __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     extern __shared__ __attribute__((aligned(16))) char xv_smem_raw[];
@@ -817,7 +899,11 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
 
     f32x4v acc[6][4];
     const bool live = !a.active || a.active[b];
-    xv_mainloop<false, X1>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+    if constexpr (X1) {
+        xv1_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+    } else {
+        xv_mainloop<false, false>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+    }
 
     const float sc = a.inv_scale[b];
     if (a.sym_out) {

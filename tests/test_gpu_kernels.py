@@ -443,6 +443,29 @@ def test_gemm_x3_matches_fp64(K, M, N, Kd):
     assert err < max(3 * err32, 1e-6), (err, err32)
 
 
+@pytest.mark.parametrize("M,N,Kd,blocked", [(192, 4096, 4096, True), (100, 1000, 32, False), (192, 400, 64, True),
+                                            (250, 770, 96, False), (192, 384, 128, True)])
+def test_gemm_x3_single_product_matches_fp64(K, M, N, Kd, blocked):
+    """single mode (the filter's low-precision steps, 4-slot hi-only ring): C = Ah Bh^T * inv
+    with fp32 accumulation -- pinned against fp64 of the same fp16 operands, short K (ring
+    prologue deeper than the loop), ragged tiles and the K-blocked layouts included."""
+    Bt = 2
+    g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g)
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g) * 3.0
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 10, blocked=blocked)
+    Bh, Bl = K.split_f16(Bm.contiguous(), 2.0 ** 8, blocked=blocked)
+    inv = torch.full((Bt,), 2.0 ** -18, device=DEV)
+    C = torch.full((Bt, M, N), float("nan"), device=DEV)
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C, a_blocked=blocked, b_blocked=blocked, single=True)
+    if blocked:  # back to row-major for the reference
+        Ah = Ah.view(Bt, Kd // 32, M, 32).permute(0, 2, 1, 3).reshape(Bt, M, Kd)
+        Bh = Bh.view(Bt, Kd // 32, N, 32).permute(0, 2, 1, 3).reshape(Bt, N, Kd)
+    ref = torch.matmul(Ah.double(), Bh.double().transpose(1, 2)) * 2.0 ** -18
+    err = ((C.double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < 2e-6, err
+
+
 def test_gemm_x3_tri_upper_exact(K):
     """tri mode: the upper triangle of Y Y^T equals the full product's bit for bit."""
     g = torch.Generator(device=DEV).manual_seed(21)
