@@ -46,7 +46,7 @@ WORKLOADS = {
                  batch=256, desc="BASELINE configs[1]: 4096x4096 fp16, rank 128, Q_bits 2, L/R_bits 16, "
                                  "iters 5, update_order [Q, LR], H = I"),
     "cfg3": dict(m=4096, n=11008, Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, lplr_iters=5, H=True,
-                 batch=96, desc="BASELINE configs[2]: 4096x11008 fp16, activation-aware diag H (resampled "
+                 batch=192, desc="BASELINE configs[2]: 4096x11008 fp16, activation-aware diag H (resampled "
                                 "diag_Hessians.pt down_proj entry), rank 128, Q_bits 2, L/R_bits 16, iters 5"),
     "cfg5": dict(m=4096, n=4096, Q_bits=2, L_bits=4, R_bits=4, rank=256, iters=5, lplr_iters=10, H=False,
                  batch=256, desc="BASELINE configs[4]: 4096x4096 fp16, rank 256, Q_bits 2, L/R_bits 4, "

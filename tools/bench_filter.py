@@ -63,6 +63,11 @@ print(f"[{tag}] filter B={B}: {ms:.3f} ms/launch  {by / ms / 1e6:.0f} GB/s algor
 plain = lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, b_blocked=True, a_blocked=True)
 ms2 = bench(plain)
 print(f"[{tag}] plain X^T G B={B}: {ms2:.3f} ms/launch", flush=True)
+single = lambda: K.gemm_x3(Xh, Xl, Gh, Gl, inv, Ct, P=Pv, D=Xt, alpha_v=a, beta_v=bb, gamma_v=c, out_h=Oh, out_l=Ol,
+                           out_scale=xs, overflow=ovf, b_blocked=True, a_blocked=True, o_blocked=True, single=True)
+ms6 = bench(single)
+print(f"[{tag}] single-product filter B={B}: {ms6:.3f} ms/launch  "
+      f"{B * (2 * k * k + 20 * p * k) / ms6 / 1e6:.0f} GB/s algorithmic", flush=True)
 if tag.startswith("w4"):
     def reblock(t, n, kk):  # 32-blocked -> 16-blocked
         return t.view(-1, kk // 32, n, 32).permute(0, 2, 1, 3).reshape(-1, n, kk // 16, 16).permute(0, 2, 1, 3).contiguous().view(-1, n, kk)
