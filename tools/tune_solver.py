@@ -1,32 +1,35 @@
-"""Solver tuning sweep on the bench workload (config 2): for each setting, time one batched
-step of B matrices (after a warm-up step) and report the parity of the seed-0 matrix
-against the reference's golden sketch (tests/golden/sum_large.npz).
-    python tools/tune_solver.py B "tol=5e-6" "tol=2e-5" "tol=1e-5,deg_warm=(12,6)"
+"""Solver tuning sweep on a bench workload: for each setting, time one batched step of B
+matrices (after a warm-up step) and report the parity of seeds 0-3 (batch positions 0-3)
+against the reference's golden sketches (bench.parity_of_timed_step).
+    python tools/tune_solver.py cfg2 128 "tol=1e-5" "deg_cold=(8,12,12,12)" "cheap_cold=2"
 """
-import os, sys, time
+import os
+import sys
+import time
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "ee274_convexcaldera_llm_quantization_amd")]
+sys.path.insert(0, ROOT)
 import torch
+
 import bench
 from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
-from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
 
 dev = torch.device("cuda", 0)
-B = int(sys.argv[1])
-qp = bench.make_params()
-ep = EngineParams.from_caldera_params(qp)
-Wb = bench.synth_batch(B, 0, dev)  # seed 0 first: its result is the parity sample
-W0 = bench.synth_batch(1, 0, "cpu")[0]
+name, B = sys.argv[1], int(sys.argv[2])
+wl = bench.WORKLOADS[name]
+ep = EngineParams.from_caldera_params(bench.make_params(wl))
+Wb = bench.synth_batch(wl, B, 0, dev)
+h = bench.make_h(wl)
+h = None if h is None else h.to(dev)
 
 
 def run(kw):
-    tol = kw.pop("tol", 5e-6)
+    tol = kw.pop("tol", 1e-5)
     eng = CalderaEngine(ep, solver_tol=tol, solver_kwargs=kw)
-    outs = run_interleaved([eng.run_iter(Wb, None, True)], dev)
-    return outs[0], eng
+    return eng.run(Wb, h), eng
 
 
-for spec in sys.argv[2:]:
+for spec in sys.argv[3:]:
     kw = eval(f"dict({spec})")
     run(dict(kw))
     torch.cuda.synchronize()
@@ -34,11 +37,10 @@ for spec in sys.argv[2:]:
     decs, eng = run(dict(kw))
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    from types import SimpleNamespace
-    par, _ = bench.frob_vs_reference(SimpleNamespace(**decs[0]), W0, False)
+    par = bench.parity_of_timed_step(name, decs, wl)
     st = eng.solver.stats
-    print(f"{spec:40s} {B / el:7.1f} matrices/s  {1000 * el:8.1f} ms/step  matvecs {st.matvecs:4d}  "
-          f"outer {st.outer:3d}  frob_vs_sketch {par['frob_err_vs_ref_sketch']:.2e}  "
-          f"hist {[(h[1], ['%.1e' % x for x in h[2]]) for h in st.history]}", flush=True)
+    ps = " ".join(f"{k}={v:.1e}" for k, v in par.items() if k.startswith("seed"))
+    print(f"{spec:44s} {B / el:7.1f} matrices/s {1000 * el:8.1f} ms  matvecs {st.matvecs:4d} outer {st.outer:3d}  "
+          f"{ps}  hist {[(hh[1], ['%.1e' % x for x in hh[2]]) for hh in st.history]}", flush=True)
     del decs, eng
     torch.cuda.empty_cache()
