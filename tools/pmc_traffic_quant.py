@@ -39,5 +39,5 @@ for k in sorted(fe):
 print(json.dumps({"config": {"batch": B, "m": m, "n": n, "bits": bits}, "kernels": res,
                   "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KB*1024), gfx950 (MI355X_MICROARCH.md HBM)",
                   "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) "
-                            f"--kernel-include-regex 'quant_w_stream|q_update_v' -- python3 bench.py --batch {B} "
-                            f"--steps 1 --warmup 0 --no-parity"}, indent=1))
+                            f"--kernel-include-regex 'quant_w_stream|q_update_p|q_update_v' -- python3 bench.py --batch {B} "
+                            f"--steps 1 --warmup 0 --no-parity --no-cpu-baseline --no-api-path"}, indent=1))

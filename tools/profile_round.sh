@@ -10,12 +10,12 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- \
-    python3 bench.py --batch $B --steps 1 --warmup 1 --no-parity > $OUT/stats.log 2>&1
+    python3 bench.py --batch $B --steps 1 --warmup 1 --no-parity --no-cpu-baseline --no-api-path > $OUT/stats.log 2>&1
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --kernel-include-regex gemm_x3 -d $OUT/pmc_$c -o run \
-      --output-format csv -- python3 bench.py --batch $B --steps 1 --warmup 0 --no-parity > $OUT/pmc_$c.log 2>&1
-  timeout -k 10 400 rocprofv3 --pmc $c --kernel-include-regex 'quant_w_stream|q_update_v' -d $OUT/qpmc_$c -o run \
-      --output-format csv -- python3 bench.py --batch $B --steps 1 --warmup 0 --no-parity > $OUT/qpmc_$c.log 2>&1
+      --output-format csv -- python3 bench.py --batch $B --steps 1 --warmup 0 --no-parity --no-cpu-baseline --no-api-path > $OUT/pmc_$c.log 2>&1
+  timeout -k 10 400 rocprofv3 --pmc $c --kernel-include-regex 'quant_w_stream|q_update_p|q_update_v' -d $OUT/qpmc_$c -o run \
+      --output-format csv -- python3 bench.py --batch $B --steps 1 --warmup 0 --no-parity --no-cpu-baseline --no-api-path > $OUT/qpmc_$c.log 2>&1
 done
 python3 tools/profile_summary.py $OUT/stats $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE > $OUT/summary.txt
 python3 tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $B 192 4096 > $OUT/pmc_traffic.json
