@@ -186,36 +186,36 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
     }
 }
 
-// 4 x 4 register tile per thread of a 64 x 64 fp64 product C = op(X) Y from LDS.
-// transX: C[u][v] = sum_k X[k][u] Y[k][v]; else C[u][v] = sum_k X[u][k] Y[k][v].
-template <bool transX>
-__device__ __forceinline__ void mm64(const double* X, const double* Y, double acc[4][4], int tu, int tv) {
+// 64 x 64 x 64 fp64 product C = X Y on v_mfma_f64_16x16x4f64 (products and sums in fp64,
+// as the fp64 FMA loop it replaces): wave w owns the 32 x 32 quadrant (rows 32 (w >> 1),
+// columns 32 (w & 1)) as 2 x 2 tiles; xa(i, k) / yb(k, j) fetch the operands (global/L2 or
+// LDS).  Result C[32 (w >> 1) + 16 ti + (lane >> 4) + 4 r][32 (w & 1) + 16 tj + (lane & 15)]
+// = acc[ti][tj][r] (the f64 MFMA's C/D map).
+using f64x4v = __attribute__((ext_vector_type(4))) double;
+
+template <class FX, class FY>
+__device__ __forceinline__ void mfma64(FX xa, FY yb, f64x4v (&acc)[2][2], int wid, int lane) {
+    const int ri = 32 * (wid >> 1), cj = 32 * (wid & 1), l16 = lane & 15, lk = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-    for (int k = 0; k < D; ++k) {
-        double xa[4], yb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xa[i] = transX ? X[k * LDP + tu + 16 * i] : X[(tu + 16 * i) * LDP + k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) yb[j] = Y[k * LDP + tv + 16 * j];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = fma(xa[i], yb[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int k0 = 0; k0 < D; k0 += 4) {
+        const int k = k0 + lk;
+        const double a0 = xa(ri + l16, k), a1 = xa(ri + 16 + l16, k);
+        const double b0 = yb(k, cj + l16), b1 = yb(k, cj + 16 + l16);
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
 }
 
-__device__ __forceinline__ void load_v(double* dst, const double* Vs, bool rotated, int tid) {
-    for (int t = tid; t < D * D; t += BT) {
-        const int u = t / D, v = t % D;
-        dst[u * LDP + v] = rotated ? Vs[t] : (u == v ? 1.0 : 0.0);
-    }
-}
-
-// Workgroups [0, npair*(npair-1)): off-diagonal pair-block (P, Q), A[P,Q] <- V_P^T A[P,Q] V_Q.
-// Workgroups [npair*(npair-1), + npair) (with eigenvectors): Vt[P, :] <- V_P^T Vt[P, :].
+// Workgroups [0, npair*(npair-1)): off-diagonal pair-block (P, Q), A[P,Q] <- V_P^T A[P,Q] V_Q
+// (operands straight from L2 into the MFMAs; T = V_P^T A[P,Q] re-laid out through LDS).
+// Workgroups [npair*(npair-1), + npair * nch) (with eigenvectors): Vt[P, x0:x0+64] <-
+// V_P^T Vt[P, x0:x0+64], one 64-column chunk each.  33 KB of LDS: several workgroups per CU.
 __global__ __launch_bounds__(BT) void bj_update_kernel(double* __restrict__ A_all, int p, int nblk, int step,
                                                        const double* __restrict__ Vs_all,
                                                        const int* __restrict__ rot_all, const int* __restrict__ done,
@@ -225,15 +225,15 @@ __global__ __launch_bounds__(BT) void bj_update_kernel(double* __restrict__ A_al
     const int w = blockIdx.x;
     const int64_t b = blockIdx.y;
     if (done[b]) return;
-    __shared__ double Xs[D * LDP];
-    __shared__ double Ys[D * LDP];
     __shared__ double Ms[D * LDP];
     __shared__ int gP[D], gQ[D];
     __shared__ double red[16];
-    const int tid = threadIdx.x, tu = tid / 16, tv = tid % 16;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ri = 32 * (wid >> 1), cj = 32 * (wid & 1), l16 = lane & 15, lk = lane >> 4;
     double* A = A_all + b * (int64_t)p * p;
     const int* rot = rot_all + b * npair;
     const double* Vs = Vs_all + b * npair * (int64_t)(D * D);
+    f64x4v acc[2][2];
     if (w < noff) {
         const int P = w / (npair - 1);
         int Q = w % (npair - 1);
@@ -244,40 +244,55 @@ __global__ __launch_bounds__(BT) void bj_update_kernel(double* __restrict__ A_al
         if (tid < D) { gP[tid] = gidx(a, c, tid, p); gQ[tid] = gidx(e, f, tid, p); }
         __syncthreads();
         const bool rp = rot[P] != 0, rq = rot[Q] != 0;
-        for (int t = tid; t < D * D; t += BT) {
-            const int u = t / D, v = t % D;
-            const int gu = gP[u], gv = gQ[v];
-            Ms[u * LDP + v] = (gu >= 0 && gv >= 0) ? A[(int64_t)gu * p + gv] : 0.0;
-        }
+        auto apq = [&](int k, int j) -> double {
+            const int gu = gP[k], gv = gQ[j];
+            return (gu >= 0 && gv >= 0) ? A[(int64_t)gu * p + gv] : 0.0;
+        };
         double off = 0.0;
         if (rp || rq) {
-            load_v(Xs, Vs + (int64_t)P * D * D, rp, tid);
-            load_v(Ys, Vs + (int64_t)Q * D * D, rq, tid);
+            const double* VP = Vs + (int64_t)P * D * D;
+            const double* VQ = Vs + (int64_t)Q * D * D;
+            if (rp) {  // T = V_P^T A_PQ into Ms
+                mfma64([&](int i, int k) { return VP[k * D + i]; }, apq, acc, wid, lane);
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            Ms[(ri + 16 * ti + lk + 4 * r) * LDP + cj + 16 * tj + l16] = acc[ti][tj][r];
+            } else {
+                for (int t = tid; t < D * D; t += BT) Ms[(t / D) * LDP + (t % D)] = apq(t / D, t % D);
+            }
             __syncthreads();
-            double acc[4][4];
-            mm64<true>(Xs, Ms, acc, tu, tv);       // T = V_P^T A_PQ
-            __syncthreads();
+            if (rq) {  // C = T V_Q
+                mfma64([&](int i, int k) { return Ms[i * LDP + k]; }, [&](int k, int j) { return VQ[k * D + j]; },
+                       acc, wid, lane);
+            } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) Ms[(tu + 16 * i) * LDP + tv + 16 * j] = acc[i][j];
-            __syncthreads();
-            mm64<false>(Ms, Ys, acc, tu, tv);      // T V_Q
+                    for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                        for (int r = 0; r < 4; ++r)
+                            acc[ti][tj][r] = Ms[(ri + 16 * ti + lk + 4 * r) * LDP + cj + 16 * tj + l16];
+            }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int u = tu + 16 * i, v = tv + 16 * j;
-                    const int gu = gP[u], gv = gQ[v];
-                    if (gu >= 0 && gv >= 0) {
-                        A[(int64_t)gu * p + gv] = acc[i][j];
-                        off += acc[i][j] * acc[i][j];
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int gu = gP[ri + 16 * ti + lk + 4 * r], gv = gQ[cj + 16 * tj + l16];
+                        if (gu >= 0 && gv >= 0) {
+                            const double x = acc[ti][tj][r];
+                            A[(int64_t)gu * p + gv] = x;
+                            off += x * x;
+                        }
                     }
-                }
         } else {
-            __syncthreads();
             for (int t = tid; t < D * D; t += BT) {
-                const double x = Ms[(t / D) * LDP + (t % D)];
+                const double x = apq(t / D, t % D);
                 off += x * x;
             }
         }
@@ -285,33 +300,32 @@ __global__ __launch_bounds__(BT) void bj_update_kernel(double* __restrict__ A_al
         if (tid == 0) part_off[b * nslots + npair + w] = offs;
         return;
     }
-    // eigenvector rows of pair P
-    const int P = w - noff;
+    // eigenvector rows of pair P, one 64-column chunk
+    const int nch = (p + D - 1) / D;
+    const int P = (w - noff) / nch, x0 = ((w - noff) % nch) * D;
     if (!Vt_all || !rot[P]) return;
     int a, c;
     rr(nblk, step, P, a, c);
     if (tid < D) gP[tid] = gidx(a, c, tid, p);
-    load_v(Xs, Vs + (int64_t)P * D * D, true, tid);
+    __syncthreads();
+    const double* VP = Vs + (int64_t)P * D * D;
     double* Vt = Vt_all + b * (int64_t)p * p;
-    for (int x0 = 0; x0 < p; x0 += D) {
-        __syncthreads();
-        for (int t = tid; t < D * D; t += BT) {
-            const int u = t / D, l = t % D;
-            const int gu = gP[u];
-            Ms[u * LDP + l] = (gu >= 0 && x0 + l < p) ? Vt[(int64_t)gu * p + x0 + l] : 0.0;
-        }
-        __syncthreads();
-        double acc[4][4];
-        mm64<true>(Xs, Ms, acc, tu, tv);           // V_P^T Vt[P, x0:x0+64]
+    mfma64([&](int i, int k) { return VP[k * D + i]; },
+           [&](int k, int l) {
+               const int gu = gP[k];
+               return (gu >= 0 && x0 + l < p) ? Vt[(int64_t)gu * p + x0 + l] : 0.0;
+           },
+           acc, wid, lane);
+    __syncthreads();  // every wave has read the chunk's rows before any is overwritten
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+    for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int u = tu + 16 * i, l = tv + 16 * j;
-                const int gu = gP[u];
-                if (gu >= 0 && x0 + l < p) Vt[(int64_t)gu * p + x0 + l] = acc[i][j];
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gu = gP[ri + 16 * ti + lk + 4 * r], l = cj + 16 * tj + l16;
+                if (gu >= 0 && x0 + l < p) Vt[(int64_t)gu * p + x0 + l] = acc[ti][tj][r];
             }
-    }
 }
 
 __global__ void bj_check_kernel(const double* __restrict__ part_off, const double* __restrict__ part_dg, int nslots,
@@ -385,6 +399,7 @@ int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, dou
     const int nblk = (int)(ceil_div(p, NB) + (ceil_div(p, NB) & 1));
     const int npair = nblk / 2, noff = npair * (npair - 1), nslots = npair + noff;
     const bool want_v = V32 || V64;
+    const int nch = (int)ceil_div(p, D);  // 64-column chunks of the eigenvector rows
     char* w = reinterpret_cast<char*>(ws);
     auto take = [&](size_t bytes) { char* r = w; w += align_up(bytes, 256); return r; };
     double* Vt = reinterpret_cast<double*>(take((size_t)batch * p * p * sizeof(double)));
@@ -410,7 +425,7 @@ int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, dou
         for (int st = 0; st < nblk - 1; ++st) {
             bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
                                                                                    done, poff, pdg, nslots);
-            bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair : 0)), (unsigned)batch), BT, 0, s>>>(
+            bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair * nch : 0)), (unsigned)batch), BT, 0, s>>>(
                 A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
         }
         bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
