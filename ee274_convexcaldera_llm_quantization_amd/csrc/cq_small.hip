@@ -1071,6 +1071,178 @@ __global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
         }
 }
 
+// ------------------------------------------------------------------ blocked SPD whitening, MFMA
+// The same elimination in LDL^T block form, nb = 32 pivots per panel J:
+//   1. one wave factors the 32 x 32 diagonal block in registers (lane l = row l of the
+//      symmetric block and of its L^{-1}; the pivot row is broadcast by shuffles): pivots
+//      (rank-revealing drop rule unchanged), L11^{-1};
+//   2. panel rows of S right of the block, U12 = L11^{-1} S12, and the panel rows of
+//      E = L^{-1} (columns < J + 32), Ep = L11^{-1} E_panel — v_mfma_f64_16x16x4f64 tiles of
+//      32 rows x 16 columns (one wave per column block: in place without a race);
+//   3. trailing S (upper tiles) -= G^T U12 with G = diag(1/d) U12, trailing E rows -= G^T Ep.
+// Three workgroup barriers per panel instead of two per pivot; operands come from L2 (S, E
+// are fp64 p x p per matrix), so the LDS footprint is small and p is unbounded.  Products and
+// sums in fp64, as the scalar loops; the row operations are the same, in block order.
+constexpr int kWmThreads = 512;
+constexpr int kWmWaves = kWmThreads / 64;
+
+
+__global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __restrict__ S_all, int p, double rc2,
+                                                                     double* __restrict__ E_all,
+                                                                     float* __restrict__ W32, int* __restrict__ info) {
+    extern __shared__ __attribute__((aligned(16))) double wm_smem[];
+    double* piv = wm_smem;          // p pivots (inf for dropped)
+    double* Li = piv + p;           // 32 x 33: L11^{-1} of the current panel (row-major, padded)
+    double* rp = Li + 32 * 33;      // 32: 1 / pivot (0 for dropped) of the current panel
+    double* Bk = rp + 32;           // 32 x 33: the diagonal block being factored
+    __shared__ int bad;
+    __shared__ double dmax_s;
+    __shared__ double red[16];
+    const int64_t b = blockIdx.x;
+    double* S = S_all + b * (int64_t)p * p;
+    double* E = E_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int l16 = lane & 15, lk = lane >> 4;
+    for (int i = wid; i < p; i += kWmWaves)
+        for (int c = lane; c < p; c += 64) E[(int64_t)i * p + c] = (i == c) ? 1.0 : 0.0;
+    double dm = 0.0;
+    for (int j = tid; j < p; j += kWmThreads) dm = fmax(dm, fabs(S[(int64_t)j * p + j]));
+    for (int o = 32; o > 0; o >>= 1) {
+        const int2 x = __builtin_bit_cast(int2, dm);
+        int2 y;
+        y.x = __shfl_xor(x.x, o, 64);
+        y.y = __shfl_xor(x.y, o, 64);
+        dm = fmax(dm, __builtin_bit_cast(double, y));
+    }
+    if (lane == 0) red[wid] = dm;
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    if (tid == 0) {
+        double m = 0.0;
+        for (int w = 0; w < kWmWaves; ++w) m = fmax(m, red[w]);
+        dmax_s = m;
+    }
+    __syncthreads();
+    const double dmax = dmax_s;
+    for (int J = 0; J < p; J += 32) {
+        const int nb = min(32, p - J);
+        const int t0 = J + nb;
+        // ---- 1. diagonal block (wave 0)
+        // the symmetric block (Bk) and L11^{-1} (Li) in LDS; thread (row r = tid / 16, columns
+        // c = tid % 16 and c + 16) applies the row operation of pivot k to its elements: within a
+        // step nothing it reads (row k, column k) is written, so one barrier per pivot
+        {
+            const int r = tid >> 4, c0 = tid & 15;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = c0 + 16 * h;
+                const int a = min(r, c), e = max(r, c);
+                Bk[r * 33 + c] = (r < nb && c < nb) ? S[(int64_t)(J + a) * p + J + e] : 0.0;
+                Li[r * 33 + c] = (c == r) ? 1.0 : 0.0;
+            }
+            __syncthreads();
+            int nbad = 0;
+            for (int k = 0; k < nb; ++k) {
+                const double d = Bk[k * 33 + k];
+                const bool drop = !(d > 1e-300 && d > dmax * rc2);
+                nbad += drop;
+                if (tid == 0) {
+                    piv[J + k] = drop ? __longlong_as_double(0x7ff0000000000000ll) : d;
+                    rp[k] = drop ? 0.0 : 1.0 / d;
+                }
+                if (!drop && r > k && r < nb) {
+                    const double f = Bk[r * 33 + k] / d;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int c = c0 + 16 * h;
+                        if (c > k && c < nb) Bk[r * 33 + c] -= f * Bk[k * 33 + c];
+                        else if (c <= k) Li[r * 33 + c] -= f * Li[k * 33 + c];
+                    }
+                }
+                __syncthreads();
+            }
+            if (tid == 0) bad += nbad;
+        }
+        __syncthreads();
+        // ---- 2. U12 = L11^{-1} S12 (columns >= t0) and Ep = L11^{-1} E_panel (columns < t0),
+        // in place; one wave per 16-column block, both 16-row halves
+        const int ncs = (p - t0 + 15) / 16, nce = (t0 + 15) / 16;
+        for (int cb = wid; cb < ncs + nce; cb += kWmWaves) {
+            const bool isS = cb < ncs;
+            double* M = isS ? S : E;
+            const int c0 = isS ? t0 + 16 * cb : 16 * (cb - ncs);
+            const int clim = isS ? p : t0;
+            const int col = c0 + l16;
+            f64x4v acc[2] = {f64x4v{0.0, 0.0, 0.0, 0.0}, f64x4v{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+            for (int k0 = 0; k0 < 32; k0 += 4) {
+                const int k = k0 + lk;
+                const double bv = (k < nb && col < clim) ? M[(int64_t)(J + k) * p + col] : 0.0;
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[l16 * 33 + k], bv, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[(16 + l16) * 33 + k], bv, acc[1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int k = 16 * h + lk + 4 * r;
+                    if (k < nb && col < clim) M[(int64_t)(J + k) * p + col] = acc[h][r];
+                }
+        }
+        __syncthreads();
+        // ---- 3. trailing updates with G^T[i][k] = U12[k][i] / d_k:
+        //   S[i][c] -= sum_k G^T[i][k] U12[k][c]  (16 x 16 tiles on or above the diagonal)
+        //   E[i][c] -= sum_k G^T[i][k] Ep[k][c]   (rows i >= t0, columns c < t0)
+        const int nt = (p - t0 + 15) / 16;
+        const int nst = nt * (nt + 1) / 2, net = nt * nce;
+        for (int t = wid; t < nst + net; t += kWmWaves) {
+            int ti, c0;
+            double* M;
+            if (t < nst) {  // upper tile (ti, tj), tj >= ti
+                int tj = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+                if (tj * (tj + 1) / 2 > t) --tj;
+                if ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
+                ti = t - tj * (tj + 1) / 2;
+                c0 = t0 + 16 * tj;
+                M = S;
+            } else {
+                ti = (t - nst) / nce;
+                c0 = 16 * ((t - nst) % nce);
+                M = E;
+            }
+            const int i0 = t0 + 16 * ti;
+            const int clim = (M == S) ? p : t0;
+            const int col = c0 + l16, arow = i0 + l16;
+            f64x4v acc = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k0 = 0; k0 < 32; k0 += 4) {
+                const int k = k0 + lk;
+                const bool kv = k < nb;
+                const double av = (kv && arow < p) ? S[(int64_t)(J + k) * p + arow] * rp[k] : 0.0;
+                const double bv = (kv && col < clim) ? M[(int64_t)(J + k) * p + col] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + lk + 4 * r;
+                if (i < p && col < clim) {
+                    double* dst = M + (int64_t)i * p + col;
+                    *dst = *dst - acc[r];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) info[b] = bad;
+    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular; 0 for dropped pivots); staged in S
+    for (int a = wid; a < p; a += kWmWaves)
+        for (int c = lane; c < p; c += 64) {
+            const double v = (c >= a) ? E[(int64_t)c * p + a] / sqrt(piv[c]) : 0.0;
+            if (W32) W32[b * (int64_t)p * p + (int64_t)a * p + c] = (float)v;
+            S[(int64_t)a * p + c] = v;
+        }
+}
+
 static size_t whiten_lds_bytes(int p, int nb) {
     return (size_t)(2 * nb * p + p + nb) * sizeof(double) + 16;
 }
@@ -1202,7 +1374,11 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
     hipStream_t s = as_stream(stream);
     // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
     const size_t wl32 = whiten_lds_bytes((int)p, 32), wl16 = whiten_lds_bytes((int)p, 16);
-    if (wl32 <= 160 * 1024)
+    static const bool legacy = getenv("CQ_WHITEN_LEGACY") != nullptr;  // A/B switch: the scalar kernels
+    const size_t wlm = (size_t)(p + 2 * 32 * 33 + 32) * sizeof(double);
+    if (!legacy && wlm <= 64 * 1024)
+        spd_whiten_mfma_kernel<<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    else if (wl32 <= 160 * 1024)
         spd_whiten_blocked_kernel<32><<<(unsigned)batch, kSmallThreads, wl32, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     else if (wl16 <= 160 * 1024)
         spd_whiten_blocked_kernel<16><<<(unsigned)batch, kSmallThreads, wl16, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);

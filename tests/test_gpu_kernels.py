@@ -735,6 +735,26 @@ def test_residual_split_matches_unfused(K, bits, weighted):
     assert torch.allclose(sq, (Ysrc.double() ** 2).sum((1, 2)), rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("p", [1, 17, 32, 33, 96, 200, 256, 384])
+def test_spd_whiten_shapes(K, p):
+    """Blocked LDL^T whitening (MFMA panels of 32): Wt^T S Wt = I and Wt upper triangular for
+    ragged last panels, a single pivot, and p > 192 (the LPLR normal equations at rank 200 /
+    256, the p = 384 CholQR); per-matrix results independent of the batch."""
+    g = torch.Generator().manual_seed(p)
+    X = torch.randn(3, 4 * p + 8, p, dtype=torch.float64, generator=g)
+    X[1] *= 1e3
+    S = X.transpose(1, 2) @ X
+    Wt32, Wt64, info = K.spd_whiten(S.clone().to(DEV))
+    assert torch.all(info == 0)
+    Wt = Wt64.cpu()
+    I = Wt.transpose(1, 2) @ S @ Wt
+    assert (I - torch.eye(p, dtype=torch.float64)).abs().max().item() < 1e-9
+    assert torch.equal(torch.triu(Wt), Wt)
+    assert torch.equal(Wt32.cpu(), Wt.float())
+    _, W1, _ = K.spd_whiten(S[2:3].clone().to(DEV))
+    assert torch.equal(W1.cpu()[0], Wt[2])
+
+
 @pytest.mark.parametrize("p", [24, 200, 300, 384, 700])  # blocked nb 32 / nb 16, unblocked
 def test_spd_whiten_rank_deficient_is_gelsy_basic_solution(K, p):
     """lstsq through the normal equations with dependent columns (alg.py:162-177 with a
