@@ -140,8 +140,8 @@ def cpu_baseline(name, wl, dec0):
 def run_model(args):
     """BASELINE configs[3]: the 224 Llama-2-7B linear weights (random-init fp16, one device RNG
     seed per matrix, resident in HBM before the timed region), rank i % world decomposing
-    matrix i (sharding.decompose_sharded: same-shape batches of <= 16 interleaved on their own
-    HIP streams), results packed in HBM and gathered to rank 0 over RCCL.  One step = the
+    matrix i (sharding.decompose_sharded: same-shape batches of <= 16 (8 GPUs) / 64 interleaved on
+    their own HIP streams), results packed in HBM and gathered to rank 0 over RCCL.  One step = the
     whole model."""
     from ee274_convexcaldera_llm_quantization_amd import sharding as S
     from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
@@ -168,12 +168,17 @@ def run_model(args):
         Wd[name] = (torch.randn(m, n, generator=g, device=dev) * 0.02).to(torch.float16)
     ep = EngineParams.from_caldera_params(qp)
 
+    # a rank's share at 8 GPUs is 28 matrices (3 shape batches, interleaved on their own HIP
+    # streams); on fewer GPUs the same-shape batches grow (up to 64) so the one-CU-per-matrix
+    # solver kernels fill the chip, and two of them are interleaved at a time (HBM: ~1.2 GB of
+    # scratch per 11008x4096 matrix)
+    max_batch = args.model_batch or (16 if world >= 8 else 64)
+    group = 4 if max_batch <= 16 else 2
+
     def run_all(batches):
-        # up to 4 shape batches interleaved on their own HIP streams at a time (a rank's share
-        # at 8 GPUs is 3 batches; the whole model on one GPU is 14, whose scratch would not fit)
         res = []
-        for g0 in range(0, len(batches), 4):
-            grp = batches[g0:g0 + 4]
+        for g0 in range(0, len(batches), group):
+            grp = batches[g0:g0 + group]
             engines = [CalderaEngine(ep) for _ in grp]
             run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)], dev)
             res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"], d["R"],
@@ -186,7 +191,7 @@ def run_model(args):
     decompose.run_all = run_all
 
     def step():
-        return S.decompose_sharded(items, decompose, rank=rank, world=world, max_batch=16, device=dev)
+        return S.decompose_sharded(items, decompose, rank=rank, world=world, max_batch=max_batch, device=dev)
 
     for _ in range(args.warmup):
         step()
@@ -219,6 +224,7 @@ def run_model(args):
                                    "gate,up 11008x4096, down 4096x11008), r 128, Q2, L/R 16, iters 5, H = I; "
                                    "round-robin matrix sharding, RCCL gather of the packed (Q, L, R) to rank 0",
                        "name": "model", "matrices_per_step": len(items), "matrices_on_rank0": len(mine),
+                       "max_batch": max_batch, "interleaved_batches": group,
                        "parallelism": f"dp{world} (matrix-sharded)"},
             "gathered_bytes": int(sum(r.codes.numel() * r.codes.element_size() + r.L.numel() * 4 + r.R.numel() * 4
                                       for r in out)),
@@ -238,6 +244,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-api-path", action="store_true")
+    ap.add_argument("--model-batch", type=int, default=None,
+                    help="--workload model: same-shape batch size (default 64 below 8 GPUs, 16 at 8)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     args = ap.parse_args()
