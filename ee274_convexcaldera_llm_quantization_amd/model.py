@@ -181,7 +181,7 @@ def select_layers(model: torch.nn.Module, hessians=None, selection: LayerSelecti
 def apply_caldera_quantization(model: torch.nn.Module, hessians=None, quant_params=None, *,
                                selection: LayerSelection | None = None, error_threshold: float = 0.99,
                                scale_W: bool = False, hadamard: bool = False, device="cuda",
-                               max_batch: int = 16, keep_dtype: bool = True, decompose: Callable | None = None,
+                               max_batch: int = 64, keep_dtype: bool = True, decompose: Callable | None = None,
                                log: Callable | None = None, hadamard_gate: bool = False) -> QuantizationReport:
     """main.py:135-251 on the MI355X engine.
 
