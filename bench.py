@@ -382,7 +382,7 @@ def main():
             "frac_of_bound": max(t_hbm, t_mfma) / t, "launches_timed": g["count"], "avg_call_ms": g["avg_ms"],
             "bytes_per_call": g["bytes_per_launch"],
             "kernel": ("quant_w_stream_kernel (cq_q_update_x3, r = 0, max|W| known)" if kind == "w"
-                       else "q_update_v_kernel<0|1, bits> (cq_q_update_x3)")}
+                       else "q_update_p_kernel<0|1, bits> (cq_q_update_x3 row panels; q_update_v_kernel past r = 256)")}
     if qroof:
         result["roofline_quantise"] = qroof
     if lprobe:

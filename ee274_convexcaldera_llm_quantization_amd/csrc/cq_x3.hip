@@ -1876,16 +1876,19 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             }
         }
     };
-    qp_issue_r<NW>(Rhb, Rlb, 0, K, smem, wid, lane);
-    load_w(0, wr);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int64_t ch = 0; ch < nchunks; ++ch) {
+    // chunk body: R^T stage of chunk ch+1 and W of chunk `wload_ch` are issued at its start,
+    // its own W (wc) was loaded earlier.  Pass 0 (absmax: no stores in the loop) keeps W two
+    // chunks ahead (three register buffers, rotated by unrolling the loop by 3, so no in-flight
+    // destination is ever copied): at the end-of-chunk wait W(ch+2) is the wave's most recent
+    // vector-memory traffic and vmcnt(RB * WV) retires only the next R^T stage.  Pass 1 stores
+    // codes in the loop and keeps one chunk ahead (two buffers).
+    constexpr int WAHEAD = PASS == 0 ? 2 : 1;
+    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV]) {
         const int64_t n0 = ch * QP_BN;
-        if (ch + 1 < nchunks) {  // next chunk's R^T (LDS-DMA) and W in flight during this chunk
+        if (ch + 1 < nchunks)  // next chunk's R^T (LDS-DMA) in flight during this chunk
             qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
-            load_w(n0 + QP_BN, wn);
-        }
+        const bool wlive = ch + WAHEAD < nchunks;
+        if (wlive) load_w(n0 + WAHEAD * QP_BN, wl);
         const _Float16* st = smem + (ch & 1) * QP_STAGE;
         f32x4v acc[RB][2];
 #pragma unroll
@@ -1925,10 +1928,10 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                     const int u = 4 * c + i;
                     float w;
                     if (DT == CQ_F16) {
-                        const uint32_t pr = (&wr[rb][0].x)[u >> 1];
+                        const uint32_t pr = (&wc[rb][0].x)[u >> 1];
                         w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
                     } else {
-                        w = __uint_as_float((&wr[rb][(u >> 2) & (WV - 1)].x)[u & 3]);
+                        w = __uint_as_float((&wc[rb][(u >> 2) & (WV - 1)].x)[u & 3]);
                     }
                     v[u] = w - acc[rb][c][i] * sc;   // res = W - L R (alg.py:262)
                 }
@@ -1990,14 +1993,35 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 }
             }
         }
-        if (ch + 1 < nchunks) {
+        if (PASS == 0 && wlive) {
+            // vmcnt in bits [3:0] and [15:14]; expcnt / lgkmcnt at their maxima (not waited)
+            constexpr int nw = RB * WV;
+            __builtin_amdgcn_s_waitcnt((nw & 15) | ((nw >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
+    };
+    uint4 w3[PASS == 0 ? RB : 1][WV];
+    qp_issue_r<NW>(Rhb, Rlb, 0, K, smem, wid, lane);
+    load_w(0, wr);
+    if (PASS == 0 && nchunks > 1) load_w(QP_BN, wn);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if constexpr (PASS == 0) {
+        for (int64_t ch = 0; ch < nchunks; ch += 3) {
+            chunk(ch, wr, w3);
+            if (ch + 1 < nchunks) chunk(ch + 1, wn, wr);
+            if (ch + 2 < nchunks) chunk(ch + 2, w3, wn);
+        }
+    } else {
+        for (int64_t ch = 0; ch < nchunks; ++ch) {
+            chunk(ch, wr, wn);
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-                for (int w = 0; w < WV; ++w) wr[rb][w] = wn[rb][w];
+                for (int w = 0; w < WV; ++w) wr[rb][w] = wn[rb][w];  // landed at the chunk's vmcnt(0)
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
     }
     if (PASS == 0) {
         mx = wave_max_u32(mx);
@@ -2178,11 +2202,11 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     if (pk && !known) {
         // pass 0 (absmax) and pass 1 (quantise + packing, more live values) may use different
         // panel geometries: every 16 x 16 output block runs the same MFMA sequence whatever
-        // the geometry, so both passes see identical res.  8 waves; 4 (pass 0) / 3 (pass 1)
-        // row blocks per wave for K <= 128 and fp16 W (VGPR budget), 2 otherwise.
+        // the geometry, so both passes see identical res.  8 waves; 3 row blocks per wave for
+        // K <= 128 and fp16 W (VGPR budget: pass 0 keeps three W buffers), 2 otherwise.
         const bool f16 = dtype == CQ_F16;
         const bool small = r <= 128;
-        const int rb0 = (small && f16) ? 4 : 2, rb1 = (small && f16) ? 3 : 2;
+        const int rb0 = (small && f16) ? 3 : 2, rb1 = (small && f16) ? 3 : 2;
         const int64_t p0 = ceil_div(m, (int64_t)QP_WAVES * 16 * rb0), p1 = ceil_div(m, (int64_t)QP_WAVES * 16 * rb1);
         CQ_REQUIRE(p0 * batch < (1ll << 31), "cq_q_update_x3: grid too large");
         q.x.batch = batch;
@@ -2192,7 +2216,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
 #define CQ_QP(PS, B, DTV, RBV, KSV, G, P) \
         q_update_p_kernel<PS, B, DTV, RBV, KSV, QP_WAVES><<<G, QP_WAVES * 64, QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)P)
 #define CQ_QP_B(B) do { \
-            if (f16 && small) { CQ_QP(0, B, CQ_F16, 4, 4, g0, p0); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
+            if (f16 && small) { CQ_QP(0, B, CQ_F16, 3, 4, g0, p0); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
             else if (f16) { CQ_QP(0, B, CQ_F16, 2, 8, g0, p0); CQ_QP(1, B, CQ_F16, 2, 8, g1, p1); } \
             else if (small) { CQ_QP(0, B, CQ_F32, 2, 4, g0, p0); CQ_QP(1, B, CQ_F32, 2, 4, g1, p1); } \
             else { CQ_QP(0, B, CQ_F32, 2, 8, g0, p0); CQ_QP(1, B, CQ_F32, 2, 8, g1, p1); } } while (0)
