@@ -48,6 +48,10 @@ WORKLOADS = {
     "cfg3": dict(m=4096, n=11008, Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, lplr_iters=5, H=True,
                  batch=192, desc="BASELINE configs[2]: 4096x11008 fp16, activation-aware diag H (resampled "
                                 "diag_Hessians.pt down_proj entry), rank 128, Q_bits 2, L/R_bits 16, iters 5"),
+    "cfg4t": dict(m=11008, n=4096, Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, lplr_iters=5, H=False,
+                  batch=64, seed0=4, desc="BASELINE configs[3]'s tall gate/up shape: 11008x4096 fp16, rank 128, "
+                                          "Q_bits 2, L/R_bits 16, iters 5, H = I (matrix 0 = the golden run's "
+                                          "seed 4)"),
     "cfg5": dict(m=4096, n=4096, Q_bits=2, L_bits=4, R_bits=4, rank=256, iters=5, lplr_iters=10, H=False,
                  batch=256, desc="BASELINE configs[4]: 4096x4096 fp16, rank 256, Q_bits 2, L/R_bits 4, "
                                 "lplr_iters 10, iters 5, H = I"),
@@ -97,7 +101,8 @@ def parity_of_timed_step(name, decs, wl):
     """Relative Frobenius error (16-column Gaussian sketch) of Q + L R of the timed step's
     matrices 0-3 (seeds 0-3) against the reference's golden run of the same matrix."""
     g = golden()
-    tags = {"cfg2": ["cfg2", "cfg2s1", "cfg2s2", "cfg2s3"], "cfg3": ["cfg3"], "cfg5": ["cfg5"]}[name]
+    tags = {"cfg2": ["cfg2", "cfg2s1", "cfg2s2", "cfg2s3"], "cfg3": ["cfg3"], "cfg4t": ["cfg4t"],
+            "cfg5": ["cfg5"]}[name]
     out = {}
     for i, tag in enumerate(tags[:len(decs)]):
         d = decs[i]
@@ -115,7 +120,7 @@ def cpu_baseline(name, wl, dec0):
     on this host's threads; a bounded sample (all `iters` outer iterations for cfg2/cfg3, one
     outer iteration of cfg5's five, value scaled accordingly)."""
     from oracle import caldera_torch_cpu as T  # CPU baseline leg only
-    W0 = synth_W(wl, 0)
+    W0 = synth_W(wl, wl.get("seed0", 0))
     h = make_h(wl)
     iters = 1 if name == "cfg5" else wl["iters"]
     t0 = time.perf_counter()
@@ -270,7 +275,7 @@ def main():
     qp = make_params(wl)
     ep = EngineParams.from_caldera_params(qp)
     B = args.batch or wl["batch"]
-    Wb = synth_batch(wl, B, 1000 * rank, dev)
+    Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev)
     h = make_h(wl)
     h = None if h is None else h.to(dev)
     parts = max(1, args.streams or 1)

@@ -395,6 +395,13 @@ class CalderaEngine:
                     self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
                     self._ytl = scratch.get("lr.ytl", (B, n, m), torch.float16, dev)
                 halves.update(thi=self._yth, tlo=self._ytl)
+            # m > n: Y's own halves (K-blocked over n) for L = Y V on split-fp16 products
+            x3_yv = not sv.left and self.lplr_x3
+            if x3_yv:
+                if self._yrh is None:
+                    self._yrh = scratch.get("lr.yrh", (B, m, n), torch.float16, dev)
+                    self._yrl = scratch.get("lr.yrl", (B, m, n), torch.float16, dev)
+                halves.update(hi=self._yrh, lo=self._yrl)
             K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
                              ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
                              res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
@@ -414,6 +421,7 @@ class CalderaEngine:
         tiny = (S32 <= S32[:, :1] * 1e-30) | (S32 == 0)
         L = torch.empty((B, m, r), dtype=torch.float32, device=dev)
         R = torch.empty((B, r, n), dtype=torch.float32, device=dev)
+        yv2 = None  # ||Y V||^2 of the right-side Pythagorean error (m > n)
         if sv.left:
             U = vecs  # (B, m, r) view, ld p
             if p.activation_aware_LR:
@@ -443,15 +451,23 @@ class CalderaEngine:
         else:
             V = vecs  # (B, n, r)
             inv = torch.where(tiny, torch.zeros_like(S32), 1.0 / S32.clamp_min(1e-30))
+            # unit error weights (H = I, or not data-aware with h = 1) and unquantised factors:
+            # L R = Y V V^T in both branches below, so the error is ||Y||^2 - ||Y V||^2
+            # (Pythagoras, V orthonormal) from the Y V product the factors need anyway
+            pyth_right = (not quantized and not rand and not wts.dense and wts.ycol is None and wts.err_unit)
             if p.activation_aware_LR:
-                K.gemm(Ysrc, V, C=L)                 # Y V
+                self._y_times_v(sv, Ysrc, V, L)      # Y V
+                if pyth_right:
+                    yv2 = K.weighted_sqsum(L, None, r)
                 K.scale_rc(L, colscale=inv, out=L)   # U = Y V / S
                 K.scale_rc(V, trans=True, rowscale=S32, colscale=wts.rinv, out=R)  # S V^T diag(rinv)
                 if wts.dense:
                     R = K.gemm(R.clone(), wts.Vinv, tb=True, C=R)
             else:
                 sq = torch.sqrt(S32)
-                K.gemm(Ysrc, V, C=L)
+                self._y_times_v(sv, Ysrc, V, L)
+                if pyth_right:
+                    yv2 = K.weighted_sqsum(L, None, r)
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
                 K.scale_rc(V, trans=True, rowscale=sq, out=R)
         self._lplr_err2 = None
@@ -477,9 +493,32 @@ class CalderaEngine:
             ysq = K.weighted_sqsum(Ysrc, None, n) if ysq is None else ysq
             self._pyth = True  # run_iter recomputes small errors directly (cancellation)
             return ysq - K.weighted_sqsum(R, wts.err if wts.ycol is not None else None, n)
+        if yv2 is not None:
+            # ||res - L R||^2 = ||Y||^2 - ||Y V||^2 (unit weights, Y = res); small errors are
+            # recomputed directly by run_iter (cancellation), as for the left-side identity
+            ysq = K.weighted_sqsum(Ysrc, None, n) if ysq is None else ysq
+            self._pyth = True
+            return ysq - yv2
         err = torch.empty(B, dtype=torch.float64, device=dev)
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
+
+    def _y_times_v(self, sv, Ysrc, V, L):
+        """L = Y V (m > n; V = the first r columns of the solver's Ritz block, n x r): from Y's
+        K-blocked halves (written by cq_residual_split) as the split-fp16 product L^T = V^T Y^T
+        (A = the block's transposed split, rows r of p), transposed into L; the fp32 MFMA GEMM
+        when the halves are not there."""
+        if self._yrh is None or isinstance(sv, RandSVD) or sv.direct:
+            K.gemm(Ysrc, V, C=L)
+            return
+        X = sv.X
+        B, n, p = X.shape
+        r = L.shape[2]
+        xh, xl = sv.split_block_t(X)
+        Lt = torch.empty((B, r, L.shape[1]), dtype=torch.float32, device=L.device)
+        K.gemm_x3(xh, xl, self._yrh, self._yrl, 1.0 / (self._ys * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
+                  lda=p, M=r)
+        K.transpose_split(Lt, out=L)
 
     def _ut_y(self, sv, R):
         """R = U^T Y (U = the solver's Ritz block, first r columns; m <= n) as a split-fp16
@@ -740,6 +779,7 @@ class CalderaEngine:
         self._w_finite = None
         self._yh = self._yl = self._ys = None
         self._yth = self._ytl = None
+        self._yrh = self._yrl = None
         if wts.dense:  # den = tr(W H W^T) (alg.py:298)
             self._etmp = torch.empty((B, m, n), dtype=torch.float32, device=dev)
             wf = torch.empty((B, m, n), dtype=torch.float32, device=dev)
@@ -799,6 +839,7 @@ class CalderaEngine:
             self.solver.release()  # G, halves, blocks: ~300 MB per 4096^2 matrix
         self._yh = self._yl = None
         self._yth = self._ytl = None
+        self._yrh = self._yrl = None
         if host_copy is not None:
             Ws_out = host_copy()  # joins the copy thread: the host tensor
         out = self._finalize(best, st, W, Ws_out, gs, errors, wts, spare=(work, res))
