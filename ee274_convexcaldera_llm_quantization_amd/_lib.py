@@ -100,6 +100,8 @@ _SIGS = {
     "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_size, c_vp]),
+    "cq_tridiag_workspace": (c_size, [c_i64, c_i64]),
+    "cq_tridiag_eigh": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp, c_vp]),
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
                                  c_vp]),
@@ -494,6 +496,22 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
     _check(lib.cq_jacobi_eigh(_p(A), p, B, max_sweeps, tol, _p(ev), _p(V32), _p(V64), _p(sw), _p(ws),
                               ws.numel(), _stream(A.device)), "cq_jacobi_eigh")
     return ev, V32, V64, sw
+
+
+def tridiag_eigh(A: torch.Tensor, want_vectors: bool = True):
+    """A (B, p, p) fp64 symmetric, p <= 192 (not modified) -> (evals desc (B,p), V32 or None,
+    fallback): the tridiagonal path (cq_tridiag_eigh); fallback True means some matrix had a
+    near-degenerate pair and V32 must not be used (cq_jacobi_eigh reruns such batches)."""
+    _require_hip(A)
+    B, p, _ = A.shape
+    ev = torch.empty((B, p), dtype=torch.float64, device=A.device)
+    V32 = torch.empty((B, p, p), dtype=torch.float32, device=A.device) if want_vectors else None
+    lib = load()
+    ws = workspace(lib.cq_tridiag_workspace(p, B), A.device)
+    fb = ctypes.c_int(0)
+    _check(lib.cq_tridiag_eigh(_p(A), p, B, _p(ev), _p(V32), _p(ws), ws.numel(), ctypes.byref(fb),
+                               _stream(A.device)), "cq_tridiag_eigh")
+    return ev, V32, bool(fb.value)
 
 
 def ritz_residual(X, Z, theta, r):

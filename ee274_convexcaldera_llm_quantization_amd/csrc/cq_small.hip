@@ -1391,7 +1391,8 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
 
 size_t cq_jacobi_workspace(int64_t p, int64_t batch) {
     if (p > kBlockJacobiMinP) return cq::bj_workspace(p, batch);
-    return (size_t)batch * p * p * sizeof(double);
+    const size_t jac = (size_t)batch * p * p * sizeof(double);
+    return cq::trid_supported(p) ? std::max(jac, cq::trid_workspace(p, batch)) : jac;
 }
 
 int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals,
@@ -1407,6 +1408,21 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     const size_t l32 = jacobi_lds_bytes((int)p, 4), lreg = jacobi_reg_bytes((int)p);
     if (p > kBlockJacobiMinP)  // A does not fit one CU's LDS: block Jacobi over many workgroups
         return cq::bj_eigh(A, p, batch, max_sweeps, tol, evals, V32, V64, sweeps_out, ws, ws_bytes, s);
+    // opt-in (CQ_EIGH=trid), p <= 192 without fp64 vectors: Householder tridiagonalisation +
+    // bisection + twisted factorisations (cq_trid.hip); a batch with a near-degenerate pair runs
+    // the Jacobi below.  Not the default: ~4.5 ms per B = 256 call with vectors, 2.9 ms for
+    // values, against the Jacobi's 1-5 warm sweeps
+    static const bool use_trid = [] { const char* e = getenv("CQ_EIGH"); return e && e[0] == 't'; }();
+    if (!V64 && use_trid && cq::trid_supported(p)) {
+        int fallback = 0;
+        const int rc = cq::trid_eigh(A, p, batch, evals, V32, ws, ws_bytes, s, &fallback);
+        if (rc != 0) return rc;
+        if (!fallback) {
+            if (sweeps_out && hipMemsetD32Async(sweeps_out, 1, (size_t)batch, s) != hipSuccess)
+                return set_error(CQ_EHIP, "cq_jacobi_eigh: memset failed");
+            return 0;
+        }
+    }
     if (p <= 192 && lreg <= 160 * 1024) {
         // fp64 A in LDS, V in registers (no per-round memory traffic for V)
         if (p <= 64)

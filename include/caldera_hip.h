@@ -221,6 +221,16 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
                    double* evals, float* V32, double* V64, int* sweeps_out, void* ws,
                    size_t ws_bytes, void* stream);
 
+/* Symmetric eigendecomposition by Householder tridiagonalisation (fp64, A packed in one CU's
+ * LDS, p <= 192), bisection and twisted factorisations, same output contract as
+ * cq_jacobi_eigh (descending; V32 columns, may be NULL for values only; A not modified).
+ * *fallback = 1: some matrix has a pair of eigenvalues closer than 1e-9 of the norm, whose
+ * vectors this method does not orthogonalise -- V32 is then incomplete and the caller runs
+ * cq_jacobi_eigh.  cq_jacobi_eigh uses it itself when CQ_EIGH=trid is set. */
+size_t cq_tridiag_workspace(int64_t p, int64_t batch);
+int cq_tridiag_eigh(const double* A, int64_t p, int64_t batch, double* evals, float* V32, void* ws,
+                    size_t ws_bytes, int* fallback, void* stream);
+
 /* Ritz residuals: out[b] = max_{i<r} ||Z[:,i] - theta_i X[:,i]||_2 / |theta_0|
  * (X, Z: k x p row-major with ld p).  theta fp64 [b*p..]. */
 size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch);
