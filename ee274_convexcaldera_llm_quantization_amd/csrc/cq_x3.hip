@@ -14,6 +14,8 @@
 // MFMA blocks).  LDS images [row][k] with an 80-byte row stride (64 B data + 16 B pad) make
 // both the 16-byte stage writes and the ds_read_b128 fragment reads conflict-free; two
 // stages (140 KB) double-buffer the K loop with a register prefetch.
+#include <type_traits>
+
 #include "cq_common.h"
 
 namespace cq {
@@ -1060,6 +1062,7 @@ struct QUK {
     float* scale;                // [batch] out (pass 1)
     const float* ew;             // error column weights [n] or NULL (= 1)
     double* part;                // [batch * tiles] error partials
+    const uint32_t* nrm;         // [batch * 4] max row norms of L hi/lo, R^T hi/lo (float bits), or NULL
 };
 
 template <int PASS, int BITS>
@@ -1805,14 +1808,80 @@ __device__ __forceinline__ f16x8g qp_frag(const _Float16* stage, int half, int r
     return *reinterpret_cast<const f16x8g*>(stage + (half * QP_BN + row) * QP_ROW + 8 * (chunk ^ qp_swz(row)));
 }
 
+// Largest row norms of the factor halves, per matrix: out[4 b + 0..3] = max_i ||Lh_i||,
+// max_i ||Ll_i||, max_j ||Rh_j||, max_j ||Rl_j|| (R^T rows), as float bits (atomicMax on
+// non-negative floats), each rounded up by 2^-10 (covers the fp32 sum of K <= 256 squares).
+// They bound how far the hi x hi product can sit from the split product (approximate pass 0).
+__global__ __launch_bounds__(256) void qp_norms_kernel(const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
+                                                       const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl,
+                                                       int64_t m, int64_t n, int K, uint32_t* __restrict__ out) {
+    // 16 lanes per row (16-byte loads, coalesced), 16 rows per block step, a grid-stride loop
+    // over rows and one atomic per block and value (same-address atomics serialise)
+    const int64_t b = blockIdx.y;
+    const int sub = threadIdx.x & 15;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); i < m + n; i += (int64_t)gridDim.x * 16) {
+        const bool isR = i >= m;
+        const int64_t row = isR ? i - m : i;
+        const uint16_t* ph = (isR ? Rh + b * n * (int64_t)K : Lh + b * m * (int64_t)K) + row * K;
+        const uint16_t* pl = (isR ? Rl + b * n * (int64_t)K : Ll + b * m * (int64_t)K) + row * K;
+        float sh = 0.f, sl = 0.f;
+        for (int k = 8 * sub; k < K; k += 128) {
+            const f16x8g h = *reinterpret_cast<const f16x8g*>(ph + k);
+            const f16x8g l = *reinterpret_cast<const f16x8g*>(pl + k);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float a = (float)h[e], c = (float)l[e];
+                sh += a * a;
+                sl += c * c;
+            }
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) {   // the row's 16 lanes (aligned groups of 16)
+            sh += __shfl_xor(sh, off, 64);
+            sl += __shfl_xor(sl, off, 64);
+        }
+        const int t = isR ? 2 : 0;
+        v[t] = fmaxf(v[t], sqrtf(sh) * (1.f + 0x1p-10f));
+        v[t + 1] = fmaxf(v[t + 1], sqrtf(sl) * (1.f + 0x1p-10f));
+    }
+    __shared__ uint32_t red[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t mx = wave_max_u32(__float_as_uint(v[t]));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const uint32_t mx = max(max(red[0][threadIdx.x], red[1][threadIdx.x]), max(red[2][threadIdx.x], red[3][threadIdx.x]));
+        if (mx) atomicMax(out + 4 * b + threadIdx.x, mx);
+    }
+}
+
 // RB row-blocks of 16 rows per wave; K = r <= 32 KSMAX.  FAST (pass 1): the scale is a
 // finite normal number and |res| <= scale, so x / s and c / k take the branch-free correctly
 // rounded division (div_fast; same results as IEEE division), and 2-bit dequantisation is
-// c * s (k = 1: (c / 1) * s is exactly c * s).
-template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, int NW>
+// c * s (k = 1: (c / 1) * s is exactly c * s).  The per-element arithmetic runs on packed
+// fp32 pairs (v_pk_mul/add/fma_f32: two elements per VALU issue, each rounded as the scalar
+// op would be), so pass 1's epilogue costs about half the VALU issue slots.
+//
+// AP (pass 0 only): approximate absmax with an exact fix-up.  The chunk's residual is first
+// formed from the hi x hi product alone (one MFMA instead of three); q.nrm bounds how far any
+// such value v' can sit from the split-product value v: |v - v'| <= e (Cauchy-Schwarz on the
+// dropped hi x lo and lo x hi terms, plus the fp32 accumulation and rounding terms).  The wave
+// keeps rw = max |v'| seen so far (a lower bound of the matrix's max |v'|, M').  The element
+// holding the exact max |v| has |v'| >= M' - 2e >= rw - 2e, so a chunk with no element at or
+// above rw - 2e cannot hold it; every other chunk (the first one, and a handful of running-
+// max records after it) is recomputed with the split product, in exactly pass 1's MFMA order,
+// and only those exact values enter the max.  So the max, hence the scale and every code,
+// is bit-identical to the exact pass.
+typedef float qf2 __attribute__((ext_vector_type(2)));
+
+template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, bool AP, int NW>
 __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
                                         const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl, int K,
                                         int panels, _Float16* smem) {
+    static_assert(!AP || PASS == 0, "approximate absmax is a pass-0 mode");
     constexpr int ROWS = NW * 16 * RB;
     constexpr int WV = DT == CQ_F16 ? 1 : 2;        // uint4 per lane-run of 8 W elements
     const int64_t m = q.m, n = q.n, MN = m * n;
@@ -1858,6 +1927,18 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const float ys = 1.f / s, yk = 1.f / kq;
     uint32_t mx = 0;
     double err = 0.0;
+    // AP: e2 = 2 e, e bounding |v - v'| for every element of this matrix (see above)
+    float e2 = 0.f;
+    uint32_t rw = 0;   // AP: wave-uniform running max of |v'| (float bits)
+    if constexpr (AP) {
+        const float nLh = __uint_as_float(q.nrm[4 * b]), nLl = __uint_as_float(q.nrm[4 * b + 1]);
+        const float nRh = __uint_as_float(q.nrm[4 * b + 2]), nRl = __uint_as_float(q.nrm[4 * b + 3]);
+        const float cross = nLh * nRl + nLl * nRh;                 // the dropped hi x lo, lo x hi terms
+        const float gam = (float)(4 * K + 64) * 0x1p-24f;         // fp32 accumulation of both sums
+        const float eacc = (cross + gam * (nLh * nRh + cross)) * (1.f + 0x1p-8f);
+        e2 = 2.f * (sc * eacc * (1.f + 0x1p-8f)) + 0x1p-120f;
+        if (!(e2 < 0x1p100f)) e2 = __builtin_inff();              // non-finite factors: all exact
+    }
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -1876,21 +1957,10 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             }
         }
     };
-    // chunk body: R^T stage of chunk ch+1 and W of chunk `wload_ch` are issued at its start,
-    // its own W (wc) was loaded earlier.  Pass 0 (absmax: no stores in the loop) keeps W two
-    // chunks ahead (three register buffers, rotated by unrolling the loop by 3, so no in-flight
-    // destination is ever copied): at the end-of-chunk wait W(ch+2) is the wave's most recent
-    // vector-memory traffic and vmcnt(RB * WV) retires only the next R^T stage.  Pass 1 stores
-    // codes in the loop and keeps one chunk ahead (two buffers).
-    constexpr int WAHEAD = PASS == 0 ? 2 : 1;
-    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV]) {
-        const int64_t n0 = ch * QP_BN;
-        if (ch + 1 < nchunks)  // next chunk's R^T (LDS-DMA) in flight during this chunk
-            qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
-        const bool wlive = ch + WAHEAD < nchunks;
-        if (wlive) load_w(n0 + WAHEAD * QP_BN, wl);
-        const _Float16* st = smem + (ch & 1) * QP_STAGE;
-        f32x4v acc[RB][2];
+    // the chunk's products: acc[rb][c][i] is (W row row0 + 16 rb + l16, column n0 + 8 lq + 4 c + i);
+    // split: al x lh, ah x ll, ah x lh per K step (the one order both passes use); else ah x lh
+    auto mma = [&](auto split_c, const _Float16* st, f32x4v (&acc)[RB][2]) {
+        constexpr bool split = decltype(split_c)::value;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -1902,94 +1972,172 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     ah[c] = qp_frag(st, 0, acol0 + 4 * c, 4 * ks + lq);
-                    al[c] = qp_frag(st, 1, acol0 + 4 * c, 4 * ks + lq);
+                    if (split) al[c] = qp_frag(st, 1, acol0 + 4 * c, 4 * ks + lq);
                 }
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
-                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[c], ll[rb][ks], acc[rb][c], 0, 0, 0);
+                        if (split) {
+                            acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
+                            acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[c], ll[rb][ks], acc[rb][c], 0, 0, 0);
+                        }
                         acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
                     }
             }
         }
-        // epilogue: acc[rb][c][i] is (W row row0 + 16 rb + l16, column n0 + 8 lq + 4 c + i)
+    };
+    // res = W - L R (alg.py:262) of row block rb as 4 pairs: v[p] = elements 2p, 2p + 1
+    auto resid = [&](const uint4 (&wc)[RB][WV], const f32x4v (&acc)[RB][2], int rb, qf2 (&v)[4]) {
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const int64_t row = row0 + 16 * rb + l16;
-            if (row >= m) continue;
-            const int64_t e = row * n + n0 + 8 * lq;
-            float v[8];
+        for (int p = 0; p < 4; ++p) {
+            qf2 w;
+            if (DT == CQ_F16) {
+                const uint32_t pr = (&wc[rb][0].x)[p];
+                w = qf2{(float)__builtin_bit_cast(_Float16, (uint16_t)(pr & 0xffffu)),
+                        (float)__builtin_bit_cast(_Float16, (uint16_t)(pr >> 16))};
+            } else {
+                const uint32_t* wp = &wc[rb][(p >> 1) & (WV - 1)].x;
+                w = qf2{__uint_as_float(wp[2 * (p & 1)]), __uint_as_float(wp[2 * (p & 1) + 1])};
+            }
+            const int c = p >> 1, i = 2 * (p & 1);
+            v[p] = w - qf2{acc[rb][c][i], acc[rb][c][i + 1]} * sc;
+        }
+    };
+    auto vmax = [&](const qf2 (&v)[4], uint32_t cur) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
+        for (int p = 0; p < 4; ++p) cur = max(cur, max(abs_bits(v[p].x), abs_bits(v[p].y)));
+        return cur;
+    };
+    // chunk body: R^T stage of chunk ch+1 and W of chunk ch + WAHEAD are issued at its start,
+    // its own W (wc) was loaded earlier.  Pass 0 (absmax: no stores in the loop) keeps W two
+    // chunks ahead (three register buffers, rotated by unrolling the loop by 3, so no in-flight
+    // destination is ever copied): at the end-of-chunk wait W(ch+2) is the wave's most recent
+    // vector-memory traffic and vmcnt(RB * WV) retires only the next R^T stage.  Pass 1 stores
+    // codes in the loop and keeps one chunk ahead (two buffers).  (A 3-slot R^T ring two
+    // chunks ahead, with pass 1's packed stores deferred to the next chunk so a counted wait
+    // could leave R(ch+2) in flight, measured slower: pass 0 3.13 vs 3.20 ms, pass 1 5.77 vs
+    // 5.02 ms per B = 256 call -- the passes are not waiting on the R^T stages.)
+    constexpr int WAHEAD = PASS == 0 ? 2 : 1;
+    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV]) {
+        const int64_t n0 = ch * QP_BN;
+        if (ch + 1 < nchunks)  // next chunk's R^T (LDS-DMA) in flight during this chunk
+            qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
+        const bool wlive = ch + WAHEAD < nchunks;
+        if (wlive) load_w(n0 + WAHEAD * QP_BN, wl);
+        const _Float16* st = smem + (ch & 1) * QP_STAGE;
+        f32x4v acc[RB][2];
+        if constexpr (AP) {
+            mma(std::false_type{}, st, acc);
+            uint32_t lm = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int u = 4 * c + i;
-                    float w;
-                    if (DT == CQ_F16) {
-                        const uint32_t pr = (&wc[rb][0].x)[u >> 1];
-                        w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
-                    } else {
-                        w = __uint_as_float((&wc[rb][(u >> 2) & (WV - 1)].x)[u & 3]);
-                    }
-                    v[u] = w - acc[rb][c][i] * sc;   // res = W - L R (alg.py:262)
+            for (int rb = 0; rb < RB; ++rb) {
+                if (row0 + 16 * rb + l16 >= m) continue;
+                qf2 v[4];
+                resid(wc, acc, rb, v);
+                lm = vmax(v, lm);
+            }
+            // thr <= rw - 2e - 2^-18 rw (the last term covers the roundings of v and thr)
+            const float thr = __uint_as_float(rw) * (1.f - 0x1p-18f) - e2;
+            const bool cand = lm >= 0x7f800000u || rw >= 0x7f800000u || __uint_as_float(lm) >= thr;
+            if (__any(cand)) {
+                rw = max(rw, wave_max_u32(lm));
+                mma(std::true_type{}, st, acc);
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) {
+                    if (row0 + 16 * rb + l16 >= m) continue;
+                    qf2 v[4];
+                    resid(wc, acc, rb, v);
+                    mx = vmax(v, mx);
                 }
-            if (PASS == 0) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) mx = max(mx, abs_bits(v[u]));
-                continue;
             }
-            int cq8[8];
+        } else {
+            mma(std::true_type{}, st, acc);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                float e4[4];
-                float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
-                if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + n0 + 8 * lq + 4 * h);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float x = v[4 * h + i];
-                    float c, dq;
-                    if (FAST) {
-                        c = rintf(div_fast(x, s, ys) * kq);
-                        dq = BITS == 2 ? c * s : div_fast(c, kq, yk) * s;
-                    } else {
-                        c = quant_code_r(x, s, ys, kq);
-                        dq = dequant_r(c, kq, yk, s);
-                    }
-                    const float d = dq - x;
-                    e4[i] = (d * d) * (&wv.x)[i];
-                    cq8[4 * h + i] = (int)c;
+            for (int rb = 0; rb < RB; ++rb) {
+                const int64_t row = row0 + 16 * rb + l16;
+                if (row >= m) continue;
+                const int64_t e = row * n + n0 + 8 * lq;
+                qf2 v[4];
+                resid(wc, acc, rb, v);
+                if (PASS == 0) {
+                    mx = vmax(v, mx);
+                    continue;
                 }
-                err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
-            }
-            if (BITS == 2 && q.packed) {  // bytes: codes 0-3, 4-7, MSB-first offset binary (c + 1)
-                uint32_t w16 = 0;
+                qf2 cf[4];   // codes (integral floats), pairs as v
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    w16 |= (((uint32_t)(cq8[4 * h] + 1) << 6) | ((uint32_t)(cq8[4 * h + 1] + 1) << 4) |
-                            ((uint32_t)(cq8[4 * h + 2] + 1) << 2) | (uint32_t)(cq8[4 * h + 3] + 1)) << (8 * h);
-                *reinterpret_cast<uint16_t*>(q.packed + (b * MN + e) / 4) = (uint16_t)w16;
-            } else if (BITS == 4 && q.packed) {
-                uint32_t w32 = 0;
+                for (int h = 0; h < 2; ++h) {
+                    qf2 e4[2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    w32 |= (((uint32_t)(cq8[2 * j] + 7) << 4) | (uint32_t)(cq8[2 * j + 1] + 7)) << (8 * j);
-                *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 2) = w32;
-            }
-            if (q.codes) {
-                if (BITS <= 8) {
-                    uint32_t c0 = 0, c1 = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        c0 |= (uint32_t)(uint8_t)(int8_t)cq8[j] << (8 * j);
-                        c1 |= (uint32_t)(uint8_t)(int8_t)cq8[4 + j] << (8 * j);
+                    for (int t = 0; t < 2; ++t) {
+                        const qf2 x = v[2 * h + t];
+                        qf2 c, dq;
+                        if (FAST) {
+                            // div_fast on the pair: q = x y, r = x - q s (FMA), q + r y
+                            const qf2 qd = x * ys;
+                            const qf2 rr = __builtin_elementwise_fma(-qd, qf2{s, s}, x);
+                            const qf2 z = __builtin_elementwise_fma(rr, qf2{ys, ys}, qd) * kq;
+                            c = qf2{rintf(z.x), rintf(z.y)};
+                            if (BITS == 2) {
+                                dq = c * s;
+                            } else {
+                                const qf2 qk = c * yk;
+                                const qf2 rk = __builtin_elementwise_fma(-qk, qf2{kq, kq}, c);
+                                dq = __builtin_elementwise_fma(rk, qf2{yk, yk}, qk) * s;
+                            }
+                        } else {
+                            c = qf2{quant_code_r(x.x, s, ys, kq), quant_code_r(x.y, s, ys, kq)};
+                            dq = qf2{dequant_r(c.x, kq, yk, s), dequant_r(c.y, kq, yk, s)};
+                        }
+                        const qf2 d = dq - x;
+                        e4[t] = d * d;
+                        cf[2 * h + t] = c;
                     }
-                    *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) = make_uint2(c0, c1);
-                } else {
-                    int16_t* cp = reinterpret_cast<int16_t*>(q.codes) + b * MN + e;
-                    *reinterpret_cast<short4*>(cp) = make_short4((short)cq8[0], (short)cq8[1], (short)cq8[2], (short)cq8[3]);
-                    *reinterpret_cast<short4*>(cp + 4) = make_short4((short)cq8[4], (short)cq8[5], (short)cq8[6], (short)cq8[7]);
+                    if (q.ew) {  // error column weights (activation-aware error, alg.py:286-302)
+                        const float4 wv = *reinterpret_cast<const float4*>(q.ew + n0 + 8 * lq + 4 * h);
+                        e4[0] = e4[0] * qf2{wv.x, wv.y};
+                        e4[1] = e4[1] * qf2{wv.z, wv.w};
+                    }
+                    err += (double)((e4[0].x + e4[0].y) + (e4[1].x + e4[1].y));  // fp32 within a run of 4, fp64 across
+                }
+                if (BITS == 2 && q.packed) {
+                    // bytes: codes 0-3, 4-7, MSB-first offset binary (c + 1): element u's code
+                    // has weight 2^(8 (u / 4) + 6 - 2 (u % 4)); the sum of (c_u + 1) times these
+                    // weights is an integer below 2^16, exact in fp32 (four packed FMAs)
+                    constexpr float wt[8] = {64.f, 16.f, 4.f, 1.f, 16384.f, 4096.f, 1024.f, 256.f};
+                    qf2 acc2 = qf2{wt[0] + wt[2] + wt[4] + wt[6], wt[1] + wt[3] + wt[5] + wt[7]};
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+                        acc2 = __builtin_elementwise_fma(cf[p], qf2{wt[2 * p], wt[2 * p + 1]}, acc2);
+                    const uint32_t w16 = (uint32_t)(acc2.x + acc2.y);
+                    *reinterpret_cast<uint16_t*>(q.packed + (b * MN + e) / 4) = (uint16_t)w16;
+                }
+                int cq8[8];
+                if (q.codes || (BITS == 4 && q.packed)) {
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) { cq8[2 * p] = (int)cf[p].x; cq8[2 * p + 1] = (int)cf[p].y; }
+                }
+                if (BITS == 4 && q.packed) {
+                    uint32_t w32 = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        w32 |= (((uint32_t)(cq8[2 * j] + 7) << 4) | (uint32_t)(cq8[2 * j + 1] + 7)) << (8 * j);
+                    *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 2) = w32;
+                }
+                if (q.codes) {
+                    if (BITS <= 8) {
+                        uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            c0 |= (uint32_t)(uint8_t)(int8_t)cq8[j] << (8 * j);
+                            c1 |= (uint32_t)(uint8_t)(int8_t)cq8[4 + j] << (8 * j);
+                        }
+                        *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e) = make_uint2(c0, c1);
+                    } else {
+                        int16_t* cp = reinterpret_cast<int16_t*>(q.codes) + b * MN + e;
+                        *reinterpret_cast<short4*>(cp) = make_short4((short)cq8[0], (short)cq8[1], (short)cq8[2], (short)cq8[3]);
+                        *reinterpret_cast<short4*>(cp + 4) = make_short4((short)cq8[4], (short)cq8[5], (short)cq8[6], (short)cq8[7]);
+                    }
                 }
             }
         }
@@ -2033,7 +2181,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
 }
 
-template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW>
+template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW, bool AP = false>
 __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uint16_t* __restrict__ Lh,
                                                                    const uint16_t* __restrict__ Ll,
                                                                    const uint16_t* __restrict__ Rh,
@@ -2042,7 +2190,7 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
     extern __shared__ __attribute__((aligned(16))) char qp_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(qp_smem_raw);
     if (PASS == 0) {
-        qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+        qp_body<PASS, BITS, DT, RB, KSMAX, false, AP, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
         return;
     }
     // which matrix this workgroup serves (same mapping as qp_body) decides the division path
@@ -2051,8 +2199,8 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
     const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
     const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
     const float sb = quant_scale(q.absmax[lin / panels], q.eps);
-    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
-    else qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    else qp_body<PASS, BITS, DT, RB, KSMAX, false, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
 }
 constexpr size_t QP_LDS_BYTES = (size_t)2 * QP_STAGE * sizeof(_Float16);  // 64 KB
 
@@ -2130,11 +2278,17 @@ int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch
 }
 
 
+static int64_t qu_tiles(int64_t m, int64_t n) {
+    return std::max(ceil_div(n, XW_BM) * ceil_div(m, XW_BN), ceil_div(m, XW_BM) * ceil_div(n, XW_BN));
+}
+
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
     // tile counts of both Q-update kernels (q_update_v_kernel tiles W as m x n, the 32x32
     // kernel as n x m)
-    const int64_t tiles = std::max(ceil_div(n, XW_BM) * ceil_div(m, XW_BN), ceil_div(m, XW_BM) * ceil_div(n, XW_BN));
-    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) + (size_t)batch * tiles * sizeof(double);
+    const int64_t tiles = qu_tiles(m, n);
+    // absmax bits | error partials | factor-half row norms (approximate absmax pass)
+    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) +
+           align_up((size_t)batch * tiles * sizeof(double), 256) + (size_t)batch * 4 * sizeof(uint32_t);
 }
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
@@ -2185,7 +2339,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     q.W = W; q.wf16 = dtype == CQ_F16; q.m = m; q.n = n;
     q.absmax = reinterpret_cast<uint32_t*>(ws);
     q.part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + align_up((size_t)batch * sizeof(uint32_t), 256));
-    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w;
+    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w; q.nrm = nullptr;
     hipStream_t s = as_stream(stream);
     const bool known = absmax_in && r == 0;  // max|W| bits given: skip the absmax pass
     if (known) {
@@ -2213,13 +2367,33 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
         const uint16_t *lh = Lh, *ll = Ll, *rh = Rth, *rl = Rtl;
         const int Ki = (int)r;
         const unsigned g0 = (unsigned)(p0 * batch), g1 = (unsigned)(p1 * batch);
+        // CQ_QP0_APPROX=1: pass 0 on the hi x hi product with an exact fix-up of the candidate
+        // chunks (qp_body, AP).  Bit-identical max, but measured no faster (3.13-3.20 vs 3.3 ms
+        // per B = 256 call, plus the row-norm kernel): the pass is bound by its W stream (64 B
+        // per row per chunk), not by the MFMAs, so the split product stays the default.
+        static const bool approx0 = getenv("CQ_QP0_APPROX") != nullptr;
+        const bool ap = approx0 && (f16 || small);   // (fp32 W past r = 128: no VGPRs to spare)
+        if (ap) {
+            uint32_t* nrm = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(q.part) +
+                                                        align_up((size_t)batch * qu_tiles(m, n) * sizeof(double), 256));
+            if (hipMemsetAsync(nrm, 0, (size_t)batch * 4 * sizeof(uint32_t), s) != hipSuccess)
+                return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
+            CQ_REQUIRE(batch < 65536, "cq_q_update_x3: batch too large");
+            qp_norms_kernel<<<dim3((unsigned)std::min<int64_t>(32, ceil_div(m + n, 16)), (unsigned)batch), 256, 0, s>>>(lh, ll, rh, rl, m, n,
+                                                                                                  Ki, nrm);
+            q.nrm = nrm;
+        }
 #define CQ_QP(PS, B, DTV, RBV, KSV, G, P) \
         q_update_p_kernel<PS, B, DTV, RBV, KSV, QP_WAVES><<<G, QP_WAVES * 64, QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)P)
+#define CQ_QP0(B, DTV, RBV, KSV) do { \
+            if (ap) q_update_p_kernel<0, B, DTV, RBV, KSV, QP_WAVES, true><<<g0, QP_WAVES * 64, QP_LDS_BYTES, s>>>( \
+                q, lh, ll, rh, rl, Ki, (int)p0); \
+            else CQ_QP(0, B, DTV, RBV, KSV, g0, p0); } while (0)
 #define CQ_QP_B(B) do { \
-            if (f16 && small) { CQ_QP(0, B, CQ_F16, 3, 4, g0, p0); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
-            else if (f16) { CQ_QP(0, B, CQ_F16, 2, 8, g0, p0); CQ_QP(1, B, CQ_F16, 2, 8, g1, p1); } \
-            else if (small) { CQ_QP(0, B, CQ_F32, 2, 4, g0, p0); CQ_QP(1, B, CQ_F32, 2, 4, g1, p1); } \
-            else { CQ_QP(0, B, CQ_F32, 2, 8, g0, p0); CQ_QP(1, B, CQ_F32, 2, 8, g1, p1); } } while (0)
+            if (f16 && small) { CQ_QP0(B, CQ_F16, 3, 4); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
+            else if (f16) { CQ_QP0(B, CQ_F16, 2, 8); CQ_QP(1, B, CQ_F16, 2, 8, g1, p1); } \
+            else if (small) { CQ_QP0(B, CQ_F32, 2, 4); CQ_QP(1, B, CQ_F32, 2, 4, g1, p1); } \
+            else { CQ_QP0(B, CQ_F32, 2, 8); CQ_QP(1, B, CQ_F32, 2, 8, g1, p1); } } while (0)
         switch (bits) {
             case 2: CQ_QP_B(2); break;
             case 4: CQ_QP_B(4); break;
@@ -2227,6 +2401,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
             default: CQ_QP_B(16); break;
         }
 #undef CQ_QP_B
+#undef CQ_QP0
 #undef CQ_QP
         q_update_finalize_kernel<<<(unsigned)batch, 64, 0, s>>>(q.absmax, q.part, p1, batch, eps, scale_out, err_out);
         return check_launch("cq_q_update_x3");
