@@ -1877,7 +1877,7 @@ __global__ __launch_bounds__(256) void qp_norms_kernel(const uint16_t* __restric
 // is bit-identical to the exact pass.
 typedef float qf2 __attribute__((ext_vector_type(2)));
 
-template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, bool AP, int NW>
+template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, bool AP, int NW, bool PW = false>
 __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
                                         const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl, int K,
                                         int panels, _Float16* smem) {
@@ -2018,13 +2018,31 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     // chunks ahead, with pass 1's packed stores deferred to the next chunk so a counted wait
     // could leave R(ch+2) in flight, measured slower: pass 0 3.13 vs 3.20 ms, pass 1 5.77 vs
     // 5.02 ms per B = 256 call -- the passes are not waiting on the R^T stages.)
+    //
+    // PW (pass 0): W in pairs of chunks.  A wave's W load covers 16 rows x 64 B of one chunk,
+    // so consecutive chunks hit each row's 128-B line (and DRAM page) a chunk apart; with PW
+    // an even chunk ch issues W(ch+2) and W(ch+3) back to back (each row's 128 B together;
+    // four register buffers, loop unrolled by 4) and an odd chunk issues none.  End-of-chunk
+    // waits: even, vmcnt(2 nW) (or nW past the end) leaves both in flight and retires R(ch+1)
+    // and W(ch+1) (issued two chunks earlier); odd, vmcnt(0).
     constexpr int WAHEAD = PASS == 0 ? 2 : 1;
-    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV]) {
+    static_assert(!PW || PASS == 0, "paired W loads are a pass-0 mode");
+    int nwl = 0;   // PW: W chunks issued by this chunk
+    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV], uint4 (&wl2)[RB][WV]) {
         const int64_t n0 = ch * QP_BN;
         if (ch + 1 < nchunks)  // next chunk's R^T (LDS-DMA) in flight during this chunk
             qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
         const bool wlive = ch + WAHEAD < nchunks;
-        if (wlive) load_w(n0 + WAHEAD * QP_BN, wl);
+        if constexpr (PW) {
+            nwl = 0;
+            if ((ch & 1) == 0 && wlive) {
+                load_w(n0 + 2 * QP_BN, wl);
+                nwl = 1;
+                if (ch + 3 < nchunks) { load_w(n0 + 3 * QP_BN, wl2); nwl = 2; }
+            }
+        } else if (wlive) {
+            load_w(n0 + WAHEAD * QP_BN, wl);
+        }
         const _Float16* st = smem + (ch & 1) * QP_STAGE;
         f32x4v acc[RB][2];
         if constexpr (AP) {
@@ -2141,9 +2159,13 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 }
             }
         }
-        if (PASS == 0 && wlive) {
-            // vmcnt in bits [3:0] and [15:14]; expcnt / lgkmcnt at their maxima (not waited)
-            constexpr int nw = RB * WV;
+        // vmcnt in bits [3:0] and [15:14]; expcnt / lgkmcnt at their maxima (not waited)
+        constexpr int nw = RB * WV;
+        if (PW && nwl == 2) {
+            __builtin_amdgcn_s_waitcnt(((2 * nw) & 15) | (((2 * nw) >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        } else if (PW && nwl == 1) {
+            __builtin_amdgcn_s_waitcnt((nw & 15) | ((nw >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        } else if (!PW && PASS == 0 && wlive) {
             __builtin_amdgcn_s_waitcnt((nw & 15) | ((nw >> 4) << 14) | (0x7 << 4) | (0xF << 8));
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2151,20 +2173,28 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
     };
     uint4 w3[PASS == 0 ? RB : 1][WV];
+    uint4 w4[PW ? RB : 1][WV];
     qp_issue_r<NW>(Rhb, Rlb, 0, K, smem, wid, lane);
     load_w(0, wr);
     if (PASS == 0 && nchunks > 1) load_w(QP_BN, wn);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if constexpr (PASS == 0) {
+    if constexpr (PW) {
+        for (int64_t ch = 0; ch < nchunks; ch += 4) {
+            chunk(ch, wr, w3, w4);
+            if (ch + 1 < nchunks) chunk(ch + 1, wn, wn, wn);   // (odd chunks load nothing)
+            if (ch + 2 < nchunks) chunk(ch + 2, w3, wr, wn);
+            if (ch + 3 < nchunks) chunk(ch + 3, w4, w4, w4);
+        }
+    } else if constexpr (PASS == 0) {
         for (int64_t ch = 0; ch < nchunks; ch += 3) {
-            chunk(ch, wr, w3);
-            if (ch + 1 < nchunks) chunk(ch + 1, wn, wr);
-            if (ch + 2 < nchunks) chunk(ch + 2, w3, wn);
+            chunk(ch, wr, w3, w3);
+            if (ch + 1 < nchunks) chunk(ch + 1, wn, wr, wr);
+            if (ch + 2 < nchunks) chunk(ch + 2, w3, wn, wn);
         }
     } else {
         for (int64_t ch = 0; ch < nchunks; ++ch) {
-            chunk(ch, wr, wn);
+            chunk(ch, wr, wn, wn);
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2181,7 +2211,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
 }
 
-template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW, bool AP = false>
+template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW, bool AP = false, bool PW = false>
 __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uint16_t* __restrict__ Lh,
                                                                    const uint16_t* __restrict__ Ll,
                                                                    const uint16_t* __restrict__ Rh,
@@ -2190,7 +2220,7 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
     extern __shared__ __attribute__((aligned(16))) char qp_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(qp_smem_raw);
     if (PASS == 0) {
-        qp_body<PASS, BITS, DT, RB, KSMAX, false, AP, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+        qp_body<PASS, BITS, DT, RB, KSMAX, false, AP, NW, PW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
         return;
     }
     // which matrix this workgroup serves (same mapping as qp_body) decides the division path
@@ -2373,6 +2403,9 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
         // per row per chunk), not by the MFMAs, so the split product stays the default.
         static const bool approx0 = getenv("CQ_QP0_APPROX") != nullptr;
         const bool ap = approx0 && (f16 || small);   // (fp32 W past r = 128: no VGPRs to spare)
+        // CQ_QP0_PAIRW=1: pass 0 loads W in pairs of chunks (qp_body, PW; fp16 W, r <= 128)
+        static const bool pairw = getenv("CQ_QP0_PAIRW") != nullptr;
+        const bool pw = pairw && f16 && small;
         if (ap) {
             uint32_t* nrm = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(q.part) +
                                                         align_up((size_t)batch * qu_tiles(m, n) * sizeof(double), 256));
@@ -2388,6 +2421,8 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
 #define CQ_QP0(B, DTV, RBV, KSV) do { \
             if (ap) q_update_p_kernel<0, B, DTV, RBV, KSV, QP_WAVES, true><<<g0, QP_WAVES * 64, QP_LDS_BYTES, s>>>( \
                 q, lh, ll, rh, rl, Ki, (int)p0); \
+            else if (pw) q_update_p_kernel<0, B, DTV, RBV, KSV, QP_WAVES, false, true><<<g0, QP_WAVES * 64, \
+                QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)p0); \
             else CQ_QP(0, B, DTV, RBV, KSV, g0, p0); } while (0)
 #define CQ_QP_B(B) do { \
             if (f16 && small) { CQ_QP0(B, CQ_F16, 3, 4); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
