@@ -8,8 +8,10 @@ alg.py:24-112) over B matrices resident in HBM.
                   [--no-cpu-baseline] [--no-parity] [--no-api-path]
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank decomposes
-its own batch (matrices are independent: weak scaling, no data-path collective); the
-timed region is bracketed by barrier + synchronize and the max over ranks is reported.
+its own batch (matrices are independent: weak scaling) and, inside each timed step, its
+packed results (2-bit codes, L, R, scales) are gathered to rank 0 over RCCL -- the one
+collective of the path; the timed region is bracketed by barrier + synchronize and the max
+over ranks is reported.
 
 Prints ONE JSON line (rank 0) with value = matrices/s over all ranks, the roofline of the
 dominant kernel (timed with HIP events on its stream inside the timed region), parity of the
@@ -99,19 +101,42 @@ def _sketch(Q, L, R, n):
 
 def parity_of_timed_step(name, decs, wl):
     """Relative Frobenius error (16-column Gaussian sketch) of Q + L R of the timed step's
-    matrices 0-3 (seeds 0-3) against the reference's golden run of the same matrix."""
+    matrices against the reference's golden run of the same matrix, and their final integer
+    codes against the reference's (tests/final_codes.py: bit-exact, or every flip at a
+    reference near-tie).  cfg2: batch positions 0-15 = seeds 0-15 (tests/golden/final_codes.npz,
+    with the reference's own 4- vs 8-thread spread per seed); cfg3 / cfg4t / cfg5: matrix 0."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from final_codes import compare, fixture
+    fx = fixture()
     g = golden()
-    tags = {"cfg2": ["cfg2", "cfg2s1", "cfg2s2", "cfg2s3"], "cfg3": ["cfg3"], "cfg4t": ["cfg4t"],
-            "cfg5": ["cfg5"]}[name]
-    out = {}
+    if name == "cfg2":
+        tags = ["cfg2"] + [f"cfg2s{s}" for s in range(1, 16)]
+        tags = [t for t in tags if f"{t}_sketch_QLR" in fx.files]
+        code_tags = tags
+    else:
+        tags = {"cfg3": ["cfg3"], "cfg4t": ["cfg4t"], "cfg5": ["cfg5"]}[name]
+        code_tags = {"cfg3": ["cfg3"], "cfg4t": ["cfg4t"], "cfg5": ["cfg5r"]}[name]
+    out, codes = {}, {}
     for i, tag in enumerate(tags[:len(decs)]):
         d = decs[i]
         sk = _sketch(d["Q"], d["L"], d["R"], wl["n"])
-        ref = g[f"{tag}_sketch_QLR"]
+        ref = fx[f"{tag}_sketch_QLR"] if f"{tag}_sketch_QLR" in fx.files else g[f"{tag}_sketch_QLR"]
         out[f"seed{i}"] = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
+        ct = code_tags[i]
+        if f"{ct}_rowhash" in fx.files and d.get("Q_idxs") is not None:
+            codes[f"seed{i}"] = compare(ct, d["Q_idxs"], wl["m"], wl["n"])
+    if codes:
+        out["final_codes"] = codes
+        out["final_codes_summary"] = {
+            "matrices": len(codes), "bit_exact": sum(c["sha_equal"] for c in codes.values()),
+            "flips_at_near_ties": sum(c["flips"] for c in codes.values()),
+            "rows_unexplained": sum(c["rows_unexplained"] for c in codes.values())}
     if name == "cfg2":  # the reference's own spread on the same matrices (4 vs 8 CPU threads)
-        sp = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_spread_cfg2_seeds.json")))
-        out["reference_4_vs_8_threads"] = {f"seed{k}": v for k, v in sp["rel_frob_QLR_ref4_vs_ref8"].items()}
+        sp = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_spread_cfg2_seeds16.json")))["seeds"]
+        out["reference_4_vs_8_threads"] = {f"seed{k}": v["rel_frob_QLR_ref4_vs_ref8"] for k, v in sp.items()}
+        over = {k: v for k, v in out.items() if k.startswith("seed") and v > 1e-4}
+        out["seeds_over_1e-4"] = {k: {"ours": v, "reference_spread": out["reference_4_vs_8_threads"].get(k)}
+                                  for k, v in over.items()}
     return out
 
 
@@ -142,8 +167,35 @@ def cpu_baseline(name, wl, dec0):
     return cpu, par
 
 
+def model_parity(out, dev):
+    """The whole-model results that golden reference runs pin (after the gather, on rank 0):
+    layer 0/1 q, k, v, o_proj = config-2 seeds 0-3 / 7-10 (tests/golden/final_codes.npz) and
+    layer-0 gate_proj = the cfg4t run (seed 4, 11008 x 4096): relative Frobenius error of
+    Q + L R (sketch) and the final integer codes (tests/final_codes.py)."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from final_codes import compare, fixture
+    fx, g = fixture(), golden()
+    pins = {f"model.layers.{l}.self_attn.{p}_proj": (f"cfg2s{7 * l + i}" if 7 * l + i else "cfg2")
+            for l in (0, 1) for i, p in enumerate("qkvo")}
+    pins["model.layers.0.mlp.gate_proj"] = "cfg4t"
+    res = {}
+    for r in out:
+        tag = pins.get(r.name)
+        if tag is None or f"{tag}_rowhash" not in fx.files:
+            continue
+        m, n = r.m, r.n
+        codes = K.unpack_codes(r.codes.to(dev).view(1, -1), m * n, r.Q_bits)
+        Q = K.dequantize_uniform(codes.view(1, -1), torch.tensor([r.Q_scale], device=dev), r.Q_bits).view(m, n)
+        sk = _sketch(Q, r.L.to(dev), r.R.to(dev), n)
+        ref = fx[f"{tag}_sketch_QLR"] if f"{tag}_sketch_QLR" in fx.files else g[f"{tag}_sketch_QLR"]
+        res[r.name] = {"golden": tag, "rel_frob_QLR": float(np.linalg.norm(sk - ref) / np.linalg.norm(ref)),
+                       "final_codes": compare(tag, codes, m, n)}
+    return res
+
+
 def run_model(args):
-    """BASELINE configs[3]: the 224 Llama-2-7B linear weights (random-init fp16, one device RNG
+    """BASELINE configs[3]: the 224 Llama-2-7B linear weights (random-init fp16, one host RNG
     seed per matrix, resident in HBM before the timed region), rank i % world decomposing
     matrix i (sharding.decompose_sharded: same-shape batches of <= 16 (8 GPUs) / 64 interleaved on
     their own HIP streams), results packed in HBM and gathered to rank 0 over RCCL.  One step = the
@@ -168,9 +220,12 @@ def run_model(args):
     mine = [items[i] for i in S.shard_indices(len(items), world, rank)]
     Wd = {}
     for name, m, n, seed in mine:
-        g = torch.Generator(device=dev)
-        g.manual_seed(seed)
-        Wd[name] = (torch.randn(m, n, generator=g, device=dev) * 0.02).to(torch.float16)
+        # the survey's recipe on the HOST generator (torch.manual_seed(seed); randn * 0.02 ->
+        # fp16), as sharding.engine_decompose_batch and the golden runs: layer-0/1 q,k,v,o
+        # (seeds 0-3, 7-10) are tests/golden/final_codes.npz's cfg2 seeds, layer-0 gate_proj
+        # (seed 4) is sum_large.npz's cfg4t run
+        torch.manual_seed(seed)
+        Wd[name] = (torch.randn(m, n) * 0.02).to(torch.float16).to(dev)
     ep = EngineParams.from_caldera_params(qp)
 
     # a rank's share at 8 GPUs is 28 matrices (3 shape batches, interleaved on their own HIP
@@ -224,7 +279,7 @@ def run_model(args):
             "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None,
             "dtype": "f32 (fp16 W in; fp32-grade split-fp16 MFMA products, fp64 small solves; int2 codes)",
-            "data": "synthetic: 224 random-init fp16 Llama-2-7B-shaped weights (randn*0.02, device RNG per seed)",
+            "data": "synthetic: 224 random-init fp16 Llama-2-7B-shaped weights (randn*0.02, host RNG, seed = layer*7+proj)",
             "config": {"workload": "BASELINE configs[3]: 224 Llama-2-7B linear weights (32 x q,k,v,o 4096x4096, "
                                    "gate,up 11008x4096, down 4096x11008), r 128, Q2, L/R 16, iters 5, H = I; "
                                    "round-robin matrix sharding, RCCL gather of the packed (Q, L, R) to rank 0",
@@ -234,6 +289,8 @@ def run_model(args):
             "gathered_bytes": int(sum(r.codes.numel() * r.codes.element_size() + r.L.numel() * 4 + r.R.numel() * 4
                                       for r in out)),
         }
+        if not args.no_parity:
+            result["parity_pinned"] = model_parity(out, dev)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -290,7 +347,24 @@ def main():
         outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], h, True) for i, e in enumerate(engines)], dev)
         # no reference cycles: the previous step's buffers must be freed as soon as the
         # next step drops them, or the caching allocator grows and stalls on hipMalloc
+        if world > 1:
+            # N > 1: the one collective north_star names -- every rank's packed results
+            # (2-bit codes, L, R, scales, errors) gathered to rank 0 over RCCL (HBM -> HBM)
+            from ee274_convexcaldera_llm_quantization_amd import sharding as S
+            res = [S.MatrixResult(f"rank{rank}.m{j}", wl["m"], wl["n"], wl["rank"], wl["Q_bits"], d["codes"],
+                                  d["Q_scale"], d["L"], d["R"], d["global_scale"], d["errors"])
+                   for j, d in enumerate(pd for e in engines for pd in e.last_packed)]
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            pl = S.gather_to_rank0(S.pack_results(res, device=dev), device=dev)
+            torch.cuda.synchronize()
+            gather_stats["ms"] += 1000.0 * (time.perf_counter() - tg)
+            gather_stats["calls"] += 1
+            gather_stats["bytes"] = 0 if pl is None else int(sum(x.numel() for x in pl))
+            gather_stats["ranks"] = 0 if pl is None else len(pl)
         return [d for o in outs for d in o], engines[0]
+
+    gather_stats = {"ms": 0.0, "calls": 0, "bytes": 0, "ranks": 0}
 
     for _ in range(args.warmup):
         step()
@@ -301,6 +375,8 @@ def main():
     solver.EVENT_PROBE.enable(True)
     solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * max(1, args.streams or 1))
     solver.LPLR_PROBE.enable(wl["L_bits"] < 16, max_pairs=64)
+    solver.GRAM_PROBE.enable(True, max_pairs=16 * args.steps * parts)
+    gather_stats.update(ms=0.0, calls=0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -324,6 +400,8 @@ def main():
     solver.QUANT_PROBE.enable(False)
     lprobe = solver.LPLR_PROBE.summary()
     solver.LPLR_PROBE.enable(False)
+    gprobe = solver.GRAM_PROBE.summary()
+    solver.GRAM_PROBE.enable(False)
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -407,9 +485,29 @@ def main():
                 "launches_timed": g["count"], "avg_call_ms": g["avg_ms"], "flops_per_call": g["flops_per_launch"],
                 "kernel": ("x3 split-fp16 kernel (cq_gemm_x3, 3 x v_mfma_f32_16x16x32_f16)" if lx3
                            else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")}
+    if gprobe:
+        # the LR update's MFMA-bound kernel (north_star: "MFMA utilisation on the LR update"):
+        # the split-fp16 Gram G = Y Y^T (gemm_x3v_kernel<false>, sym_out), 3 fp16 MFMA products
+        # over the upper half of the symmetric k x k output; fp32-equivalent flops k^2 n
+        gp = gprobe["gram"]
+        t = gp["avg_ms"] * 1e-3
+        ach = gp["flops_per_launch"] / t / 1e12
+        result["roofline_gram"] = {
+            "bound": "mfma", "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s (fp16 MFMA)",
+            "frac": ach / PEAK_F16_MFMA_TFLOPS, "launches_timed": gp["count"], "avg_launch_ms": gp["avg_ms"],
+            "f16_flops_per_launch": gp["flops_per_launch"], "fp32_equiv_tflops": ach / 3.0,
+            "bytes_per_launch": gp["bytes_per_launch"],
+            "kernel": "gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"}
+    if world > 1:
+        result["gather"] = {"collective": "torch.distributed.gather (RCCL) of packed (codes, L, R) to rank 0",
+                            "gathered_bytes_per_step": gather_stats["bytes"], "ranks": gather_stats["ranks"],
+                            "gather_ms_per_step": gather_stats["ms"] / max(1, gather_stats["calls"]),
+                            "included_in_value": True}
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
     result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
-                        "outer_iters": st.get("outer", 0)}
+                        "outer_iters": st.get("outer", 0), "stalled_matrices": st.get("stalls", 0),
+                        "jacobi_unconverged": st.get("jacobi_unconverged", 0),
+                        "jacobi_budget_redos": st.get("jacobi_redo", 0)}
     if rank == 0 and not args.no_parity:
         # parity of the LAST TIMED STEP's own results (rank 0: batch positions 0-3 = seeds 0-3)
         par = parity_of_timed_step(args.workload, decs, wl)

@@ -100,8 +100,6 @@ _SIGS = {
     "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_size, c_vp]),
-    "cq_tridiag_workspace": (c_size, [c_i64, c_i64]),
-    "cq_tridiag_eigh": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp, c_vp]),
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
                                  c_vp]),
@@ -113,7 +111,6 @@ _SIGS = {
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
-    "cq_x3_clock": (c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
@@ -498,22 +495,6 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
     return ev, V32, V64, sw
 
 
-def tridiag_eigh(A: torch.Tensor, want_vectors: bool = True):
-    """A (B, p, p) fp64 symmetric, p <= 192 (not modified) -> (evals desc (B,p), V32 or None,
-    fallback): the tridiagonal path (cq_tridiag_eigh); fallback True means some matrix had a
-    near-degenerate pair and V32 must not be used (cq_jacobi_eigh reruns such batches)."""
-    _require_hip(A)
-    B, p, _ = A.shape
-    ev = torch.empty((B, p), dtype=torch.float64, device=A.device)
-    V32 = torch.empty((B, p, p), dtype=torch.float32, device=A.device) if want_vectors else None
-    lib = load()
-    ws = workspace(lib.cq_tridiag_workspace(p, B), A.device)
-    fb = ctypes.c_int(0)
-    _check(lib.cq_tridiag_eigh(_p(A), p, B, _p(ev), _p(V32), _p(ws), ws.numel(), ctypes.byref(fb),
-                               _stream(A.device)), "cq_tridiag_eigh")
-    return ev, V32, bool(fb.value)
-
-
 def ritz_residual(X, Z, theta, r):
     _require_hip(X, Z, theta)
     B, k, p = X.shape
@@ -670,14 +651,6 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         g.out_scale = out_scale
     _check(load().cq_gemm_x3(ctypes.byref(g), _stream(Ah.device)), "cq_gemm_x3")
     return C
-
-
-def x3_clock():
-    """(shader ticks, 100 MHz ticks) summed over cq_gemm_x3 workgroups since the last call
-    (only with CQ_X3_CLOCK set when the library was first used); resets the sums."""
-    out = (ctypes.c_ulonglong * 2)()
-    _check(load().cq_x3_clock(out), "cq_x3_clock")
-    return int(out[0]), int(out[1])
 
 
 def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None, bits: int, *, eps: float = 1e-8,

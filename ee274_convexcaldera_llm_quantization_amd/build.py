@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcaldera_hip.so")
 SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_codebook.hip", "cq_calib.hip",
-           "cq_bjacobi.hip", "cq_trid.hip"]
+           "cq_bjacobi.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          # bit-exact quantiser: no FMA contraction, IEEE-correct fp32 division/sqrt
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"]

@@ -14,8 +14,8 @@
 //                     V_P^T Vt[P, :].  Blocks whose pairs did not rotate are left alone.
 // Both kernels also leave per-block off-diagonal / diagonal square sums; bj_check_kernel
 // turns them into the per-matrix stop test off^2 <= tol^2 sum a_ii^2 after every sweep
-// (the host reads the flags once per sweep and stops when every matrix has converged;
-// converged matrices' workgroups exit at entry).  Everything is fp64.
+// (a converged matrix's later workgroups exit at entry; the caller's sweep budget bounds the
+// launches, no host synchronisation inside).  Everything is fp64.
 #include "cq_common.h"
 
 namespace cq {
@@ -391,8 +391,11 @@ size_t bj_workspace(int64_t p, int64_t batch) {
     return s;
 }
 
-// Block-Jacobi eigensolver (host loop; one stream synchronisation per sweep to read the
-// per-matrix convergence flags).
+// Block-Jacobi eigensolver, stream-ordered: max_sweeps sweeps are launched without any host
+// read-back.  A matrix whose off-norm test passed (bj_check_kernel) has done[b] set, and every
+// later workgroup of that matrix exits at entry; the per-matrix sweep counts reach the caller
+// through sweeps_out (the solver reads them with its convergence check and sizes the next
+// call's budget from them, redoing an outer iteration whose budget ran out).
 int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
             double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s) {
     if (ws_bytes < bj_workspace(p, batch)) return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
@@ -412,16 +415,7 @@ int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, dou
     int* ranks = reinterpret_cast<int*>(take((size_t)batch * p * sizeof(int)));
     const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
     bj_init_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
-    int* flags = new int[batch];
     for (int sw = 0; sw < max_sweeps; ++sw) {
-        if (hipMemcpyAsync(flags, done, batch * sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            delete[] flags;
-            return check_launch("cq_jacobi_eigh (block Jacobi flags)");
-        }
-        bool all = true;
-        for (int64_t i = 0; i < batch && all; ++i) all = flags[i] != 0;
-        if (all) break;
         for (int st = 0; st < nblk - 1; ++st) {
             bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
                                                                                    done, poff, pdg, nslots);
@@ -430,7 +424,6 @@ int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, dou
         }
         bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
     }
-    delete[] flags;
     bj_finish_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64, sweeps,
                                                      sweeps_out, ranks);
     return check_launch("cq_jacobi_eigh (block Jacobi)");

@@ -112,11 +112,6 @@ constexpr int64_t kBlockJacobiMinP = 192;
 size_t bj_workspace(int64_t p, int64_t batch);
 int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
             double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s);
-// tridiagonal eigensolver (cq_trid.hip) behind cq_jacobi_eigh for p <= 192 without fp64 vectors
-size_t trid_workspace(int64_t p, int64_t batch);
-bool trid_supported(int64_t p);
-int trid_eigh(const double* A, int64_t p, int64_t batch, double* evals, float* V32, void* ws, size_t ws_bytes,
-              hipStream_t s, int* fallback);
 
 }  // namespace cq
 

@@ -238,469 +238,6 @@ static int gram_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
-// ------------------------------------------------------------------ SPD whitening
-// Symmetric Gaussian elimination S = L D L^T on the upper triangle (the trailing block stays
-// symmetric), E = L^{-1} built alongside; Wt = E^T D^{-1/2}.  One workgroup per matrix,
-// operands L2-resident.  2-D wave/lane loops (no integer division in the hot loops), every
-// lane keeps several independent row elements in flight.
-constexpr int kSmallThreads = 1024;
-constexpr int kSmallWaves = kSmallThreads / 64;
-
-__global__ __launch_bounds__(kSmallThreads) void spd_whiten_kernel(double* __restrict__ S_all,
-                                                                    int p, double rc2, double* __restrict__ E_all,
-                                                                    float* __restrict__ W32,
-                                                                    int* __restrict__ info) {
-    extern __shared__ double fac[];  // row factors of the current step + pivots
-    double* piv = fac + p;
-    __shared__ int bad;  // number of dropped (dependent) pivots
-    __shared__ double dmax_s;
-    const int64_t b = blockIdx.x;
-    double* S = S_all + b * (int64_t)p * p;
-    double* E = E_all + b * (int64_t)p * p;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = wid; i < p; i += kSmallWaves)
-        for (int c = lane; c < p; c += 64) E[i * p + c] = (i == c) ? 1.0 : 0.0;
-    if (tid == 0) {
-        bad = 0;
-        double dm = 0.0;
-        for (int j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
-        dmax_s = dm;
-    }
-    __syncthreads();
-    const double dmax = dmax_s;
-    for (int j = 0; j < p; ++j) {
-        const double d = S[j * p + j];
-        // a pivot at or below rc2 * max diag: column j depends on the previous ones; it is
-        // dropped (coefficient 0, Wt column 0) — the basic least-squares solution of gelsy
-        // (torch.linalg.lstsq's CPU driver) in index order
-        const bool drop = !(d > 1e-300 && d > dmax * rc2);
-        for (int i = j + 1 + tid; i < p; i += kSmallThreads) fac[i] = drop ? 0.0 : S[j * p + i] / d;  // upper row j
-        if (tid == 0) {
-            piv[j] = drop ? __longlong_as_double(0x7ff0000000000000ll) : d;
-            bad += drop;
-        }
-        __syncthreads();
-        // S[i][c] -= f_i S[j][c] for j < i <= c  (upper trailing);  E[i][c] -= f_i E[j][c], c <= j
-        for (int i = j + 1 + wid; i < p; i += kSmallWaves) {
-            const double f = fac[i];
-            double* Si = S + i * p;
-            const double* Sj = S + j * p;
-#pragma unroll 4
-            for (int c = i + lane; c < p; c += 64) Si[c] -= f * Sj[c];
-            double* Ei = E + i * p;
-            const double* Ej = E + j * p;
-#pragma unroll 4
-            for (int c = lane; c <= j; c += 64) Ei[c] -= f * Ej[c];
-        }
-        __syncthreads();
-    }
-    if (tid == 0) info[b] = bad;
-    // Wt[a][c] = E[c][a] / sqrt(piv[c])  (upper triangular; 0 for dropped pivots); staged in S
-    for (int a = wid; a < p; a += kSmallWaves)
-        for (int c = lane; c < p; c += 64) {
-            const double v = (c >= a) ? E[c * p + a] / sqrt(piv[c]) : 0.0;
-            if (W32) W32[b * (int64_t)p * p + a * p + c] = (float)v;
-            S[a * p + c] = v;
-        }
-}
-
-// ------------------------------------------------------------------ Jacobi eigensolver
-// Parallel cyclic Jacobi: round-robin pairing, p/2 disjoint rotations per round.  A is updated
-// on 2x2 blocks (pair a <= pair b), mirrored; one wave per pair-b row strip, lanes over
-// pair a.  Eigenvectors are accumulated TRANSPOSED (row i of Vt = eigenvector i), so a
-// rotation of columns i, j of V is a coalesced update of rows i, j of Vt (one wave per pair,
-// lanes along the row).  All index math is 32-bit and division-free.
-__device__ __forceinline__ void rr_pair(int P, int rd, int q, int& i, int& j) {
-    const int n1 = P - 1;
-    if (q == 0) { i = n1; j = rd; }
-    else {
-        i = rd + q; if (i >= n1) i -= n1;
-        j = rd - q; if (j < 0) j += n1;
-    }
-    if (i > j) { const int t = i; i = j; j = t; }
-}
-
-__global__ __launch_bounds__(kSmallThreads) void jacobi_kernel(double* __restrict__ A_all,
-                                                                int p, int max_sweeps, double tol,
-                                                                double* __restrict__ Vt_all,
-                                                                double* __restrict__ evals,
-                                                                float* __restrict__ V32,
-                                                                double* __restrict__ V64,
-                                                                int* __restrict__ sweeps_out) {
-    extern __shared__ double sm[];
-    const int P = p + (p & 1);
-    const int H = P / 2;
-    double* cs = sm;          // H
-    double* sn = sm + H;      // H
-    int* pi = reinterpret_cast<int*>(sm + 2 * H);  // P ints (pi | pj during rounds)
-    int* pj = pi + H;
-    __shared__ double red[16];
-    __shared__ int stop, nact;
-    const int64_t b = blockIdx.x;
-    double* A = A_all + b * (int64_t)p * p;
-    double* Vt = Vt_all + b * (int64_t)p * p;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool want_v = V32 || V64;  // values only: no eigenvector rotations
-    for (int i = wid; i < p; i += kSmallWaves)
-        for (int c = lane; c < p; c += 64) {
-            if (want_v) Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
-            if (i < c) {  // symmetrise (Rayleigh-Ritz matrices carry rounding asymmetry)
-                const double s = 0.5 * (A[i * p + c] + A[c * p + i]);
-                A[i * p + c] = s;
-                A[c * p + i] = s;
-            }
-        }
-    __syncthreads();
-    // Threshold Jacobi: a pair whose |a_ij| is below thr * sqrt|a_ii a_jj| is not rotated.  With
-    // thr = tol / (2 sqrt p), a matrix whose pairs are all below it already has
-    // off^2 <= thr^2 (sum |a_ii|)^2 <= thr^2 p sum a_ii^2 = tol^2 dg / 4, i.e. passes the stop
-    // test, so skipping cannot stall convergence.  Near-diagonal (warm Rayleigh-Ritz) matrices
-    // then skip most of the scattered 2x2 block updates of A and most V row updates.
-    const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
-    int sweep = 0;
-    for (; sweep < max_sweeps; ++sweep) {
-        double off = 0.0, dg = 0.0;
-        for (int i = wid; i < p; i += kSmallWaves)
-            for (int c = lane; c < p; c += 64) {
-                if (c < i) continue;  // sweeps keep the upper triangle only
-                const double v = A[i * p + c];
-                if (i == c) dg += v * v; else off += 2.0 * v * v;
-            }
-        const double offs = block_sum_f64(off, red);
-        const double dgs = block_sum_f64(dg, red);
-        if (tid == 0) stop = (offs <= tol * tol * dgs) ? 1 : 0;
-        __syncthreads();
-        if (stop) break;
-        for (int rd = 0; rd < P - 1; ++rd) {
-            if (tid == 0) nact = 0;
-            __syncthreads();
-            for (int q = tid; q < H; q += kSmallThreads) {
-                int i, j;
-                rr_pair(P, rd, q, i, j);
-                double c = 1.0, s = 0.0;
-                if (j < p) {
-                    const double aij = A[i * p + j];
-                    const double aii = A[i * p + i], ajj = A[j * p + j];
-                    if (fabs(aij) > 1e-300 && fabs(aij) > thr * sqrt(fabs(aii * ajj))) {
-                        const double th = (ajj - aii) / (2.0 * aij);
-                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
-                        c = 1.0 / sqrt(1.0 + t * t);
-                        s = t * c;
-                        atomicAdd(&nact, 1);
-                    }
-                }
-                cs[q] = c; sn[q] = s; pi[q] = i; pj[q] = j;
-            }
-            __syncthreads();
-            if (nact == 0) continue;
-            // ---- A <- J^T A J on 2x2 pair blocks (qa <= qb), upper triangle only.  The
-            // H(H+1)/2 blocks of a round are disjoint, so each thread takes JU blocks of the
-            // linear triangle enumeration and issues all their loads before any store (the
-            // scattered L2 round trips overlap instead of serialising block by block).
-            {
-                constexpr int JU = 4;
-                const int T = H * (H + 1) / 2;
-                for (int t0 = tid; t0 < T; t0 += JU * kSmallThreads) {
-                    int ua[JU][4];
-                    double xv[JU][4], cc[JU][2], ss[JU][2];
-                    bool act[JU], va[JU], vb[JU], dgb[JU];
-#pragma unroll
-                    for (int k = 0; k < JU; ++k) {
-                        const int t = t0 + k * kSmallThreads;
-                        act[k] = false;
-                        if (t >= T) continue;
-                        int qb = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-                        while ((qb + 1) * (qb + 2) / 2 <= t) ++qb;
-                        while (qb * (qb + 1) / 2 > t) --qb;
-                        const int qa = t - qb * (qb + 1) / 2;
-                        const double sa = sn[qa], sb = sn[qb];
-                        if (sa == 0.0 && sb == 0.0) continue;
-                        act[k] = true;
-                        dgb[k] = qa == qb;
-                        cc[k][0] = cs[qa]; ss[k][0] = sa; cc[k][1] = cs[qb]; ss[k][1] = sb;
-                        const int ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
-                        va[k] = ja < p; vb[k] = jb < p;
-                        ua[k][0] = ia < ib ? ia * p + ib : ib * p + ia;
-                        ua[k][1] = ia < jb ? ia * p + jb : jb * p + ia;
-                        ua[k][2] = ja < ib ? ja * p + ib : ib * p + ja;
-                        ua[k][3] = ja < jb ? ja * p + jb : jb * p + ja;
-                        xv[k][0] = A[ua[k][0]];
-                        xv[k][1] = vb[k] ? A[ua[k][1]] : 0.0;
-                        xv[k][2] = va[k] ? A[ua[k][2]] : 0.0;
-                        xv[k][3] = (va[k] && vb[k]) ? A[ua[k][3]] : 0.0;
-                    }
-#pragma unroll
-                    for (int k = 0; k < JU; ++k) {
-                        if (!act[k]) continue;
-                        const double ca = cc[k][0], sa = ss[k][0], cb = cc[k][1], sb = ss[k][1];
-                        const double x00 = xv[k][0], x01 = xv[k][1], x10 = xv[k][2], x11 = xv[k][3];
-                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                        const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                        const double z00 = ca * y00 - sa * y10, z10 = sa * y00 + ca * y10;
-                        const double z01 = ca * y01 - sa * y11, z11 = sa * y01 + ca * y11;
-                        if (dgb[k]) {  // diagonal block: (ia, ja) is the annihilated pair
-                            A[ua[k][0]] = z00;
-                            if (va[k] && vb[k]) A[ua[k][3]] = z11;
-                            if (vb[k]) A[ua[k][1]] = 0.0;
-                        } else {
-                            A[ua[k][0]] = z00;
-                            if (vb[k]) A[ua[k][1]] = z01;
-                            if (va[k]) A[ua[k][2]] = z10;
-                            if (va[k] && vb[k]) A[ua[k][3]] = z11;
-                        }
-                    }
-                }
-            }
-
-            // ---- Vt rows i, j of each active pair (coalesced along the row)
-            for (int q = wid; want_v && q < H; q += kSmallWaves) {
-                const double s = sn[q];
-                if (s == 0.0) continue;
-                const double c = cs[q];
-                double* ri = Vt + pi[q] * p;
-                double* rj = Vt + pj[q] * p;
-#pragma unroll 4
-                for (int x = lane; x < p; x += 64) {
-                    const double vi = ri[x], vj = rj[x];
-                    ri[x] = c * vi - s * vj;
-                    rj[x] = s * vi + c * vj;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
-    // sort descending by rank counting (ties broken by index); eigenvector i = row i of Vt
-    for (int i = tid; i < p; i += kSmallThreads) {
-        const double di = A[i * p + i];
-        int rank = 0;
-        for (int j = 0; j < p; ++j) {
-            const double dj = A[j * p + j];
-            rank += (dj > di) || (dj == di && j < i);
-        }
-        evals[b * p + rank] = di;
-        pi[i] = rank;
-    }
-    __syncthreads();
-    for (int i = wid; want_v && i < p; i += kSmallWaves) {
-        const int rk = pi[i];
-        for (int x = lane; x < p; x += 64) {  // component x of eigenvector i -> V[x][rk]
-            const double v = Vt[i * p + x];
-            if (V32) V32[b * (int64_t)p * p + x * p + rk] = (float)v;
-            if (V64) V64[b * (int64_t)p * p + x * p + rk] = v;
-        }
-    }
-}
-
-// ------------------------------------------------------------------ Jacobi, LDS-resident A
-// Same cyclic round-robin Jacobi as jacobi_kernel, with A packed (upper triangle) in LDS:
-// fp64 for p <= 180, fp32 for p <= 256 (fp32 rotations: near-degenerate Ritz pairs mix at
-// ~eps32*||T||/gap, far below the 1e-4 product tolerance).  The eigenvector
-// rows (Vt) stay in global memory, updated coalesced along rows for active pairs only.
-#ifndef CQ_JAC_ABL
-#define CQ_JAC_ABL 0  // diagnostic builds only (tools/jacobi_ablate.sh): 1 no A update, 2 no V rotation, 4 no seat shift
-#endif
-constexpr int JB = 2;  // pair blocks per thread held in registers per pass (register budget at 1024 threads)
-
-template <typename T>
-__global__ __launch_bounds__(kSmallThreads) void jacobi_lds_kernel(const double* __restrict__ A_all,
-                                                                    int p, int max_sweeps, double tol,
-                                                                    double* __restrict__ Vt_all,
-                                                                    double* __restrict__ evals,
-                                                                    float* __restrict__ V32,
-                                                                    double* __restrict__ V64,
-                                                                    int* __restrict__ sweeps_out) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int P = p + (p & 1);
-    const int H = P / 2;
-    double* cs = reinterpret_cast<double*>(smem_raw);       // H
-    double* sn = cs + H;                                    // H
-    int* pi = reinterpret_cast<int*>(sn + H);               // P ints (pi | pj)
-    int* pj = pi + H;
-    T* a = reinterpret_cast<T*>(pi + P + 2 + (P & 1));      // packed upper triangle
-    __shared__ double red[16];
-    __shared__ int stop;
-    const int64_t b = blockIdx.x;
-    const double* Ag = A_all + b * (int64_t)p * p;
-    double* Vt = Vt_all + b * (int64_t)p * p;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // packed upper index of (i, j), i <= j: row i starts at i*p - i*(i-1)/2
-    auto pk = [p](int i, int j) -> int {
-        if (i > j) { const int t = i; i = j; j = t; }
-        return i * p - ((i * (i - 1)) >> 1) + (j - i);
-    };
-    for (int i = wid; i < p; i += kSmallWaves)
-        for (int c = lane; c < p; c += 64) {
-            Vt[i * p + c] = (i == c) ? 1.0 : 0.0;
-            if (c >= i) a[pk(i, c)] = (T)(0.5 * (Ag[i * p + c] + Ag[c * p + i]));
-        }
-    __syncthreads();
-    const double skip_rel = sizeof(T) == 4 ? 1e-9 : 1e-17;
-    int sweep = 0;
-    for (; sweep < max_sweeps; ++sweep) {
-        double off = 0.0, dg = 0.0;
-        for (int i = wid; i < p; i += kSmallWaves)
-            for (int c = i + lane; c < p; c += 64) {
-                const double v = (double)a[pk(i, c)];
-                if (c == i) dg += v * v; else off += 2.0 * v * v;
-            }
-        const double offs = block_sum_f64(off, red);
-        const double dgs = block_sum_f64(dg, red);
-        if (tid == 0) stop = (offs <= tol * tol * dgs) ? 1 : 0;
-        __syncthreads();
-        if (stop) break;
-        for (int rd = 0; rd < P - 1; ++rd) {
-            int act = 0;
-            for (int q = tid; q < H; q += kSmallThreads) {
-                int i, j;
-                rr_pair(P, rd, q, i, j);
-                double c = 1.0, s = 0.0;
-                if (j < p) {
-                    const double aij = (double)a[pk(i, j)];
-                    const double aii = (double)a[pk(i, i)], ajj = (double)a[pk(j, j)];
-                    if (fabs(aij) > 1e-300 && fabs(aij) > skip_rel * sqrt(fabs(aii * ajj))) {
-                        const double th = (ajj - aii) / (2.0 * aij);
-                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
-                        c = 1.0 / sqrt(1.0 + t * t);
-                        s = t * c;
-                        act = 1;
-                    }
-                }
-                cs[q] = c; sn[q] = s; pi[q] = i; pj[q] = j;
-            }
-            if (!__syncthreads_or(act)) continue;
-            // ---- A <- J^T A J on pair blocks (qa <= qb), LDS.  Block e (triangular order) goes
-            //      to thread e mod 1024; a thread's <= JB blocks are loaded before any is stored.
-            {
-                const int nblk = H * (H + 1) / 2;
-                for (int e0 = tid; e0 < nblk; e0 += kSmallThreads * JB) {
-                    int o[JB][4];
-                    double x[JB][4], ca[JB], sa[JB], cb[JB], sb[JB];
-                    bool live[JB], dgn[JB];
-#pragma unroll
-                    for (int u = 0; u < JB; ++u) {
-                        const int e = e0 + u * kSmallThreads;
-                        live[u] = false;
-                        dgn[u] = false;
-                        if (e < nblk) {
-                            int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-                            if (qb * (qb + 1) / 2 > e) --qb;
-                            if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
-                            const int qa = e - qb * (qb + 1) / 2;
-                            ca[u] = cs[qa]; sa[u] = sn[qa]; cb[u] = cs[qb]; sb[u] = sn[qb];
-                            const int ia = pi[qa], ja = pj[qa], ib = pi[qb], jb = pj[qb];
-                            const bool va = ja < p, vb = jb < p;
-                            if ((sa[u] != 0.0 || sb[u] != 0.0) && (qa != qb || va)) {
-                                live[u] = true;
-                                dgn[u] = (qa == qb);
-                                if (dgn[u]) {
-                                    o[u][0] = pk(ia, ia); o[u][1] = pk(ia, ja);
-                                    o[u][2] = o[u][1]; o[u][3] = pk(ja, ja);
-                                } else {
-                                    o[u][0] = pk(ia, ib);
-                                    o[u][1] = vb ? pk(ia, jb) : -1;
-                                    o[u][2] = va ? pk(ja, ib) : -1;
-                                    o[u][3] = (va && vb) ? pk(ja, jb) : -1;
-                                }
-#pragma unroll
-                                for (int w4 = 0; w4 < 4; ++w4)
-                                    x[u][w4] = o[u][w4] >= 0 ? (double)a[o[u][w4]] : 0.0;
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < JB; ++u) {
-                        if (!live[u]) continue;
-                        const double y00 = cb[u] * x[u][0] - sb[u] * x[u][1], y01 = sb[u] * x[u][0] + cb[u] * x[u][1];
-                        const double y10 = cb[u] * x[u][2] - sb[u] * x[u][3], y11 = sb[u] * x[u][2] + cb[u] * x[u][3];
-                        if (dgn[u]) {
-                            a[o[u][0]] = (T)(ca[u] * y00 - sa[u] * y10);
-                            a[o[u][3]] = (T)(sa[u] * y01 + ca[u] * y11);
-                            a[o[u][1]] = (T)0;
-                        } else {
-                            a[o[u][0]] = (T)(ca[u] * y00 - sa[u] * y10);
-                            if (o[u][1] >= 0) a[o[u][1]] = (T)(ca[u] * y01 - sa[u] * y11);
-                            if (o[u][2] >= 0) a[o[u][2]] = (T)(sa[u] * y00 + ca[u] * y10);
-                            if (o[u][3] >= 0) a[o[u][3]] = (T)(sa[u] * y01 + ca[u] * y11);
-                        }
-                    }
-                }
-            }
-            // ---- Vt rows of active pairs (global, coalesced); 3 pairs' rows in flight per wave
-            for (int q0 = wid; q0 < H; q0 += 3 * kSmallWaves) {
-                double vi[3][4], vj[3][4], cc[3], ss[3];
-                double* ri[3];
-                double* rj[3];
-#pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    const int q = q0 + u * kSmallWaves;
-                    ss[u] = (q < H) ? sn[q] : 0.0;
-                    cc[u] = (q < H) ? cs[q] : 1.0;
-                    ri[u] = Vt + (q < H ? pi[q] : 0) * p;
-                    rj[u] = Vt + (q < H ? pj[q] : 0) * p;
-                    if (ss[u] != 0.0) {
-#pragma unroll
-                        for (int c4 = 0; c4 < 4; ++c4) {
-                            const int x = lane + 64 * c4;
-                            if (x < p) { vi[u][c4] = ri[u][x]; vj[u][c4] = rj[u][x]; }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    if (ss[u] == 0.0) continue;
-#pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4) {
-                        const int x = lane + 64 * c4;
-                        if (x < p) {
-                            ri[u][x] = cc[u] * vi[u][c4] - ss[u] * vj[u][c4];
-                            rj[u][x] = ss[u] * vi[u][c4] + cc[u] * vj[u][c4];
-                        }
-                    }
-                }
-                // p > 256: remaining columns, unbatched
-#pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    if (ss[u] == 0.0) continue;
-                    for (int x = lane + 256; x < p; x += 64) {
-                        const double a0 = ri[u][x], a1 = rj[u][x];
-                        ri[u][x] = cc[u] * a0 - ss[u] * a1;
-                        rj[u][x] = ss[u] * a0 + cc[u] * a1;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
-    int* rk = pi;  // P >= p ints
-    for (int i = tid; i < p; i += kSmallThreads) {
-        const double di = (double)a[pk(i, i)];
-        int rank = 0;
-        for (int j = 0; j < p; ++j) {
-            const double dj = (double)a[pk(j, j)];
-            rank += (dj > di) || (dj == di && j < i);
-        }
-        evals[b * p + rank] = di;
-        rk[i] = rank;
-    }
-    __syncthreads();
-    for (int i = wid; i < p; i += kSmallWaves) {
-        const int r = rk[i];
-        for (int x = lane; x < p; x += 64) {
-            const double v = Vt[i * p + x];
-            if (V32) V32[b * (int64_t)p * p + x * p + r] = (float)v;
-            if (V64) V64[b * (int64_t)p * p + x * p + r] = v;
-        }
-    }
-}
-
-static size_t jacobi_lds_bytes(int p, int esize) {
-    const int P = p + (p & 1), H = P / 2;
-    return (size_t)2 * H * sizeof(double) + (size_t)(P + 2 + (P & 1)) * sizeof(int) +
-           (size_t)p * (p + 1) / 2 * esize + 16;
-}
-
 // ------------------------------------------------------------------ Jacobi, V in registers
 // A (fp64, packed upper triangle) lives in LDS in index space; the eigenvector matrix V
 // (fp32) lives in REGISTERS in "seat" space.  The round-robin is the circle method with
@@ -800,7 +337,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             const bool any = __syncthreads_or(act);
             if (any) {
                 // ---- A <- J^T A J on pair blocks (qa <= qb) in LDS
-                const int nblk = (CQ_JAC_ABL & 1) ? 0 : H * (H + 1) / 2;
+                const int nblk = H * (H + 1) / 2;
                 if constexpr (JBR == 1) {
                     // one pair block at a time, few live values (V stays in registers)
 #pragma unroll 1
@@ -894,7 +431,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                 }
                 // ---- V rotations (registers; skipped when only eigenvalues are wanted)
 #pragma unroll
-                for (int u = 0; u < ((CQ_JAC_ABL & 2) ? 0 : PPT); ++u) {
+                for (int u = 0; u < PPT; ++u) {
                     if (!wantv) break;
                     const int k = k0 + u;
                     if (k < H) {
@@ -913,7 +450,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             }
             // ---- seat shift of V (every round, rotations or not)
 #pragma unroll
-            for (int r = 0; r < ((CQ_JAC_ABL & 4) ? 0 : RPT); ++r) {
+            for (int r = 0; r < RPT; ++r) {
                 if (!wantv) break;
                 const float from_left = __shfl_up(ev[PPT - 1][r], 1, 32);   // ev of pair k0-1
                 const float from_right = __shfl_down(od[0][r], 1, 32);      // od of pair k0+PPT
@@ -977,102 +514,10 @@ static size_t jacobi_reg_bytes(int p) {
            (size_t)p * (p + 1) / 2 * sizeof(double) + 16;
 }
 
-// ------------------------------------------------------------------ blocked SPD whitening
-// Panel-blocked symmetric elimination (nb = 32): each panel of 32 pivots is reduced in LDS,
-// then the trailing upper triangle receives one rank-32 Schur update
-//   S[i][c] -= sum_k U[k][i] U[k][c] / d_k ,   E[i][:] = -sum_k (U[k][i]/d_k) E[k][:]
-// (U = panel rows after in-panel elimination), E = L^{-1}; finally Wt = E^T D^{-1/2}.
-// NB = 32, or 16 when a 32-row panel pair does not fit the 160 KB of LDS (p up to 620).
-template <int WNB>
-__global__ __launch_bounds__(kSmallThreads) void spd_whiten_blocked_kernel(
-    double* __restrict__ S_all, int p, double rc2, double* __restrict__ E_all, float* __restrict__ W32,
-    int* __restrict__ info) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* U = reinterpret_cast<double*>(smem_raw);      // WNB x p   (panel rows of S, cols >= J)
-    double* Ep = U + WNB * p;                             // WNB x p   (panel rows of E)
-    double* piv = Ep + WNB * p;                           // p
-    double* fk = piv + p;                                 // WNB
-    __shared__ int bad;
-    __shared__ double dmax_s;
-    const int64_t b = blockIdx.x;
-    double* S = S_all + b * (int64_t)p * p;
-    double* E = E_all + b * (int64_t)p * p;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = wid; i < p; i += kSmallWaves)
-        for (int c = lane; c < p; c += 64) E[i * p + c] = (i == c) ? 1.0 : 0.0;
-    if (tid == 0) {
-        bad = 0;
-        double dm = 0.0;
-        for (int j = 0; j < p; ++j) dm = fmax(dm, fabs(S[j * p + j]));
-        dmax_s = dm;
-    }
-    __syncthreads();
-    const double dmax = dmax_s;
-    for (int J = 0; J < p; J += WNB) {
-        const int nb = min(WNB, p - J);
-        // load panel rows of S (columns >= J, upper part) and E (columns < J + nb)
-        for (int k = wid; k < nb; k += kSmallWaves)
-            for (int c = lane; c < p; c += 64) {
-                U[k * p + c] = (c >= J) ? S[(J + k) * p + c] : 0.0;
-                Ep[k * p + c] = (c < J + nb) ? E[(J + k) * p + c] : 0.0;
-            }
-        __syncthreads();
-        // in-panel elimination of pivots J..J+nb-1
-        for (int k = 0; k < nb; ++k) {
-            const double d = U[k * p + J + k];
-            const bool drop = !(d > 1e-300 && d > dmax * rc2);  // dependent column (see spd_whiten_kernel)
-            if (tid < nb) fk[tid] = (!drop && tid > k) ? U[k * p + J + tid] / d : 0.0;
-            if (tid == 0) {
-                piv[J + k] = drop ? __longlong_as_double(0x7ff0000000000000ll) : d;
-                bad += drop;
-            }
-            __syncthreads();
-            // rows k2 > k of the panel: U[k2][c] -= f_k2 U[k][c] (c >= J+k2); Ep[k2] -= f_k2 Ep[k]
-            for (int k2 = k + 1 + wid; k2 < nb; k2 += kSmallWaves) {
-                const double f = fk[k2];
-                for (int c = J + k2 + lane; c < p; c += 64) U[k2 * p + c] -= f * U[k * p + c];
-                for (int c = lane; c <= J + k; c += 64) Ep[k2 * p + c] -= f * Ep[k * p + c];
-            }
-            __syncthreads();
-        }
-        __syncthreads();
-        // write panel E rows back
-        for (int k = wid; k < nb; k += kSmallWaves)
-            for (int c = lane; c < J + nb; c += 64) E[(J + k) * p + c] = Ep[k * p + c];
-        // trailing rank-nb update, rows i >= J + nb
-        const int t0 = J + nb;
-        for (int i = t0 + wid; i < p; i += kSmallWaves) {
-            double g[WNB];
-#pragma unroll
-            for (int k = 0; k < WNB; ++k) g[k] = (k < nb) ? U[k * p + i] / piv[J + k] : 0.0;
-            for (int c = i + lane; c < p; c += 64) {
-                double acc = S[i * p + c];
-#pragma unroll
-                for (int k = 0; k < WNB; ++k)
-                    if (k < nb) acc -= g[k] * U[k * p + c];
-                S[i * p + c] = acc;
-            }
-            for (int c = lane; c < t0; c += 64) {
-                double acc = E[i * p + c];
-#pragma unroll
-                for (int k = 0; k < WNB; ++k)
-                    if (k < nb) acc -= g[k] * Ep[k * p + c];
-                E[i * p + c] = acc;
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0) info[b] = bad;
-    for (int a2 = wid; a2 < p; a2 += kSmallWaves)
-        for (int c = lane; c < p; c += 64) {
-            const double v = (c >= a2) ? E[c * p + a2] / sqrt(piv[c]) : 0.0;
-            if (W32) W32[b * (int64_t)p * p + a2 * p + c] = (float)v;
-            S[a2 * p + c] = v;
-        }
-}
-
-// ------------------------------------------------------------------ blocked SPD whitening, MFMA
-// The same elimination in LDL^T block form, nb = 32 pivots per panel J:
+// ------------------------------------------------------------------ SPD whitening
+// Symmetric Gaussian elimination S = L D L^T (rank-revealing: a pivot below rcond2 times the
+// largest is dropped), E = L^{-1}; Wt = E^T D^{-1/2}.  One workgroup per matrix.
+// LDL^T block form, nb = 32 pivots per panel J:
 //   1. one wave factors the 32 x 32 diagonal block in registers (lane l = row l of the
 //      symmetric block and of its L^{-1}; the pivot row is broadcast by shuffles): pivots
 //      (rank-revealing drop rule unchanged), L11^{-1};
@@ -1243,10 +688,6 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
         }
 }
 
-static size_t whiten_lds_bytes(int p, int nb) {
-    return (size_t)(2 * nb * p + p + nb) * sizeof(double) + 16;
-}
-
 // ------------------------------------------------------------------ Ritz residuals
 __global__ __launch_bounds__(256) void ritz_partial_kernel(const float* __restrict__ X,
                                                             const float* __restrict__ Z,
@@ -1373,17 +814,9 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
     CQ_REQUIRE(rcond2 >= 0.0, "cq_spd_whiten: rcond2 must be >= 0");
     hipStream_t s = as_stream(stream);
     // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
-    const size_t wl32 = whiten_lds_bytes((int)p, 32), wl16 = whiten_lds_bytes((int)p, 16);
-    static const bool legacy = getenv("CQ_WHITEN_LEGACY") != nullptr;  // A/B switch: the scalar kernels
     const size_t wlm = (size_t)(p + 2 * 32 * 33 + 32) * sizeof(double);
-    if (!legacy && wlm <= 64 * 1024)
-        spd_whiten_mfma_kernel<<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
-    else if (wl32 <= 160 * 1024)
-        spd_whiten_blocked_kernel<32><<<(unsigned)batch, kSmallThreads, wl32, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
-    else if (wl16 <= 160 * 1024)
-        spd_whiten_blocked_kernel<16><<<(unsigned)batch, kSmallThreads, wl16, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
-    else
-        spd_whiten_kernel<<<(unsigned)batch, kSmallThreads, 2 * p * sizeof(double), s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    CQ_REQUIRE(wlm <= 64 * 1024, "cq_spd_whiten: p too large");
+    spd_whiten_mfma_kernel<<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     if (hipMemcpyAsync(Wt64, S, (size_t)batch * p * p * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
         return set_error(CQ_EHIP, "cq_spd_whiten: copy failed");
     return check_launch("cq_spd_whiten");
@@ -1391,8 +824,7 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
 
 size_t cq_jacobi_workspace(int64_t p, int64_t batch) {
     if (p > kBlockJacobiMinP) return cq::bj_workspace(p, batch);
-    const size_t jac = (size_t)batch * p * p * sizeof(double);
-    return cq::trid_supported(p) ? std::max(jac, cq::trid_workspace(p, batch)) : jac;
+    return 16;  // the register/LDS kernel needs none
 }
 
 int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals,
@@ -1402,43 +834,18 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     CQ_REQUIRE(p <= 4096, "cq_jacobi_eigh: p too large");
     if (!ws || ws_bytes < cq_jacobi_workspace(p, batch))
         return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
-    const int64_t H = (p + (p & 1)) / 2;
     hipStream_t s = as_stream(stream);
-    double* Vt = reinterpret_cast<double*>(ws);
-    const size_t l32 = jacobi_lds_bytes((int)p, 4), lreg = jacobi_reg_bytes((int)p);
     if (p > kBlockJacobiMinP)  // A does not fit one CU's LDS: block Jacobi over many workgroups
         return cq::bj_eigh(A, p, batch, max_sweeps, tol, evals, V32, V64, sweeps_out, ws, ws_bytes, s);
-    // opt-in (CQ_EIGH=trid), p <= 192 without fp64 vectors: Householder tridiagonalisation +
-    // bisection + twisted factorisations (cq_trid.hip); a batch with a near-degenerate pair runs
-    // the Jacobi below.  Not the default: ~4.5 ms per B = 256 call with vectors, 2.9 ms for
-    // values, against the Jacobi's 1-5 warm sweeps
-    static const bool use_trid = [] { const char* e = getenv("CQ_EIGH"); return e && e[0] == 't'; }();
-    if (!V64 && use_trid && cq::trid_supported(p)) {
-        int fallback = 0;
-        const int rc = cq::trid_eigh(A, p, batch, evals, V32, ws, ws_bytes, s, &fallback);
-        if (rc != 0) return rc;
-        if (!fallback) {
-            if (sweeps_out && hipMemsetD32Async(sweeps_out, 1, (size_t)batch, s) != hipSuccess)
-                return set_error(CQ_EHIP, "cq_jacobi_eigh: memset failed");
-            return 0;
-        }
-    }
-    if (p <= 192 && lreg <= 160 * 1024) {
-        // fp64 A in LDS, V in registers (no per-round memory traffic for V)
-        if (p <= 64)
-            jacobi_reg_kernel<1, 2, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
-        else if (p <= 128)
-            jacobi_reg_kernel<2, 4, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
-        else
-            jacobi_reg_kernel<3, 6, 1, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
-    } else if (l32 <= 160 * 1024) {
-        jacobi_lds_kernel<float><<<(unsigned)batch, kSmallThreads, l32, s>>>(
-            A, (int)p, max_sweeps, std::max(tol, 1e-7), Vt, evals, V32, V64, sweeps_out);
-    } else {
-        const size_t lds = 2 * H * sizeof(double) + 2 * (2 * H) * sizeof(int);
-        jacobi_kernel<<<(unsigned)batch, kSmallThreads, lds, s>>>(
-            A, (int)p, max_sweeps, tol, Vt, evals, V32, V64, sweeps_out);
-    }
+    // p <= 192: fp64 A packed in LDS, V in registers (no per-round memory traffic for V)
+    const size_t lreg = jacobi_reg_bytes((int)p);
+    CQ_REQUIRE(lreg <= 160 * 1024, "cq_jacobi_eigh: LDS budget");
+    if (p <= 64)
+        jacobi_reg_kernel<1, 2, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+    else if (p <= 128)
+        jacobi_reg_kernel<2, 4, 2, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
+    else
+        jacobi_reg_kernel<3, 6, 1, 1024><<<(unsigned)batch, 1024, lreg, s>>>(A, (int)p, max_sweeps, tol, evals, V32, V64, sweeps_out);
     return check_launch("cq_jacobi_eigh");
 }
 

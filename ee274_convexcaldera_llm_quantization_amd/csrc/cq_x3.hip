@@ -4,16 +4,18 @@
 // Every fp32 operand x is carried as two fp16 halves, x*s = hi + lo with hi = f16(x*s) and
 // lo = f16(x*s - hi) (s a power of two), so x*s is represented to 2^-22 relative.  A product
 // sum_k a_k b_k is then hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b term is
-// 2^-22 relative), each term on v_mfma_f32_32x32x16_f16 with fp32 accumulation: three fp16
-// MFMAs at 16x the fp32 MFMA rate give fp32-grade products (measured error equal to the
-// fp32 MFMA GEMM's) at 5.3x the fp32 peak.
+// 2^-22 relative), each term one v_mfma_f32_16x16x32_f16 with fp32 accumulation: three fp16
+// MFMAs give fp32-grade products (measured error at or below the fp32 MFMA GEMM's,
+// DESIGN.md) on the fp16 matrix cores.
 //
 // Layout: the filter iterates on X^T (p x k, row-major) so both operands are K-contiguous:
 //   C[j][i] = sum_k Xt[j][k] G[i][k]   ( = (G X)^T since G = G^T )
-// Tile 192 (rows of Xt) x 256 (rows of G) x 32, 512 threads = 8 waves of 96 x 64 (3 x 2
-// MFMA blocks).  LDS images [row][k] with an 80-byte row stride (64 B data + 16 B pad) make
-// both the 16-byte stage writes and the ds_read_b128 fragment reads conflict-free; two
-// stages (140 KB) double-buffer the K loop with a register prefetch.
+// gemm_x3v_kernel: tile 192 (rows of Xt) x 384 (rows of G) x 32, 768 threads = 12 waves of
+// 96 x 64 (6 x 4 blocks of 16 x 16), operands global -> LDS by LDS-DMA into a 2-stage ring
+// (144 KB; a 4-slot ring of hi halves only for the single-product steps), XOR-swizzled 16-B
+// chunks so fragment reads are conflict-free; the transposed MFMA operand order gives each
+// lane 4 consecutive output columns for a vectorised epilogue (Chebyshev recurrence, split
+// halves of the next iterate, or the Gram's mirrored K-blocked halves).
 #include <type_traits>
 
 #include "cq_common.h"
@@ -22,16 +24,6 @@ namespace cq {
 
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 using f32x16v = __attribute__((ext_vector_type(16))) float;
-
-constexpr int X3_BM = 192, X3_BN = 256, X3_BK = 32;
-constexpr int X3_LD = 40;  // LDS row stride in halves
-constexpr int X3_THREADS = 512;
-constexpr int X3_NA = (2 * X3_BM * 4) / X3_THREADS;  // 16-B chunks per thread per stage: A (hi+lo)
-constexpr int X3_NB = (2 * X3_BN * 4) / X3_THREADS;  // B (hi+lo)
-constexpr int X3_A_HALVES = 2 * X3_BM * X3_LD;
-constexpr int X3_STAGE = X3_A_HALVES + 2 * X3_BN * X3_LD;  // halves per stage
-constexpr size_t X3_LDS_BYTES = 2 * X3_STAGE * sizeof(_Float16);
-static_assert((2 * X3_BM * 4) % X3_THREADS == 0 && (2 * X3_BN * 4) % X3_THREADS == 0, "chunking");
 
 struct X3K {
     int64_t M, N, K, batch;
@@ -46,13 +38,11 @@ struct X3K {
     float out_scale;
     int* overflow;
     int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
-    int noskip;  // A/B switch (CQ_X3_NOSKIP=1): dead waves run their MFMAs anyway
     int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
     const int* active;  // per batch (NULL = all): inactive entries skip the product, C = D
     int a_blocked;  // A halves K-blocked [K/32][lda rows][32] (lda = rows)
     int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
     int64_t tiles_n, tiles_m;
-    int probe;  // accumulate shader / constant-clock ticks per workgroup (clock diagnostics)
     int single;                // one product hi x hi (lo halves not read): ~2^-11 relative
     int sym_out;               // tri Gram: write the blocked split of the symmetric C (mirrored upper)
     const double* out_bound;   // [batch] bound on max|C|: split scale 2^(14 - e)
@@ -66,335 +56,18 @@ __device__ __forceinline__ float sym_split_scale(double bound) {
     return ldexpf(1.f, 14 - e);
 }
 
-// clock diagnostics (CQ_X3_CLOCK=1): sum over workgroups of s_memtime (shader clock) and
-// s_memrealtime (100 MHz) ticks; their ratio is the average shader clock under this load
-__device__ unsigned long long cq_clk_acc[2];
-
-__device__ __forceinline__ void x3_load(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
-                                        uint4 (&ra)[X3_NA], uint4 (&rb)[X3_NB]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int it = 0; it < X3_NA; ++it) {
-        const int idx = t + it * X3_THREADS;
-        const int part = idx / (X3_BM * 4), rem = idx % (X3_BM * 4);
-        const int row = rem >> 2, ch = rem & 3;
-        const int64_t gr = m0 + row;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (gr < a.M) {
-            const _Float16* src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + ch * 8;
-            v = *reinterpret_cast<const uint4*>(src);
-        }
-        ra[it] = v;
-    }
-#pragma unroll
-    for (int it = 0; it < X3_NB; ++it) {
-        const int idx = t + it * X3_THREADS;
-        const int part = idx / (X3_BN * 4), rem = idx % (X3_BN * 4);
-        const int row = rem >> 2, ch = rem & 3;
-        const int64_t gr = n0 + row;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (gr < a.N) {
-            const _Float16* src = (part ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + ch * 8;
-            v = *reinterpret_cast<const uint4*>(src);
-        }
-        rb[it] = v;
-    }
-}
-
-__device__ __forceinline__ void x3_store(_Float16* st, const uint4 (&ra)[X3_NA], const uint4 (&rb)[X3_NB]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int it = 0; it < X3_NA; ++it) {
-        const int idx = t + it * X3_THREADS;
-        const int part = idx / (X3_BM * 4), rem = idx % (X3_BM * 4);
-        const int row = rem >> 2, ch = rem & 3;
-        *reinterpret_cast<uint4*>(st + part * X3_BM * X3_LD + row * X3_LD + ch * 8) = ra[it];
-    }
-    _Float16* sb = st + X3_A_HALVES;
-#pragma unroll
-    for (int it = 0; it < X3_NB; ++it) {
-        const int idx = t + it * X3_THREADS;
-        const int part = idx / (X3_BN * 4), rem = idx % (X3_BN * 4);
-        const int row = rem >> 2, ch = rem & 3;
-        *reinterpret_cast<uint4*>(sb + part * X3_BN * X3_LD + row * X3_LD + ch * 8) = rb[it];
-    }
-}
-
-__device__ __forceinline__ void x3_compute(f32x16v (&acc)[3][2], const _Float16* sA, int wm, int wn, int lr, int lh) {
-    const _Float16* sB = sA + X3_A_HALVES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const int ko = 16 * s + 8 * lh;
-        f16x8 ah[3], al[3], bh[2], bl[2];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int row = 96 * wm + 32 * i + lr;
-            ah[i] = *reinterpret_cast<const f16x8*>(sA + row * X3_LD + ko);
-            al[i] = *reinterpret_cast<const f16x8*>(sA + X3_BM * X3_LD + row * X3_LD + ko);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int row = 64 * wn + 32 * j + lr;
-            bh[j] = *reinterpret_cast<const f16x8*>(sB + row * X3_LD + ko);
-            bl[j] = *reinterpret_cast<const f16x8*>(sB + X3_BN * X3_LD + row * X3_LD + ko);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-    }
-}
-
-template <int PF>
-__global__ __launch_bounds__(X3_THREADS, 1) void gemm_x3_kernel(X3K a) {
-    extern __shared__ __attribute__((aligned(16))) char x3_smem_raw[];
-    _Float16* smem = reinterpret_cast<_Float16*>(x3_smem_raw);
-
-    // XCD-aware tile order: consecutive hardware workgroup ids go round-robin over the 8
-    // XCDs; give each XCD a contiguous run of logical tiles so the tiles of one matrix
-    // (which share the X^T slices) meet in the same L2.
-    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-    int64_t lin = blockIdx.x;
-    if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
-    const int64_t tn = lin % a.tiles_n;
-    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
-    const int64_t b = lin / (a.tiles_n * a.tiles_m);
-    const int64_t m0 = tm * X3_BM, n0 = tn * X3_BN;
-    if (a.tri && n0 + X3_BN <= m0) return;  // strictly below the diagonal: mirrored later
-
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid & 1, wn = wid >> 1;  // wave tile: rows 96 wm .. +96, cols 64 wn .. +64
-    const int lr = lane & 31, lh = lane >> 5;
-
-    f32x16v acc[3][2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const bool live = !a.active || a.active[b];
-    const int64_t nt = live ? a.K / X3_BK : 0;
-    if (PF == 1) {
-        uint4 ra[X3_NA], rb[X3_NB];
-        if (nt > 0) {
-            x3_load(a, b, m0, n0, 0, ra, rb);
-            x3_store(smem, ra, rb);
-        }
-        __syncthreads();
-        for (int64_t t = 0; t < nt; ++t) {
-            const int cur = (int)(t & 1);
-            if (t + 1 < nt) x3_load(a, b, m0, n0, (t + 1) * X3_BK, ra, rb);
-            x3_compute(acc, smem + cur * X3_STAGE, wm, wn, lr, lh);
-            if (t + 1 < nt) x3_store(smem + (1 - cur) * X3_STAGE, ra, rb);
-            __syncthreads();
-        }
-    } else {
-        // prefetch distance 2: the loads of step t+2 are issued before step t computes and
-        // land in LDS at the end of step t+1, so two steps of MFMA work cover their latency
-        uint4 ra0[X3_NA], rb0[X3_NB], ra1[X3_NA], rb1[X3_NB];
-        if (nt > 0) {
-            x3_load(a, b, m0, n0, 0, ra0, rb0);
-            if (nt > 1) x3_load(a, b, m0, n0, X3_BK, ra1, rb1);
-            x3_store(smem, ra0, rb0);
-        }
-        __syncthreads();
-        for (int64_t t = 0; t < nt; t += 2) {
-            if (t + 2 < nt) x3_load(a, b, m0, n0, (t + 2) * X3_BK, ra0, rb0);
-            x3_compute(acc, smem, wm, wn, lr, lh);
-            if (t + 1 < nt) x3_store(smem + X3_STAGE, ra1, rb1);
-            __syncthreads();
-            if (t + 1 >= nt) break;
-            if (t + 3 < nt) x3_load(a, b, m0, n0, (t + 3) * X3_BK, ra1, rb1);
-            x3_compute(acc, smem + X3_STAGE, wm, wn, lr, lh);
-            if (t + 2 < nt) x3_store(smem, ra0, rb0);
-            __syncthreads();
-        }
-    }
-
-    // epilogue: C = alpha * acc * inv_scale + beta * P + gamma * D; optional fp16 split of C
-    const float sc = a.inv_scale[b];
-    // inactive entries (converged matrices) pass D through unchanged
-    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
-    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
-    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
-    bool ovf = false;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t col = n0 + 64 * wn + 32 * j + lr;
-            if (col >= a.N) continue;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + 96 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (row >= a.M) continue;
-                float v = al_ * (acc[i][j][r] * sc);
-                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
-                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
-                a.C[b * a.sc + row * a.ldc + col] = v;
-                if (a.Oh) {
-                    const float hs = v * a.out_scale;
-                    const _Float16 h = (_Float16)hs;
-                    const _Float16 l = (_Float16)(hs - (float)h);
-                    a.Oh[b * a.so + row * a.ldo + col] = h;
-                    a.Ol[b * a.so + row * a.ldo + col] = l;
-                    ovf |= !(fabsf(hs) < 65504.f);
-                }
-            }
-        }
-    if (ovf) atomicOr(a.overflow + b, 1);
-}
-
-
-// ------------------------------------------------------------------ LDS-DMA pipelined variant
-// Tile 192 x 192 x 32, 512 threads = 8 waves of 96 x 48 (6 x 3 blocks of
-// v_mfma_f32_16x16x32_f16).  Operands go global -> LDS by global_load_lds_dwordx4 (no
-// register staging) into a 3-stage ring (48 KB per stage: hi/lo of 192 A rows and 192 B
-// rows, 64 B each); the loads of stage t+2 are issued right after the barrier of step t
-// and stay in flight across it (counted vmcnt, raw s_barrier: a __syncthreads() would
-// drain them).  LDS images are linear per wave-instruction (16 rows x 64 B) with the 16-B
-// chunk index XOR-swizzled by (row >> 2) & 3 on the global source address, so the
-// fragment reads (16 rows x one chunk per 16 lanes) are conflict-free.
-constexpr int XG_BM = 192, XG_BN = 192, XG_BK = 32;
-constexpr int XG_THREADS = 512;
-constexpr int XG_PART = XG_BM * XG_BK;              // halves per part image (A and B alike)
-constexpr int XG_STAGE = 4 * XG_PART;                // Ah, Al, Bh, Bl
-constexpr int XG_NSTAGE = 3;
-constexpr size_t XG_LDS_BYTES = (size_t)XG_NSTAGE * XG_STAGE * sizeof(_Float16);  // 144 KB
-constexpr int XG_INSTR = 4 * XG_BM / 16;             // wave-instructions per stage (48)
-constexpr int XG_PER_WAVE = XG_INSTR / (XG_THREADS / 64);  // 6
-static_assert(XG_BM == XG_BN, "parts share one geometry");
-static_assert(XG_PER_WAVE == 6, "vmcnt counts below assume 6 loads per wave per stage");
-
+// ------------------------------------------------------------------ LDS images
+// LDS images are linear per wave-instruction (16 rows x 64 B) with the 16-B chunk index
+// XOR-swizzled by (row >> 2) & 3 on the global source address, so the fragment reads (16
+// rows x one chunk per 16 lanes) are conflict-free.
+constexpr int XG_BK = 32;
 using f16x8g = __attribute__((ext_vector_type(8))) _Float16;
 using f32x4v = __attribute__((ext_vector_type(4))) float;
-
-__device__ __forceinline__ void xg_issue(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t k0,
-                                         _Float16* stage, int wid, int lane) {
-#pragma unroll
-    for (int u = 0; u < XG_PER_WAVE; ++u) {
-        const int I = wid * XG_PER_WAVE + u;
-        const int part = I / 12, sub = I % 12;       // part: 0 Ah, 1 Al, 2 Bh, 3 Bl
-        const int row = 16 * sub + (lane >> 2);
-        const int c = (lane & 3) ^ ((row >> 2) & 3);  // logical chunk stored at this lane's slot
-        const bool isA = part < 2;
-        const int64_t base = isA ? m0 : n0;
-        const int64_t lim = isA ? a.M : a.N;
-        int64_t gr = base + row;
-        gr = gr < lim ? gr : lim - 1;                 // clamp: rows past the edge feed only unstored outputs
-        const _Float16* src;
-        if (isA) src = (part ? a.Al : a.Ah) + b * a.sa + gr * a.lda + k0 + c * 8;
-        else if (a.b_blocked) src = (part == 3 ? a.Bl : a.Bh) + b * a.sb + (k0 >> 5) * (a.ldb * 32) + gr * 32 + c * 8;
-        else src = (part == 3 ? a.Bl : a.Bh) + b * a.sb + gr * a.ldb + k0 + c * 8;
-        _Float16* dst = stage + part * XG_PART + (16 * sub) * XG_BK;
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-}
 
 __device__ __forceinline__ f16x8g xg_frag(const _Float16* img, int row, int chunk) {
     const int pc = chunk ^ ((row >> 2) & 3);
     return *reinterpret_cast<const f16x8g*>(img + row * XG_BK + pc * 8);
 }
-
-__global__ __launch_bounds__(XG_THREADS, 1) void gemm_x3g_kernel(X3K a) {
-    extern __shared__ __attribute__((aligned(16))) char xg_smem_raw[];
-    _Float16* smem = reinterpret_cast<_Float16*>(xg_smem_raw);
-
-    // bijective XCD remap: the tiles of one matrix run on one XCD (shared X^T slices in L2)
-    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-    const int64_t tn = lin % a.tiles_n;
-    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
-    const int64_t b = lin / (a.tiles_n * a.tiles_m);
-    const int64_t m0 = tm * XG_BM, n0 = tn * XG_BN;
-    if (a.tri && n0 + XG_BN <= m0) return;
-
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 48 wn .. +48
-    const int l16 = lane & 15, lq = lane >> 4;
-
-    f32x4v acc[6][3];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-    const bool live = !a.active || a.active[b];
-    const int64_t nt = live ? a.K / XG_BK : 0;
-    if (nt > 0) xg_issue(a, b, m0, n0, 0, smem, wid, lane);
-    if (nt > 1) xg_issue(a, b, m0, n0, XG_BK, smem + XG_STAGE, wid, lane);
-    for (int64_t t = 0; t < nt; ++t) {
-        // stage t landed (this wave's part): leave stage t+1's 6 loads in flight
-        if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's part of stage t landed; stage t-1 fully read
-        if (t + 2 < nt) xg_issue(a, b, m0, n0, (t + 2) * XG_BK, smem + ((t + 2) % XG_NSTAGE) * XG_STAGE, wid, lane);
-        const _Float16* st = smem + (t % XG_NSTAGE) * XG_STAGE;
-        f16x8g ah[6], al[6], bh[3], bl[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int row = 48 * wn + 16 * j + l16;
-            bh[j] = xg_frag(st + 2 * XG_PART, row, lq);
-            bl[j] = xg_frag(st + 3 * XG_PART, row, lq);
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int row = 96 * wm + 16 * i + l16;
-            ah[i] = xg_frag(st, row, lq);
-            al[i] = xg_frag(st + XG_PART, row, lq);
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-    }
-
-    const float sc = a.inv_scale[b];
-    // inactive entries (converged matrices) pass D through unchanged
-    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
-    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
-    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
-    bool ovf = false;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int64_t col = n0 + 48 * wn + 16 * j + l16;
-            if (col >= a.N) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = m0 + 96 * wm + 16 * i + 4 * lq + r;
-                if (row >= a.M) continue;
-                float v = al_ * (acc[i][j][r] * sc);
-                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
-                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
-                a.C[b * a.sc + row * a.ldc + col] = v;
-                if (a.Oh) {
-                    const float hs = v * a.out_scale;
-                    const _Float16 h = (_Float16)hs;
-                    const _Float16 l = (_Float16)(hs - (float)h);
-                    a.Oh[b * a.so + row * a.ldo + col] = h;
-                    a.Ol[b * a.so + row * a.ldo + col] = l;
-                    ovf |= !(fabsf(hs) < 65504.f);
-                }
-            }
-        }
-    if (ovf) atomicOr(a.overflow + b, 1);
-}
-
 
 // ------------------------------------------------------------------ wide-tile LDS-DMA variant
 // Tile 192 x 384 x 32 (12 waves of 96 x 64, 3 x 2 blocks of v_mfma_f32_32x32x16_f16), two
@@ -466,24 +139,8 @@ __device__ __forceinline__ void xw1_plan(const X3K& a, int64_t m0, int64_t n0, i
     }
 }
 
-__device__ __forceinline__ void xw1_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
-                                          const uint32_t (&off)[XW1_PER_WAVE]) {
-#pragma unroll
-    for (int u = 0; u < XW1_PER_WAVE; ++u) {
-        const int I = wid * XW1_PER_WAVE + u;
-        const bool isA = I < 12;
-        const int sub = isA ? I : I - 12;
-        const _Float16* base = isA ? a.Ah + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
-                                   : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
-        _Float16* dst = stage + (isA ? 0 : 2 * XW_APART) + (16 * sub) * XW_BK;
-        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
-                                         16, 0, 0);
-    }
-}
-
 // The 192 x 384 tile's K loop (shared by the filter/Gram product and the fused Q update):
 // acc = A[m0.., :] B[n0.., :]^T over K, split-fp16 products; nt = 0 leaves acc = 0.
-template <int MODE = 0>
 __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
                                             f32x16v (&acc)[3][2]) {
@@ -498,14 +155,13 @@ __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0,
     uint32_t off[XW_PER_WAVE];
     if (nt > 0) {
         xw_plan(a, m0, n0, wid, lane, off);
-        if (MODE != 2) xw_issue(a, b, 0, smem, wid, off);
+        xw_issue(a, b, 0, smem, wid, off);
     }
     for (int64_t t = 0; t < nt; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
-        if (MODE != 2 && t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
-        if (MODE == 1) continue;
+        if (t + 1 < nt) xw_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XW_STAGE, wid, off);
         const _Float16* sA = smem + (t & 1) * XW_STAGE;
         const _Float16* sB = sA + 2 * XW_APART;
 #pragma unroll
@@ -536,184 +192,6 @@ __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0,
     }
 }
 
-// ------------------------------------------------------------------ 4-stage ring (BK = 16)
-// Same 192 x 384 tile and wave layout, K steps of 16 in a 4-slot ring of 36 KB stages: the
-// loads of steps t+1..t+3 stay in flight while step t computes (counted vmcnt across raw
-// s_barriers), ~108 KB in flight per CU against one 72 KB stage of the 2-stage ring, whose
-// every step waited out a full HBM round trip.  Each wave-instruction fills 32 rows x 32 B
-// (one 16-deep half of a row's 64-B K-block run); the 16-B chunk index is XOR-swizzled by
-// (row >> 3) & 1 on the global source address so the fragment reads are conflict-free.
-constexpr int X4_BK = 16, X4_NS = 4;
-constexpr int X4_APART = XW_BM * X4_BK, X4_BPART = XW_BN * X4_BK;  // halves
-constexpr int X4_STAGE = 2 * X4_APART + 2 * X4_BPART;
-constexpr size_t X4_LDS_BYTES = (size_t)X4_NS * X4_STAGE * sizeof(_Float16);  // 144 KB
-constexpr int X4_PER_WAVE = (2 * XW_BM / 32 + 2 * XW_BN / 32) / (XW_THREADS / 64);  // 3
-static_assert(X4_PER_WAVE == 3, "vmcnt counts below assume 3 loads per wave per stage");
-static_assert(X4_LDS_BYTES <= 160 * 1024, "LDS");
-
-__device__ __forceinline__ void x4_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
-                                        uint32_t (&off)[X4_PER_WAVE]) {
-#pragma unroll
-    for (int u = 0; u < X4_PER_WAVE; ++u) {
-        const int I = wid * X4_PER_WAVE + u;  // 0..35: Ah 0-5, Al 6-11, Bh 12-23, Bl 24-35
-        const bool isA = I < 12;
-        const int part = isA ? (I >= 6) : (I >= 24);
-        const int sub = isA ? (I - 6 * part) : (I - 12 - 12 * part);
-        const int row = 32 * sub + (lane >> 1);
-        const int c = (lane & 1) ^ ((row >> 3) & 1);
-        const int64_t lim = isA ? a.M : a.N;
-        int64_t gr = (isA ? m0 : n0) + row;
-        gr = gr < lim ? gr : lim - 1;  // clamp: rows past the edge feed only unstored outputs
-        const int bw = isA ? (a.a_blocked == 2 ? 16 : 32) : (a.b_blocked == 2 ? 16 : 32);
-        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * bw + c * 8 : gr * a.lda + c * 8)
-                                : (a.b_blocked ? gr * bw + c * 8 : gr * a.ldb + c * 8));
-    }
-}
-
-__device__ __forceinline__ void x4_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
-                                         const uint32_t (&off)[X4_PER_WAVE]) {
-#pragma unroll
-    for (int u = 0; u < X4_PER_WAVE; ++u) {
-        const int I = wid * X4_PER_WAVE + u;
-        const bool isA = I < 12;
-        const int part = isA ? (I >= 6) : (I >= 24);
-        const int sub = isA ? (I - 6 * part) : (I - 12 - 12 * part);
-        const int64_t kb = (k0 >> 5) * 32, kr = k0 & 31;
-        const int64_t ka = a.a_blocked == 2 ? k0 * a.lda : kb * a.lda + kr;  // 16-blocked: k0 % 16 == 0
-        const int64_t kbb = a.b_blocked == 2 ? k0 * a.ldb : kb * a.ldb + kr;
-        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? ka : k0)
-                                   : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? kbb : k0);
-        _Float16* dst = stage + (isA ? part * X4_APART : 2 * X4_APART + part * X4_BPART) + (32 * sub) * X4_BK;
-        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
-                                         16, 0, 0);
-    }
-}
-
-__device__ __forceinline__ f16x8 x4_frag(const _Float16* img, int row, int chunk) {
-    const int pc = chunk ^ ((row >> 3) & 1);
-    return *reinterpret_cast<const f16x8*>(img + row * X4_BK + pc * 8);
-}
-
-template <int MODE = 0>
-__device__ __forceinline__ void x4_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
-                                            _Float16* smem, int wid, int lane, int wm, int wn,
-                                            f32x16v (&acc)[3][2]) {
-    const int lr = lane & 31, lh = lane >> 5;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    wid = __builtin_amdgcn_readfirstlane(wid);
-    uint32_t off[X4_PER_WAVE];
-    if (nt > 0) {
-        x4_plan(a, m0, n0, wid, lane, off);
-        if (MODE != 2)
-            for (int64_t s = 0; s < X4_NS - 1 && s < nt; ++s) x4_issue(a, b, s * X4_BK, smem + s * X4_STAGE, wid, off);
-    }
-    for (int64_t t = 0; t < nt; ++t) {
-        // stage t landed (this wave's part); the stages issued after it stay in flight
-        const int64_t after = nt - 1 - t;
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's part of stage t landed; slot of t-1 fully read
-        if (MODE != 2 && t + X4_NS - 1 < nt)
-            x4_issue(a, b, (t + X4_NS - 1) * X4_BK, smem + ((t + X4_NS - 1) & (X4_NS - 1)) * X4_STAGE, wid, off);
-        if (MODE == 1) continue;
-        const _Float16* sA = smem + (t & (X4_NS - 1)) * X4_STAGE;
-        const _Float16* sB = sA + 2 * X4_APART;
-        f16x8 ah[3], al[3], bh[2], bl[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int row = 64 * wn + 32 * j + lr;
-            bh[j] = x4_frag(sB, row, lh);
-            bl[j] = x4_frag(sB + X4_BPART, row, lh);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int row = 96 * wm + 32 * i + lr;
-            ah[i] = x4_frag(sA, row, lh);
-            al[i] = x4_frag(sA + X4_APART, row, lh);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-    }
-}
-
-template <int NS, int MODE = 0>
-__global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
-    extern __shared__ __attribute__((aligned(16))) char xw_smem_raw[];
-    _Float16* smem = reinterpret_cast<_Float16*>(xw_smem_raw);
-    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-    const int64_t tn = lin % a.tiles_n;
-    const int64_t tm = (lin / a.tiles_n) % a.tiles_m;
-    const int64_t b = lin / (a.tiles_n * a.tiles_m);
-    const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;
-    if (a.tri && n0 + XW_BN <= m0) return;
-
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
-    const int lr = lane & 31, lh = lane >> 5;
-    unsigned long long c0 = 0, r0 = 0;
-    if (a.probe && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-
-    f32x16v acc[3][2];
-    const bool live = !a.active || a.active[b];
-    if (NS == 2) xw_mainloop<MODE>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
-    else x4_mainloop<MODE>(a, b, m0, n0, live ? a.K / X4_BK : 0, smem, wid, lane, wm, wn, acc);
-
-    const float sc = a.inv_scale[b];
-    // inactive entries (converged matrices) pass D through unchanged
-    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
-    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
-    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
-    bool ovf = false;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t col = n0 + 64 * wn + 32 * j + lr;
-            if (col >= a.N) continue;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + 96 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (row >= a.M) continue;
-                float v = al_ * (acc[i][j][r] * sc);
-                if (a.P && be_ != 0.f) v += be_ * a.P[b * a.sp + row * a.ldp + col];
-                if (a.D && ga_ != 0.f) v += ga_ * a.D[b * a.sd + row * a.ldd + col];
-                a.C[b * a.sc + row * a.ldc + col] = v;
-                if (a.Oh) {
-                    const float hs = v * a.out_scale;
-                    const _Float16 h = (_Float16)hs;
-                    const _Float16 l = (_Float16)(hs - (float)h);
-                    const int64_t o = b * a.so + (a.o_blocked ? (col >> 5) * (a.M * 32) + row * 32 + (col & 31)
-                                                              : row * a.ldo + col);
-                    a.Oh[o] = h;
-                    a.Ol[o] = l;
-                    ovf |= !(fabsf(hs) < 65504.f);
-                }
-            }
-        }
-    if (ovf) atomicOr(a.overflow + b, 1);
-    if (a.probe && threadIdx.x == 0) {
-        atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
-        atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
-    }
-}
-
-
 // ------------------------------------------------------------------ 16x16x32 MFMA variant
 // Same tile, ring and LDS image as gemm_x3w_kernel; each wave's 96 x 64 block is 6 x 4
 // v_mfma_f32_16x16x32_f16 tiles (one MFMA per 32-deep K step and product instead of two
@@ -722,7 +200,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3w_kernel(X3K a) {
 // PERMB: block j's B fragment row for output register index t = 4 lq + r is LDS row
 // 64 wn + 16 (t >> 2) + 4 j + (t & 3), so lane (l16, lq) ends up holding the 16 consecutive
 // B rows 64 wn + 16 lq + [0, 16) in acc[i][0..3][0..3] (used by the fused Q update).
-template <bool PERMB = false, bool X1 = false>
+template <bool PERMB = false>
 __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
                                             f32x4v (&acc)[6][4]) {
@@ -732,14 +210,10 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
     wid = __builtin_amdgcn_readfirstlane(wid);
-    uint32_t off[X1 ? XW1_PER_WAVE : XW_PER_WAVE];
-    auto issue = [&](int64_t k0, _Float16* st) {
-        if constexpr (X1) xw1_issue(a, b, k0, st, wid, off);
-        else xw_issue(a, b, k0, st, wid, off);
-    };
+    uint32_t off[XW_PER_WAVE];
+    auto issue = [&](int64_t k0, _Float16* st) { xw_issue(a, b, k0, st, wid, off); };
     if (nt > 0) {
-        if constexpr (X1) xw1_plan(a, m0, n0, wid, lane, off);
-        else xw_plan(a, m0, n0, wid, lane, off);
+        xw_plan(a, m0, n0, wid, lane, off);
         issue(0, smem);
     }
     // a wave whose 96 x 64 output block lies wholly past the matrix edge (ragged last tiles)
@@ -751,7 +225,7 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
     // (PERMB: a fragment's 16 columns interleave with stride 16 across the wave's 64; the
     // wave-level test below only needs the block's first row and column)
     const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
-    uint32_t live = (a.noskip || (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0))) ? 1u : 0u;
+    uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
     live = __builtin_amdgcn_readfirstlane(live);
     if (!live) {  // the wave's whole 96 x 64 block is dead: its share of the loads and barriers only
         for (int64_t t = 0; t < nt; ++t) {
@@ -774,18 +248,12 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
         for (int j = 0; j < 4; ++j) {
             const int row = PERMB ? 64 * wn + 16 * (l16 >> 2) + 4 * j + (l16 & 3) : 64 * wn + 16 * j + l16;
             bh[j] = xg_frag(sB, row, lq);
-            if constexpr (!X1) bl[j] = xg_frag(sB + XW_BPART, row, lq);
+            bl[j] = xg_frag(sB + XW_BPART, row, lq);
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const int row = 96 * wm + 16 * i + l16;
             const f16x8 ah = xg_frag(sA, row, lq);
-            if constexpr (X1) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
-                continue;
-            }
             const f16x8 al = xg_frag(sA + XW_APART, row, lq);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {  // transposed block: lanes run over A rows, registers over B rows
@@ -847,7 +315,7 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
         for (int64_t s = 0; s < XV1_NS - 1 && s < nt; ++s) xv1_issue(a, b, s * XW_BK, smem + s * XV1_STAGE, wid, off);
     }
     const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
-    uint32_t live = (a.noskip || (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0))) ? 1u : 0u;
+    uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
     live = __builtin_amdgcn_readfirstlane(live);
     if (!live) {  // dead 96 x 64 block: its share of the loads and barriers only
         for (int64_t t = 0; t < nt; ++t) {
@@ -896,15 +364,13 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid & 1, wn = wid >> 1;  // rows 96 wm .. +96, cols 64 wn .. +64
     const int l16 = lane & 15, lq = lane >> 4;
-    unsigned long long c0 = 0, r0 = 0;
-    if (a.probe && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
 
     f32x4v acc[6][4];
     const bool live = !a.active || a.active[b];
     if constexpr (X1) {
         xv1_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
     } else {
-        xv_mainloop<false, false>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+        xv_mainloop<false>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
     }
 
     const float sc = a.inv_scale[b];
@@ -956,10 +422,6 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
                     }
                 }
             }
-        }
-        if (a.probe && threadIdx.x == 0) {
-            atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
-            atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
         }
         return;
     }
@@ -1033,10 +495,6 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
         }
     }
     if (ovf) atomicOr(a.overflow + b, 1);
-    if (a.probe && threadIdx.x == 0) {
-        atomicAdd(&cq_clk_acc[0], __builtin_amdgcn_s_memtime() - c0);
-        atomicAdd(&cq_clk_acc[1], __builtin_amdgcn_s_memrealtime() - r0);
-    }
 }
 
 
@@ -1062,7 +520,6 @@ struct QUK {
     float* scale;                // [batch] out (pass 1)
     const float* ew;             // error column weights [n] or NULL (= 1)
     double* part;                // [batch * tiles] error partials
-    const uint32_t* nrm;         // [batch * 4] max row norms of L hi/lo, R^T hi/lo (float bits), or NULL
 };
 
 template <int PASS, int BITS>
@@ -1808,80 +1265,18 @@ __device__ __forceinline__ f16x8g qp_frag(const _Float16* stage, int half, int r
     return *reinterpret_cast<const f16x8g*>(stage + (half * QP_BN + row) * QP_ROW + 8 * (chunk ^ qp_swz(row)));
 }
 
-// Largest row norms of the factor halves, per matrix: out[4 b + 0..3] = max_i ||Lh_i||,
-// max_i ||Ll_i||, max_j ||Rh_j||, max_j ||Rl_j|| (R^T rows), as float bits (atomicMax on
-// non-negative floats), each rounded up by 2^-10 (covers the fp32 sum of K <= 256 squares).
-// They bound how far the hi x hi product can sit from the split product (approximate pass 0).
-__global__ __launch_bounds__(256) void qp_norms_kernel(const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
-                                                       const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl,
-                                                       int64_t m, int64_t n, int K, uint32_t* __restrict__ out) {
-    // 16 lanes per row (16-byte loads, coalesced), 16 rows per block step, a grid-stride loop
-    // over rows and one atomic per block and value (same-address atomics serialise)
-    const int64_t b = blockIdx.y;
-    const int sub = threadIdx.x & 15;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); i < m + n; i += (int64_t)gridDim.x * 16) {
-        const bool isR = i >= m;
-        const int64_t row = isR ? i - m : i;
-        const uint16_t* ph = (isR ? Rh + b * n * (int64_t)K : Lh + b * m * (int64_t)K) + row * K;
-        const uint16_t* pl = (isR ? Rl + b * n * (int64_t)K : Ll + b * m * (int64_t)K) + row * K;
-        float sh = 0.f, sl = 0.f;
-        for (int k = 8 * sub; k < K; k += 128) {
-            const f16x8g h = *reinterpret_cast<const f16x8g*>(ph + k);
-            const f16x8g l = *reinterpret_cast<const f16x8g*>(pl + k);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float a = (float)h[e], c = (float)l[e];
-                sh += a * a;
-                sl += c * c;
-            }
-        }
-#pragma unroll
-        for (int off = 8; off > 0; off >>= 1) {   // the row's 16 lanes (aligned groups of 16)
-            sh += __shfl_xor(sh, off, 64);
-            sl += __shfl_xor(sl, off, 64);
-        }
-        const int t = isR ? 2 : 0;
-        v[t] = fmaxf(v[t], sqrtf(sh) * (1.f + 0x1p-10f));
-        v[t + 1] = fmaxf(v[t + 1], sqrtf(sl) * (1.f + 0x1p-10f));
-    }
-    __shared__ uint32_t red[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const uint32_t mx = wave_max_u32(__float_as_uint(v[t]));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = mx;
-    }
-    __syncthreads();
-    if (threadIdx.x < 4) {
-        const uint32_t mx = max(max(red[0][threadIdx.x], red[1][threadIdx.x]), max(red[2][threadIdx.x], red[3][threadIdx.x]));
-        if (mx) atomicMax(out + 4 * b + threadIdx.x, mx);
-    }
-}
-
 // RB row-blocks of 16 rows per wave; K = r <= 32 KSMAX.  FAST (pass 1): the scale is a
 // finite normal number and |res| <= scale, so x / s and c / k take the branch-free correctly
 // rounded division (div_fast; same results as IEEE division), and 2-bit dequantisation is
 // c * s (k = 1: (c / 1) * s is exactly c * s).  The per-element arithmetic runs on packed
 // fp32 pairs (v_pk_mul/add/fma_f32: two elements per VALU issue, each rounded as the scalar
 // op would be), so pass 1's epilogue costs about half the VALU issue slots.
-//
-// AP (pass 0 only): approximate absmax with an exact fix-up.  The chunk's residual is first
-// formed from the hi x hi product alone (one MFMA instead of three); q.nrm bounds how far any
-// such value v' can sit from the split-product value v: |v - v'| <= e (Cauchy-Schwarz on the
-// dropped hi x lo and lo x hi terms, plus the fp32 accumulation and rounding terms).  The wave
-// keeps rw = max |v'| seen so far (a lower bound of the matrix's max |v'|, M').  The element
-// holding the exact max |v| has |v'| >= M' - 2e >= rw - 2e, so a chunk with no element at or
-// above rw - 2e cannot hold it; every other chunk (the first one, and a handful of running-
-// max records after it) is recomputed with the split product, in exactly pass 1's MFMA order,
-// and only those exact values enter the max.  So the max, hence the scale and every code,
-// is bit-identical to the exact pass.
 typedef float qf2 __attribute__((ext_vector_type(2)));
 
-template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, bool AP, int NW, bool PW = false>
+template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, int NW>
 __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
                                         const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl, int K,
                                         int panels, _Float16* smem) {
-    static_assert(!AP || PASS == 0, "approximate absmax is a pass-0 mode");
     constexpr int ROWS = NW * 16 * RB;
     constexpr int WV = DT == CQ_F16 ? 1 : 2;        // uint4 per lane-run of 8 W elements
     const int64_t m = q.m, n = q.n, MN = m * n;
@@ -1927,18 +1322,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const float ys = 1.f / s, yk = 1.f / kq;
     uint32_t mx = 0;
     double err = 0.0;
-    // AP: e2 = 2 e, e bounding |v - v'| for every element of this matrix (see above)
-    float e2 = 0.f;
-    uint32_t rw = 0;   // AP: wave-uniform running max of |v'| (float bits)
-    if constexpr (AP) {
-        const float nLh = __uint_as_float(q.nrm[4 * b]), nLl = __uint_as_float(q.nrm[4 * b + 1]);
-        const float nRh = __uint_as_float(q.nrm[4 * b + 2]), nRl = __uint_as_float(q.nrm[4 * b + 3]);
-        const float cross = nLh * nRl + nLl * nRh;                 // the dropped hi x lo, lo x hi terms
-        const float gam = (float)(4 * K + 64) * 0x1p-24f;         // fp32 accumulation of both sums
-        const float eacc = (cross + gam * (nLh * nRh + cross)) * (1.f + 0x1p-8f);
-        e2 = 2.f * (sc * eacc * (1.f + 0x1p-8f)) + 0x1p-120f;
-        if (!(e2 < 0x1p100f)) e2 = __builtin_inff();              // non-finite factors: all exact
-    }
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -2018,58 +1401,17 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     // chunks ahead, with pass 1's packed stores deferred to the next chunk so a counted wait
     // could leave R(ch+2) in flight, measured slower: pass 0 3.13 vs 3.20 ms, pass 1 5.77 vs
     // 5.02 ms per B = 256 call -- the passes are not waiting on the R^T stages.)
-    //
-    // PW (pass 0): W in pairs of chunks.  A wave's W load covers 16 rows x 64 B of one chunk,
-    // so consecutive chunks hit each row's 128-B line (and DRAM page) a chunk apart; with PW
-    // an even chunk ch issues W(ch+2) and W(ch+3) back to back (each row's 128 B together;
-    // four register buffers, loop unrolled by 4) and an odd chunk issues none.  End-of-chunk
-    // waits: even, vmcnt(2 nW) (or nW past the end) leaves both in flight and retires R(ch+1)
-    // and W(ch+1) (issued two chunks earlier); odd, vmcnt(0).
     constexpr int WAHEAD = PASS == 0 ? 2 : 1;
-    static_assert(!PW || PASS == 0, "paired W loads are a pass-0 mode");
-    int nwl = 0;   // PW: W chunks issued by this chunk
-    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV], uint4 (&wl2)[RB][WV]) {
+    uint2 seg[RB];   // pass 1, 2-bit packed: a row's code bytes of the current 4-chunk group
+    auto chunk = [&](int64_t ch, uint4 (&wc)[RB][WV], uint4 (&wl)[RB][WV]) {
         const int64_t n0 = ch * QP_BN;
         if (ch + 1 < nchunks)  // next chunk's R^T (LDS-DMA) in flight during this chunk
             qp_issue_r<NW>(Rhb, Rlb, n0 + QP_BN, K, smem + ((ch + 1) & 1) * QP_STAGE, wid, lane);
         const bool wlive = ch + WAHEAD < nchunks;
-        if constexpr (PW) {
-            nwl = 0;
-            if ((ch & 1) == 0 && wlive) {
-                load_w(n0 + 2 * QP_BN, wl);
-                nwl = 1;
-                if (ch + 3 < nchunks) { load_w(n0 + 3 * QP_BN, wl2); nwl = 2; }
-            }
-        } else if (wlive) {
-            load_w(n0 + WAHEAD * QP_BN, wl);
-        }
+        if (wlive) load_w(n0 + WAHEAD * QP_BN, wl);
         const _Float16* st = smem + (ch & 1) * QP_STAGE;
         f32x4v acc[RB][2];
-        if constexpr (AP) {
-            mma(std::false_type{}, st, acc);
-            uint32_t lm = 0;
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) {
-                if (row0 + 16 * rb + l16 >= m) continue;
-                qf2 v[4];
-                resid(wc, acc, rb, v);
-                lm = vmax(v, lm);
-            }
-            // thr <= rw - 2e - 2^-18 rw (the last term covers the roundings of v and thr)
-            const float thr = __uint_as_float(rw) * (1.f - 0x1p-18f) - e2;
-            const bool cand = lm >= 0x7f800000u || rw >= 0x7f800000u || __uint_as_float(lm) >= thr;
-            if (__any(cand)) {
-                rw = max(rw, wave_max_u32(lm));
-                mma(std::true_type{}, st, acc);
-#pragma unroll
-                for (int rb = 0; rb < RB; ++rb) {
-                    if (row0 + 16 * rb + l16 >= m) continue;
-                    qf2 v[4];
-                    resid(wc, acc, rb, v);
-                    mx = vmax(v, mx);
-                }
-            }
-        } else {
+        {
             mma(std::true_type{}, st, acc);
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
@@ -2128,7 +1470,17 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                     for (int p = 0; p < 4; ++p)
                         acc2 = __builtin_elementwise_fma(cf[p], qf2{wt[2 * p], wt[2 * p + 1]}, acc2);
                     const uint32_t w16 = (uint32_t)(acc2.x + acc2.y);
-                    *reinterpret_cast<uint16_t*>(q.packed + (b * MN + e) / 4) = (uint16_t)w16;
+                    // a row's 8 code bytes of this chunk sit in lanes l16 + 16 t (t = 0..3): lane
+                    // lq == ch % 4 gathers them, and every 4 chunks each row stores 32 contiguous
+                    // bytes (whole 32-B sectors; one 2-B store per lane and chunk left 4.5x the
+                    // packed bytes in partial-line writes).  m % 16 == 0 keeps a row block, hence
+                    // the shuffles, wave-uniform.
+                    const int j = (int)(ch & 3);
+                    const uint32_t s0 = (uint32_t)__shfl((int)w16, l16), s1 = (uint32_t)__shfl((int)w16, l16 + 16);
+                    const uint32_t s2 = (uint32_t)__shfl((int)w16, l16 + 32), s3 = (uint32_t)__shfl((int)w16, l16 + 48);
+                    if (lq == j) seg[rb] = make_uint2(s0 | (s1 << 16), s2 | (s3 << 16));
+                    if ((j == 3 || ch + 1 == nchunks) && lq <= j)
+                        *reinterpret_cast<uint2*>(q.packed + (b * MN + row * n) / 4 + (ch - j + lq) * 8) = seg[rb];
                 }
                 int cq8[8];
                 if (q.codes || (BITS == 4 && q.packed)) {
@@ -2161,11 +1513,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         }
         // vmcnt in bits [3:0] and [15:14]; expcnt / lgkmcnt at their maxima (not waited)
         constexpr int nw = RB * WV;
-        if (PW && nwl == 2) {
-            __builtin_amdgcn_s_waitcnt(((2 * nw) & 15) | (((2 * nw) >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-        } else if (PW && nwl == 1) {
-            __builtin_amdgcn_s_waitcnt((nw & 15) | ((nw >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-        } else if (!PW && PASS == 0 && wlive) {
+        if (PASS == 0 && wlive) {
             __builtin_amdgcn_s_waitcnt((nw & 15) | ((nw >> 4) << 14) | (0x7 << 4) | (0xF << 8));
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2173,28 +1521,20 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
     };
     uint4 w3[PASS == 0 ? RB : 1][WV];
-    uint4 w4[PW ? RB : 1][WV];
     qp_issue_r<NW>(Rhb, Rlb, 0, K, smem, wid, lane);
     load_w(0, wr);
     if (PASS == 0 && nchunks > 1) load_w(QP_BN, wn);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if constexpr (PW) {
-        for (int64_t ch = 0; ch < nchunks; ch += 4) {
-            chunk(ch, wr, w3, w4);
-            if (ch + 1 < nchunks) chunk(ch + 1, wn, wn, wn);   // (odd chunks load nothing)
-            if (ch + 2 < nchunks) chunk(ch + 2, w3, wr, wn);
-            if (ch + 3 < nchunks) chunk(ch + 3, w4, w4, w4);
-        }
-    } else if constexpr (PASS == 0) {
+    if constexpr (PASS == 0) {
         for (int64_t ch = 0; ch < nchunks; ch += 3) {
-            chunk(ch, wr, w3, w3);
-            if (ch + 1 < nchunks) chunk(ch + 1, wn, wr, wr);
-            if (ch + 2 < nchunks) chunk(ch + 2, w3, wn, wn);
+            chunk(ch, wr, w3);
+            if (ch + 1 < nchunks) chunk(ch + 1, wn, wr);
+            if (ch + 2 < nchunks) chunk(ch + 2, w3, wn);
         }
     } else {
         for (int64_t ch = 0; ch < nchunks; ++ch) {
-            chunk(ch, wr, wn, wn);
+            chunk(ch, wr, wn);
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2211,7 +1551,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
 }
 
-template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW, bool AP = false, bool PW = false>
+template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW>
 __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uint16_t* __restrict__ Lh,
                                                                    const uint16_t* __restrict__ Ll,
                                                                    const uint16_t* __restrict__ Rh,
@@ -2220,7 +1560,7 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
     extern __shared__ __attribute__((aligned(16))) char qp_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(qp_smem_raw);
     if (PASS == 0) {
-        qp_body<PASS, BITS, DT, RB, KSMAX, false, AP, NW, PW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+        qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
         return;
     }
     // which matrix this workgroup serves (same mapping as qp_body) decides the division path
@@ -2229,8 +1569,8 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
     const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
     const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
     const float sb = quant_scale(q.absmax[lin / panels], q.eps);
-    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
-    else qp_body<PASS, BITS, DT, RB, KSMAX, false, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    else qp_body<PASS, BITS, DT, RB, KSMAX, false, NW>(q, Lh, Ll, Rh, Rl, K, panels, smem);
 }
 constexpr size_t QP_LDS_BYTES = (size_t)2 * QP_STAGE * sizeof(_Float16);  // 64 KB
 
@@ -2316,9 +1656,8 @@ size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
     // tile counts of both Q-update kernels (q_update_v_kernel tiles W as m x n, the 32x32
     // kernel as n x m)
     const int64_t tiles = qu_tiles(m, n);
-    // absmax bits | error partials | factor-half row norms (approximate absmax pass)
-    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) +
-           align_up((size_t)batch * tiles * sizeof(double), 256) + (size_t)batch * 4 * sizeof(uint32_t);
+    // absmax bits | error partials
+    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) + (size_t)batch * tiles * sizeof(double);
 }
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
@@ -2337,9 +1676,8 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     QUK q;
     X3K& a = q.x;
     memset(&a, 0, sizeof(a));  // a_blocked = b_blocked = 0, no active mask
-    static const bool legacy = getenv("CQ_QU_KERNEL") != nullptr;  // A/B switch: the 32x32 kernel
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    const bool vk = !legacy && n % 16 == 0 && al16(W) && (!codes || al16(codes)) && (!packed || al16(packed)) &&
+    const bool vk = n % 16 == 0 && al16(W) && (!codes || al16(codes)) && (!packed || al16(packed)) &&
                     (!err_w || al16(err_w));
     if (vk) {
         // A operand L (m x r): tile rows run over W's rows; B operand R^T (n x r): tile
@@ -2369,7 +1707,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     q.W = W; q.wf16 = dtype == CQ_F16; q.m = m; q.n = n;
     q.absmax = reinterpret_cast<uint32_t*>(ws);
     q.part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + align_up((size_t)batch * sizeof(uint32_t), 256));
-    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w; q.nrm = nullptr;
+    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w;
     hipStream_t s = as_stream(stream);
     const bool known = absmax_in && r == 0;  // max|W| bits given: skip the absmax pass
     if (known) {
@@ -2380,9 +1718,8 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     }
     const unsigned grid = (unsigned)(tiles * batch);
     // row-panel kernel (q_update_p_kernel): K <= 256, m % 16 == 0, n % 32 == 0, 16-B aligned
-    static const char* qu_env = getenv("CQ_QU_KERNEL");
     const bool pk = r > 0 && r <= QP_KMAX && m % 16 == 0 && n % QP_BN == 0 && vk && al16(Lh) && al16(Ll) &&
-                    al16(Rth) && al16(Rtl) && !(qu_env && qu_env[0] == 'v');
+                    al16(Rth) && al16(Rtl);
     if (pk && !known) {
         // pass 0 (absmax) and pass 1 (quantise + packing, more live values) may use different
         // panel geometries: every 16 x 16 output block runs the same MFMA sequence whatever
@@ -2397,33 +1734,9 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
         const uint16_t *lh = Lh, *ll = Ll, *rh = Rth, *rl = Rtl;
         const int Ki = (int)r;
         const unsigned g0 = (unsigned)(p0 * batch), g1 = (unsigned)(p1 * batch);
-        // CQ_QP0_APPROX=1: pass 0 on the hi x hi product with an exact fix-up of the candidate
-        // chunks (qp_body, AP).  Bit-identical max, but measured no faster (3.13-3.20 vs 3.3 ms
-        // per B = 256 call, plus the row-norm kernel): the pass is bound by its W stream (64 B
-        // per row per chunk), not by the MFMAs, so the split product stays the default.
-        static const bool approx0 = getenv("CQ_QP0_APPROX") != nullptr;
-        const bool ap = approx0 && (f16 || small);   // (fp32 W past r = 128: no VGPRs to spare)
-        // CQ_QP0_PAIRW=1: pass 0 loads W in pairs of chunks (qp_body, PW; fp16 W, r <= 128)
-        static const bool pairw = getenv("CQ_QP0_PAIRW") != nullptr;
-        const bool pw = pairw && f16 && small;
-        if (ap) {
-            uint32_t* nrm = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(q.part) +
-                                                        align_up((size_t)batch * qu_tiles(m, n) * sizeof(double), 256));
-            if (hipMemsetAsync(nrm, 0, (size_t)batch * 4 * sizeof(uint32_t), s) != hipSuccess)
-                return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
-            CQ_REQUIRE(batch < 65536, "cq_q_update_x3: batch too large");
-            qp_norms_kernel<<<dim3((unsigned)std::min<int64_t>(32, ceil_div(m + n, 16)), (unsigned)batch), 256, 0, s>>>(lh, ll, rh, rl, m, n,
-                                                                                                  Ki, nrm);
-            q.nrm = nrm;
-        }
 #define CQ_QP(PS, B, DTV, RBV, KSV, G, P) \
         q_update_p_kernel<PS, B, DTV, RBV, KSV, QP_WAVES><<<G, QP_WAVES * 64, QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)P)
-#define CQ_QP0(B, DTV, RBV, KSV) do { \
-            if (ap) q_update_p_kernel<0, B, DTV, RBV, KSV, QP_WAVES, true><<<g0, QP_WAVES * 64, QP_LDS_BYTES, s>>>( \
-                q, lh, ll, rh, rl, Ki, (int)p0); \
-            else if (pw) q_update_p_kernel<0, B, DTV, RBV, KSV, QP_WAVES, false, true><<<g0, QP_WAVES * 64, \
-                QP_LDS_BYTES, s>>>(q, lh, ll, rh, rl, Ki, (int)p0); \
-            else CQ_QP(0, B, DTV, RBV, KSV, g0, p0); } while (0)
+#define CQ_QP0(B, DTV, RBV, KSV) CQ_QP(0, B, DTV, RBV, KSV, g0, p0)
 #define CQ_QP_B(B) do { \
             if (f16 && small) { CQ_QP0(B, CQ_F16, 3, 4); CQ_QP(1, B, CQ_F16, 3, 4, g1, p1); } \
             else if (f16) { CQ_QP0(B, CQ_F16, 2, 8); CQ_QP(1, B, CQ_F16, 2, 8, g1, p1); } \
@@ -2523,17 +1836,6 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     return check_launch("cq_residual_split");
 }
 
-// clock diagnostics: returns the accumulated (shader ticks, 100 MHz ticks) and zeroes them
-int cq_x3_clock(unsigned long long* out) {
-    CQ_REQUIRE(out, "cq_x3_clock: null");
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cq_clk_acc), sizeof(unsigned long long) * 2) != hipSuccess)
-        return set_error(CQ_EHIP, "cq_x3_clock: copy failed");
-    const unsigned long long z[2] = {0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(cq_clk_acc), z, sizeof(z)) != hipSuccess)
-        return set_error(CQ_EHIP, "cq_x3_clock: reset failed");
-    return 0;
-}
-
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(g, "cq_gemm_x3: null args");
     CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && (g->C || g->sym_out) && g->inv_scale, "cq_gemm_x3: null operand");
@@ -2541,7 +1843,7 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
                                g->out_scale > 0.f && g->N % 32 == 0),
                "cq_gemm_x3: sym_out needs tri, out_h/out_l, out_bound, scale_out, inv_out, N % 32 == 0");
     CQ_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0 && g->batch > 0, "cq_gemm_x3: bad shape");
-    CQ_REQUIRE(g->K % X3_BK == 0, "cq_gemm_x3: K must be a multiple of 32");
+    CQ_REQUIRE(g->K % XW_BK == 0, "cq_gemm_x3: K must be a multiple of 32");
     CQ_REQUIRE(g->lda % 8 == 0 && g->ldb % 8 == 0 && g->stride_a % 8 == 0 && g->stride_b % 8 == 0,
                "cq_gemm_x3: operand rows must be 16-byte aligned");
     CQ_REQUIRE((g->a_blocked ? g->lda >= g->M : g->lda >= g->K) && (g->b_blocked ? g->ldb >= g->N : g->ldb >= g->K) &&
@@ -2579,56 +1881,16 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.active = g->active;
     a.a_blocked = g->a_blocked;
     a.o_blocked = g->o_blocked;
-    static const int probe = getenv("CQ_X3_CLOCK") ? 1 : 0;
-    a.probe = probe;
-    static const int noskip = getenv("CQ_X3_NOSKIP") ? 1 : 0;
-    a.noskip = noskip;
     CQ_REQUIRE(!g->o_blocked || g->N % 32 == 0, "cq_gemm_x3: blocked split output needs N % 32 == 0");
     CQ_REQUIRE(!g->a_blocked || g->lda >= g->M, "cq_gemm_x3: blocked A needs lda = rows >= M");
     CQ_REQUIRE(!g->active || g->D, "cq_gemm_x3: active needs D (the pass-through value)");
     CQ_REQUIRE(!g->b_blocked || g->ldb >= g->N, "cq_gemm_x3: blocked B needs ldb = rows >= N");
-    static const int variant = [] {
-        // A/B switch for benchmarking: "reg" register-staged 192x256, "g" LDS-DMA 192x192,
-        // "w2" LDS-DMA 192x384 2-stage ring on 32x32x16 MFMAs, "w4" 4-stage ring at BK 16
-        // (slower: 2.80 vs 2.52 ms per B = 128 filter product, tools/bench_filter.py); default
-        // ("v") the 2-stage ring on 16x16x32 MFMAs with the transposed, vectorised epilogue
-        // (2.66 vs 3.20 ms for the filter step)
-        const char* e = getenv("CQ_X3_KERNEL");
-        if (!e) return 8;
-        if (e[0] == 'w' && e[1] == '2') return e[2] == 'l' ? 4 : e[2] == 'm' ? 5 : 2;  // w2l / w2m: ablations
-        if (e[0] == 'w' && e[1] == '4') return e[2] == 'l' ? 6 : e[2] == 'm' ? 7 : 3;
-        if (e[0] == 'v') return 8;
-        return e[0] == 'r' ? 1 : e[0] == 'g' ? 0 : 3;
-    }();
-    CQ_REQUIRE(variant >= 2 || (!g->a_blocked && !g->o_blocked),
-               "cq_gemm_x3: blocked A / split output need the LDS-DMA 192x384 kernel");
-    CQ_REQUIRE(variant == 8 || (!g->sym_out && !g->single), "cq_gemm_x3: sym_out / single need the default kernel");
-    if (variant >= 2) {
-        a.tiles_n = ceil_div(g->N, XW_BN);
-        a.tiles_m = ceil_div(g->M, XW_BM);
-        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-        if (variant == 2) gemm_x3w_kernel<2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 4) gemm_x3w_kernel<2, 1><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 5) gemm_x3w_kernel<2, 2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 6) gemm_x3w_kernel<4, 1><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 7) gemm_x3w_kernel<4, 2><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 8 && a.single) gemm_x3v_kernel<true><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-        else if (variant == 8) gemm_x3v_kernel<false><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-        else gemm_x3w_kernel<4><<<(unsigned)total, XW_THREADS, X4_LDS_BYTES, as_stream(stream)>>>(a);
-    } else if (variant == 0 || g->b_blocked) {
-        a.tiles_n = ceil_div(g->N, XG_BN);
-        a.tiles_m = ceil_div(g->M, XG_BM);
-        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-        gemm_x3g_kernel<<<(unsigned)total, XG_THREADS, XG_LDS_BYTES, as_stream(stream)>>>(a);
-    } else {
-        a.tiles_n = ceil_div(g->N, X3_BN);
-        a.tiles_m = ceil_div(g->M, X3_BM);
-        const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-        CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-        gemm_x3_kernel<1><<<(unsigned)total, X3_THREADS, X3_LDS_BYTES, as_stream(stream)>>>(a);
-    }
+    a.tiles_n = ceil_div(g->N, XW_BN);
+    a.tiles_m = ceil_div(g->M, XW_BM);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+    if (a.single) gemm_x3v_kernel<true><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    else gemm_x3v_kernel<false><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     return check_launch("cq_gemm_x3");
 }
 

@@ -9,7 +9,7 @@ rank 0 (torch.distributed `gather`; backend "nccl" is RCCL over xGMI on MI355X, 
 CPU tests).
 
 Result payload (also the on-disk format, §8f item 2): one uint8 tensor per rank =
-  [u64 little-endian meta length][meta JSON][pad to 16][blob]
+  [magic "CQRS"][u32 format version][u64 little-endian meta length][meta JSON][pad to 16][blob]
 with, per matrix, int2/int4 offset-binary packed Q codes (or int8/int16 codes for 8/16 bits),
 fp32 L (m x r) and R (r x n), each 16-byte aligned, and in the JSON its name, shape, scales,
 global scale, error history and array offsets.  The payload is assembled where the results
@@ -36,6 +36,9 @@ LLAMA2_7B_PROJS = (("self_attn.q_proj", 4096, 4096), ("self_attn.k_proj", 4096, 
                    ("mlp.gate_proj", 11008, 4096), ("mlp.up_proj", 11008, 4096),
                    ("mlp.down_proj", 4096, 11008))
 _ALIGN = 16
+_MAGIC = b"CQRS"
+_VERSION = 2   # 1 = round-2 payloads (no magic/version word): rejected, they parse differently
+_HEAD = struct.Struct("<4sIQ")
 
 
 def llama2_7b_matrices(n_layers: int = 32):
@@ -99,17 +102,25 @@ def pack_results(results: list[MatrixResult], device=None) -> torch.Tensor:
             off += b.numel() + pad
         metas.append(entry)
     meta = json.dumps(metas).encode()
-    head = struct.pack("<Q", len(meta)) + meta
+    head = _HEAD.pack(_MAGIC, _VERSION, len(meta)) + meta
     head += b"\0" * _pad(len(head))
     head_t = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(dev)
     return torch.cat([head_t] + parts)
 
 
 def unpack_results(buf: torch.Tensor) -> list[MatrixResult]:
-    """Inverse of pack_results; arrays are views of `buf` on its device."""
-    (mlen,) = struct.unpack("<Q", bytes(buf[:8].cpu().numpy().tobytes()))
-    metas = json.loads(bytes(buf[8:8 + mlen].cpu().numpy().tobytes()).decode())
-    base = 8 + mlen + _pad(8 + mlen)
+    """Inverse of pack_results; arrays are views of `buf` on its device.  Raises ValueError
+    for a buffer without the payload magic or with an unknown format version."""
+    h = _HEAD.size
+    if buf.numel() < h:
+        raise ValueError("unpack_results: buffer shorter than the payload header")
+    magic, version, mlen = _HEAD.unpack(bytes(buf[:h].cpu().numpy().tobytes()))
+    if magic != _MAGIC:
+        raise ValueError("unpack_results: not a caldera result payload (bad magic)")
+    if version != _VERSION:
+        raise ValueError(f"unpack_results: unsupported payload format version {version} (expected {_VERSION})")
+    metas = json.loads(bytes(buf[h:h + mlen].cpu().numpy().tobytes()).decode())
+    base = h + mlen + _pad(h + mlen)
     out = []
     for e in metas:
         arrs = {}
@@ -183,7 +194,18 @@ def decompose_sharded(items, decompose_batch, *, rank: int, world: int, max_batc
         else:
             for b in batches:
                 results.extend(decompose_batch(b))
-    dev = device if device is not None else (results[0].L.device if results else torch.device("cpu"))
+    if device is not None:
+        dev = torch.device(device)
+    else:
+        # where the payload is assembled and gathered: in HBM for RCCL ("nccl"), on the host
+        # otherwise (gloo's gather takes CPU tensors), and for world 1 where the results live
+        dev = torch.device("cpu")
+        if world == 1 or not gather:
+            dev = results[0].L.device if results else dev
+        else:
+            import torch.distributed as dist
+            if dist.get_backend(group) == "nccl" and results:
+                dev = results[0].L.device
     if done:
         results.extend(MatrixResult(r.name, r.m, r.n, r.rank, r.Q_bits, r.codes.to(dev), r.Q_scale, r.L.to(dev),
                                     r.R.to(dev), r.global_scale, r.errors, r.extra) for r in done)

@@ -121,6 +121,7 @@ class _GroupProbe:
 
 QUANT_PROBE = _GroupProbe()
 LPLR_PROBE = _GroupProbe()  # the LPLR loop's m x n x r GEMMs (alg.py:162-177), bench roofline_lplr
+GRAM_PROBE = _GroupProbe()  # the split-fp16 Gram G = Y Y^T (or Y^T Y) of every solve, bench roofline_gram
 
 
 X3_SCALE = 2.0 ** 6  # power-of-two scale of the filter iterates' fp16 halves (entries <= ~1)
@@ -129,7 +130,11 @@ MAX_OUTER = 40  # outer iterations per solve (the schedule's last degree repeats
 
 
 JACOBI_MAX_SWEEPS = 30
-STALL_RATIO = 0.85
+# block Jacobi (p > 192) launches its whole sweep budget stream-ordered (no host read-back
+# inside cq_jacobi_eigh); the solver sizes the budget from the sweep counts it reads with
+# each convergence check and redoes an outer iteration whose budget ran out
+BJ_BUDGET_START, BJ_BUDGET_MIN, BJ_BUDGET_MARGIN = 12, 4, 3
+STALL_RATIO = 0.98
 
 
 class SolverStats:
@@ -138,7 +143,8 @@ class SolverStats:
         self.matvecs = 0
         self.x3_fallbacks = 0
         self.jacobi_unconverged = 0  # Rayleigh-Ritz eigensolves that used all JACOBI_MAX_SWEEPS
-        self.stalls = 0              # calls ended at the products' precision floor
+        self.jacobi_redo = 0         # outer iterations redone after a block-Jacobi budget ran out
+        self.stalls = 0              # matrices whose solve ended at the products' precision floor
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
@@ -146,7 +152,7 @@ class SolverStats:
 
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
-                    jacobi_unconverged=self.jacobi_unconverged, stalls=self.stalls,
+                    jacobi_unconverged=self.jacobi_unconverged, jacobi_redo=self.jacobi_redo, stalls=self.stalls,
                     max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks)
 
 
@@ -189,6 +195,10 @@ class RankRSolver:
         self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
         self.stats = SolverStats()
         self.valid_k = self.k  # rows >= valid_k of the eigenproblem are zero padding (engine.py)
+        # Rayleigh-Ritz sweep budget: fixed for the one-workgroup Jacobi (its sweep loop runs
+        # inside one kernel), adaptive for the block Jacobi (each sweep is a set of launches)
+        self.block_jacobi = self.p > 192
+        self.jac_budget = BJ_BUDGET_START if self.block_jacobi else JACOBI_MAX_SWEEPS
         self._bufs = None
         self._G = None
         self._yh = self._yl = None
@@ -301,11 +311,11 @@ class RankRSolver:
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps
-            theta, _, _, sw = K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=self.jacobi_tol_values,
+            theta, _, _, sw = K.jacobi_eigh(T, max_sweeps=self.jac_budget, tol=self.jacobi_tol_values,
                                             want_vectors=False)
             self._last_sw = sw
             return theta, X, None
-        theta, V32, _, sw = K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=self.jacobi_tol)
+        theta, V32, _, sw = K.jacobi_eigh(T, max_sweeps=self.jac_budget, tol=self.jacobi_tol)
         self._last_sw = sw
         Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
@@ -456,9 +466,16 @@ class RankRSolver:
             if ysq is None:
                 ysq = K.weighted_sqsum(Y, None, Y.shape[2])
             self._ysq = ysq
+            # fp16 MFMA work issued: 3 products x k^2 n (the upper half of the symmetric 2 k^2 n)
+            kk, nn = k, yh.shape[2]
+            gev = GRAM_PROBE.start("gram", 3.0 * kk * kk * nn * B, 4.0 * kk * nn * B + 4.0 * kk * kk * B)
+            if gev is not None:
+                gev[0].record()
             K.gemm_x3(yh, yl, yh, yl, yinv, None, tri=True, a_blocked=True, b_blocked=True,
                       out_h=self._Gh, out_l=self._Gl, out_scale=X3_SCALE, sym_bound=ysq,
                       scale_out=self._gscale, inv_out=self._ginv)
+            if gev is not None:
+                gev[1].record()
             g_split = True
         elif not self.x3:
             self._fill_G(Y)  # Y Y^T (upper tiles + mirror) or Y^T Y
@@ -502,6 +519,8 @@ class RankRSolver:
             degs = self.deg_warm
         self.stats.resid_hist = []
         used = []
+        hist = []                               # per-matrix test values of the full iterations
+        stalled = np.zeros(B, dtype=bool)
         n_outer = 0
         while n_outer < MAX_OUTER:
             d = degs[min(n_outer, len(degs) - 1)]
@@ -541,13 +560,25 @@ class RankRSolver:
                     res = K.ritz_residual(Xn, Zn, theta_n, self.r).double()
                 ovf = (self._ovf.max().double() if self.x3 and self._x3f
                        else torch.zeros((), dtype=torch.float64, device=dev))
-                # matrices whose Jacobi ran out of sweeps (read back with the residuals)
-                unconv = (self._last_sw >= JACOBI_MAX_SWEEPS).sum().double().view(1)
-                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res, unconv])
+                # matrices whose Jacobi used its whole sweep budget, and the most sweeps any
+                # matrix needed (read back with the residuals)
+                budget = self.jac_budget
+                unconv = (self._last_sw >= budget).sum().double().view(1)
+                maxsw = self._last_sw.max().double().view(1)
+                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res, unconv, maxsw])
                 yield
                 chk = chk.cpu().numpy()
-                self.stats.jacobi_unconverged += int(chk[-1])
-                chk = chk[:-1]
+                n_unconv, maxsw = int(chk[-2]), int(chk[-1])
+                chk = chk[:-2]
+                if self.block_jacobi:
+                    if n_unconv and budget < JACOBI_MAX_SWEEPS:
+                        # the block Jacobi's budget ran out: redo this outer iteration (same
+                        # inputs, deterministic kernels) with the full budget
+                        self.jac_budget = JACOBI_MAX_SWEEPS
+                        self.stats.jacobi_redo += 1
+                        continue
+                    self.jac_budget = min(JACOBI_MAX_SWEEPS, max(BJ_BUDGET_MIN, maxsw + BJ_BUDGET_MARGIN))
+                self.stats.jacobi_unconverged += n_unconv
                 if self.x3 and self._x3f and chk[0] != 0:
                     # an fp16 half overflowed (a Ritz value far below the true top of the
                     # spectrum, cold start): redo this outer iteration with the fp32 filter
@@ -566,18 +597,27 @@ class RankRSolver:
             ends = np.stack([chk[1:1 + B], chk[1 + B:1 + 2 * B]], 1)
             resid = chk[1 + 2 * B:]
             mr = float(resid.max())
-            # converged matrices sit out the remaining filter products (their X passes through)
-            self._active.copy_(torch.from_numpy((resid > self.tol).astype(np.int32)))
             self.stats.max_resid = mr
             self.stats.resid_hist.append(mr)
             used.append(d)
-            if mr <= self.tol:
-                break
-            # precision floor (split-fp16 products: ~2e-7 theta_0): a test that has stopped
-            # improving over two outer iterations ends the call instead of running to MAX_OUTER
-            fin = [v for v in self.stats.resid_hist if math.isfinite(v)]
-            if len(fin) >= 3 and fin[-1] > STALL_RATIO * min(fin[-3], fin[-2]):
-                self.stats.stalls += 1
+            if math.isfinite(mr) or np.isfinite(resid).any():
+                hist.append(resid.copy())
+            # precision floor (split-fp16 products), decided per matrix: a matrix whose test has
+            # not improved at all over its last two outer iterations (best of the two above
+            # STALL_RATIO x its best before them) is done; one still converging, however
+            # slowly, keeps iterating (the filter gains far more than 2 % per outer iteration
+            # unless the products' rounding dominates)
+            if len(hist) >= 3:
+                Hh = np.stack(hist)
+                before = np.min(Hh[:-2], axis=0)
+                recent = np.min(Hh[-2:], axis=0)
+                new_stall = (~stalled) & (resid > self.tol) & np.isfinite(before) & (recent > STALL_RATIO * before)
+                self.stats.stalls += int(new_stall.sum())
+                stalled |= new_stall
+            # converged (or stalled) matrices sit out the remaining filter products (X passes through)
+            live = (resid > self.tol) & ~stalled
+            self._active.copy_(torch.from_numpy(live.astype(np.int32)))
+            if not live.any():
                 break
         if Z is None:  # left the loop on a values-only iteration (MAX_OUTER): rotate once
             theta, X, Z = self._rr(X)

@@ -221,16 +221,6 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
                    double* evals, float* V32, double* V64, int* sweeps_out, void* ws,
                    size_t ws_bytes, void* stream);
 
-/* Symmetric eigendecomposition by Householder tridiagonalisation (fp64, A packed in one CU's
- * LDS, p <= 192), bisection and twisted factorisations, same output contract as
- * cq_jacobi_eigh (descending; V32 columns, may be NULL for values only; A not modified).
- * *fallback = 1: some matrix has a pair of eigenvalues closer than 1e-9 of the norm, whose
- * vectors this method does not orthogonalise -- V32 is then incomplete and the caller runs
- * cq_jacobi_eigh.  cq_jacobi_eigh uses it itself when CQ_EIGH=trid is set. */
-size_t cq_tridiag_workspace(int64_t p, int64_t batch);
-int cq_tridiag_eigh(const double* A, int64_t p, int64_t batch, double* evals, float* V32, void* ws,
-                    size_t ws_bytes, int* fallback, void* stream);
-
 /* Ritz residuals: out[b] = max_{i<r} ||Z[:,i] - theta_i X[:,i]||_2 / |theta_0|
  * (X, Z: k x p row-major with ld p).  theta fp64 [b*p..]. */
 size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch);
@@ -314,12 +304,6 @@ typedef struct cq_x3_args {
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
-
-/* Diagnostics: with the environment variable CQ_X3_CLOCK set at load time, every cq_gemm_x3
- * workgroup adds its shader-clock (s_memtime) and 100 MHz (s_memrealtime) tick counts to a
- * device accumulator; this returns both sums and zeroes them (out[0] / out[1] * 100 MHz is
- * the average shader clock under that load).  No reference counterpart. */
-int cq_x3_clock(unsigned long long* out);
 
 /* out[b] = max |X[b]| (n_per values, fp16 or fp32), NaN sorting above inf. */
 int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out, void* stream);

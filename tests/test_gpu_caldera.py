@@ -137,6 +137,9 @@ def test_cfg2_full_size(api, large):
     ref = large["cfg2_sketch_QLR"]
     rel = np.linalg.norm(sk - ref) / np.linalg.norm(ref)
     assert rel < 1e-4, rel
+    # final integer codes (alg.py:280-283): the reference's, bit for bit or up to near-ties
+    from final_codes import assert_final_codes
+    print("cfg2 final codes vs reference:", assert_final_codes("cfg2", d.Q_idxs, 4096, 4096))
 
 
 def test_stream_split_matches_single_stream():

@@ -328,58 +328,6 @@ def test_jacobi_register_path_accuracy(K, p):
     assert torch.equal(V32.cpu().double(), V)
 
 
-@pytest.mark.parametrize("p", [1, 2, 3, 17, 64, 96, 150, 192])
-@pytest.mark.parametrize("spectrum", ["gram", "flat", "graded"])
-def test_tridiagonal_eigh(K, p, spectrum):
-    """p <= 192 without fp64 vectors (the solver's Rayleigh-Ritz calls): Householder
-    tridiagonalisation + bisection + twisted factorisations (cq_trid.hip).  Eigenvalues to
-    fp64 accuracy against LAPACK; fp32 eigenvectors orthogonal to ~1e-6 with residual ~1e-6
-    ||S|| (bars 1e-5, as the Jacobi's fp32 V); values-only calls return the same eigenvalues."""
-    g = torch.Generator().manual_seed(7 * p + len(spectrum))
-    Bt = 3
-    if spectrum == "gram":
-        X = torch.randn(Bt, 4 * p + 4, p, dtype=torch.float64, generator=g)
-        S = X.transpose(1, 2) @ X
-    else:
-        Q, _ = torch.linalg.qr(torch.randn(Bt, p, p, dtype=torch.float64, generator=g))
-        lam = (torch.linspace(2.0, 1.0, p, dtype=torch.float64) ** 2 if spectrum == "flat"
-               else torch.logspace(0, -8, p, dtype=torch.float64))
-        lam = lam + 1e-3 * torch.rand(Bt, p, dtype=torch.float64, generator=g) * lam  # no exact ties
-        S = (Q * lam.unsqueeze(1)) @ Q.transpose(1, 2)
-        S = 0.5 * (S + S.transpose(1, 2))
-    ev, V32, fallback = K.tridiag_eigh(S.to(DEV))
-    if fallback:  # near-degenerate pair (graded spectrum): the caller's Jacobi path
-        ev, V32, _, _ = K.jacobi_eigh(S.clone().to(DEV))
-    ref = torch.linalg.eigvalsh(S).flip(-1)
-    scale = ref.abs().max(dim=1, keepdim=True).values
-    assert ((ev.cpu() - ref).abs() / scale).max().item() < 1e-13
-    V = V32.cpu().double()
-    assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 1e-5
-    res = S @ V - V * ev.cpu().unsqueeze(1)
-    assert (res.abs().amax(dim=(1, 2)) / scale[:, 0]).max().item() < 1e-5
-    ev2, _, fb2 = K.tridiag_eigh(S.to(DEV), want_vectors=False)
-    assert not fb2  # values-only never leaves the bisection
-    assert ((ev2.cpu() - ref).abs() / scale).max().item() < 1e-13
-
-
-def test_tridiagonal_eigh_degenerate_falls_back(K):
-    """Exactly repeated eigenvalues (twisted-factorisation vectors of a tie are not
-    orthogonal): the tridiagonal path reports the fallback; the Jacobi path's vectors are
-    orthonormal."""
-    p = 96
-    g = torch.Generator().manual_seed(3)
-    Q, _ = torch.linalg.qr(torch.randn(2, p, p, dtype=torch.float64, generator=g))
-    lam = torch.linspace(3.0, 1.0, p, dtype=torch.float64)
-    lam[10:14] = 2.5
-    S = (Q * lam) @ Q.transpose(1, 2)
-    S = 0.5 * (S + S.transpose(1, 2))
-    assert K.tridiag_eigh(S.to(DEV))[2]
-    ev, V32, _, _ = K.jacobi_eigh(S.clone().to(DEV))
-    V = V32.cpu().double()
-    assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 2e-5
-    assert ((S @ V - V * ev.cpu().unsqueeze(1)).abs().max()).item() < 2e-5 * 3.0
-
-
 @pytest.mark.parametrize("p", [256, 384])  # panel 32 / panel 16
 def test_whiten_blocked(K, p):
     torch.manual_seed(10)

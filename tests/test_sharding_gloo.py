@@ -150,3 +150,23 @@ def test_pack_keeps_padded_grid_and_alignment():
     back = S.unpack_results(buf)
     assert back[1].extra == {"n_padded": 8} and torch.equal(back[1].codes, r.codes)
     assert torch.equal(back[1].R, r.R) and back[1].R.data_ptr() % 16 == 0
+
+
+def test_payload_magic_and_version_are_checked():
+    """The payload starts with "CQRS" + a format version: a round-2 payload (bare u64 length,
+    no magic) or a future version is rejected instead of being misparsed."""
+    import struct
+    res = _stub(_items()[:2])
+    buf = S.pack_results(res)
+    assert bytes(buf[:4].numpy().tobytes()) == b"CQRS"
+    old = bytearray(buf.numpy().tobytes())
+    meta_len = struct.unpack("<Q", bytes(old[8:16]))[0]
+    legacy = struct.pack("<Q", meta_len) + bytes(old[16:])   # the round-2 header layout
+    with pytest.raises(ValueError, match="magic"):
+        S.unpack_results(torch.frombuffer(bytearray(legacy), dtype=torch.uint8))
+    future = bytearray(old)
+    future[4:8] = struct.pack("<I", 99)
+    with pytest.raises(ValueError, match="version 99"):
+        S.unpack_results(torch.frombuffer(future, dtype=torch.uint8))
+    with pytest.raises(ValueError):
+        S.unpack_results(torch.zeros(3, dtype=torch.uint8))
