@@ -73,12 +73,23 @@ def assert_codes_within_reference_spread(c, sp, what=""):
     """c: compare() of our codes; sp: the reference's own 4- vs 8-thread record of the matrix
     (tests/golden/ref_spread_cfg2_seeds16.json).  Where the reference reproduces its final
     codes (0 flips between its runs) ours must be bit-exact up to near-ties closer than 1e-4
-    code units; where it does not, every flip of ours must still sit at a near-tie of its
-    final quantise call (< 1e-3 code units, the fixture's band) and there may be no more of
-    them than between the reference's own two runs."""
+    code units.  Where it does not, ours may differ from its 8-thread run by no more flips
+    than its own 4-thread run does, at near-ties of the final quantise call (< 1e-3 code
+    units, the fixture's band), and in no more rows outside that band than its own run has
+    flips outside it."""
     ref_flips = sp.get("final_code_flips_ref4_vs_ref8", 0)
-    assert c["rows_unexplained"] == 0, (what, c, sp)
+    ref_far = ref_flips - sp.get("flips_at_ref8_near_ties", 0)
     if ref_flips == 0:
-        assert c["max_flip_tie_dist"] < 1e-4, (what, c, sp)
+        assert c["rows_unexplained"] == 0 and c["max_flip_tie_dist"] < 1e-4, (what, c, sp)
     else:
+        assert c["rows_unexplained"] <= ref_far, (what, c, sp)
         assert c["flips"] <= ref_flips, (what, c, sp)
+
+
+def frob_bar(tag, c, qlr_norm, ref_spread=0.0):
+    """Bar on the relative Frobenius distance of Q + L R to the reference's run: max(1e-4, the
+    reference's own run-to-run spread on this matrix) plus what the final codes' near-tie
+    flips (c = compare()) account for -- each moves Q by one code step (the final scale) and
+    L R, fitted to W - Q, by at most as much: 2 x scale x flips / ||Q + L R||."""
+    s = float(fixture()[tag + "_Q_scale"])
+    return max(1e-4, ref_spread) + 2.0 * s * c["flips"] / qlr_norm

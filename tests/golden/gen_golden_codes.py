@@ -18,8 +18,8 @@ container, like gen_golden.py.  For every full-size configuration the reference'
 Config 2 is recorded for seeds 0-15 (the bench's timed batch holds seed i at position i),
 with the reference's own 4- vs 8-thread spread per seed (relative Frobenius of Q + L R and
 the number of final-code flips between the two runs).  Config 5 (the chaotic 4-bit LPLR
-path, where two identical reference calls diverge) stores the golden run's complete codes,
-2-bit packed, plus the flips between two more reference runs of the same W.
+path, where two identical reference calls diverge in Q + L R) records the flips of the final
+codes between two more reference runs of the same W (none: the kept iterate's Q is stable).
 
 Usage:  python tests/golden/gen_golden_codes.py [cfg2seeds] [cfg3] [cfg4t] [main] [cfg5]
 Output: tests/golden/final_codes.npz, tests/golden/ref_spread_cfg2_seeds16.json
@@ -90,7 +90,8 @@ def record(o, tag, d, fin, W, el, m, n, bits):
 
 
 def sketch(d, n):
-    return (d.Q.double() + d.L.double() @ d.R.double()).numpy() @ G.sketch_omega(n)
+    """16-column Gaussian sketch of Q + L R, stored in fp32 (the tests compare at >= 1e-5)."""
+    return ((d.Q.double() + d.L.double() @ d.R.double()).numpy() @ G.sketch_omega(n)).astype(np.float32)
 
 
 def gen_cfg2_seeds(alg, CP, o, seeds=range(16)):
@@ -105,7 +106,7 @@ def gen_cfg2_seeds(alg, CP, o, seeds=range(16)):
             sk_old = large[f"{tag}_sketch_QLR"]
             rel_old = float(np.linalg.norm(sketch(d, 4096) - sk_old) / np.linalg.norm(sk_old))
             print(f"{tag}: rerun vs sum_large golden sketch {rel_old:.2e}", flush=True)
-            assert rel_old == 0.0, rel_old
+            assert rel_old < 1e-6, rel_old   # the same run (fp32-stored sketch)
         record(o, tag, d, fin, W, el, 4096, 4096, 2)
         o[tag + "_sketch_QLR"] = sketch(d, 4096)
         o[tag + "_global_scale"] = np.float64(d.global_scale)
@@ -155,12 +156,6 @@ def gen_main(alg, CP, o):
         record(o, tag, d, fin, W, el, m, n, 2)
 
 
-def pack2(codes):
-    """int8 codes in {-1, 0, 1} -> offset-binary 2-bit, 4 per byte, MSB first."""
-    c = (codes.astype(np.int16) + 1).astype(np.uint8).reshape(-1, 4)
-    return (c[:, 0] << 6 | c[:, 1] << 4 | c[:, 2] << 2 | c[:, 3]).astype(np.uint8)
-
-
 def gen_cfg5(alg, CP, o):
     kw = dict(Q_bits=2, L_bits=4, R_bits=4, rank=256, iters=5, lplr_iters=10)
     runs = []
@@ -170,7 +165,6 @@ def gen_cfg5(alg, CP, o):
     torch.set_num_threads(8)
     d, fin, W, el = runs[0]
     record(o, "cfg5r", d, fin, W, el, 4096, 4096, 2)
-    o["cfg5r_codes_packed"] = pack2(d.Q_idxs.numpy().reshape(-1))
     o["cfg5r_sketch_QLR"] = sketch(d, 4096)
     for k, v in d.errors.items():
         o["cfg5r_errors_" + k] = np.array(v, dtype=np.float64)

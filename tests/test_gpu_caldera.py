@@ -69,10 +69,21 @@ def test_cfg1_against_reference(api, cfg1):
                 W.to(DEV), None, device=DEV, use_tqdm=False)
     assert d.global_scale == float(cfg1["global_scale"])
     np.testing.assert_array_equal(d.W.numpy(), cfg1["W_scaled"])
+    # bars: the reference's own spread over 8/4/2/1 threads and a repeat (tests/golden/
+    # ref_spread_small.json: its Q errors and first LR error do not move at all, the later LR
+    # errors of the 2-bit-factor LPLR loop by up to 4.1e-4), x 1.5, floored at 1e-5
+    import json
+    import os
+    from conftest import GOLDEN
+    sp = json.load(open(os.path.join(GOLDEN, "ref_spread_small.json")))["cfg1"]["max_abs_err_diff"]
+    dq = np.abs(np.array(d.errors["Q"]) - cfg1["errors_Q"]).max()
+    dl0 = abs(d.errors["LR"][0] - cfg1["errors_LR"][0])
+    dl = np.abs(np.array(d.errors["LR"]) - cfg1["errors_LR"]).max()
+    print(f"cfg1 vs reference: max |dQ err| {dq:.2e}, |dLR err[0]| {dl0:.2e}, max |dLR err| {dl:.2e} "
+          f"(reference spread Q {sp['Q']:.2e}, LR {sp['LR']:.2e})")
     assert abs(d.errors["Q"][0] - cfg1["errors_Q"][0]) < 1e-6
-    assert abs(d.errors["LR"][0] - cfg1["errors_LR"][0]) < 2e-3  # lplr with 2-bit factors
-    for a, b in zip(d.errors["Q"] + d.errors["LR"], list(cfg1["errors_Q"]) + list(cfg1["errors_LR"])):
-        assert abs(a - b) < 1e-2
+    assert dl0 < 1e-5
+    assert dq <= max(1e-5, 1.5 * sp["Q"]) and dl <= max(1e-5, 1.5 * sp["LR"]), (dq, dl, sp)
 
 
 def test_trace_teacher_forced_steps(trace):
@@ -238,8 +249,18 @@ def test_ragged_shapes_vs_oracle(api, m, n, r, qb, lrb, dtype):
         out = (d.Q.double() + d.L.double() @ d.R.double()).cpu().numpy()
         exp = ref.Q.astype(np.float64) + ref.L.astype(np.float64) @ ref.R.astype(np.float64)
         assert np.linalg.norm(out - exp) / np.linalg.norm(exp) < 1e-4
-    else:  # quantised factors: chaotic code flips, compared loosely
-        np.testing.assert_allclose(d.errors["LR"], ref.errors["LR"], rtol=0, atol=2e-2)
+    else:
+        # quantised factors: the LPLR loop amplifies rounding differences into code flips
+        # (SURVEY.md §7.3-2); bar = 1.5 x the reference's own spread over 8/4/2/1 threads on
+        # this exact input (tests/golden/ref_spread_small.json "ragged4": 3.3e-3 Q, 3.8e-3 LR)
+        import json
+        import os
+        from conftest import GOLDEN
+        sp = json.load(open(os.path.join(GOLDEN, "ref_spread_small.json")))["ragged4"]["max_abs_err_diff"]
+        dl = np.abs(np.array(d.errors["LR"]) - np.array(ref.errors["LR"])).max()
+        dq = np.abs(np.array(d.errors["Q"]) - np.array(ref.errors["Q"])).max()
+        print(f"ragged 4-bit vs oracle: max |dLR err| {dl:.2e}, max |dQ err| {dq:.2e} (reference spread {sp})")
+        assert dl <= 1.5 * sp["LR"] and dq <= 1.5 * max(sp["Q"], sp["LR"]), (dl, dq, sp)
     assert d.Q.shape == (m, n) and d.L.shape == (m, r) and d.R.shape == (r, n)
 
 

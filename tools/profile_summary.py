@@ -45,11 +45,12 @@ def pmc(d):
     rows = list(csv.DictReader(open(f)))
     agg = collections.defaultdict(list)
     for r in rows:
-        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        wg = int(r.get("Grid_Size", 0) or 0) // max(1, int(r.get("Workgroup_Size", 1) or 1))
+        agg[(r["Kernel_Name"], r["Counter_Name"], wg)].append(float(r["Counter_Value"]))
     print(f"# PMC: {f}")
-    print(f"{'counter':>12} {'dispatches':>10} {'avg_KB':>14}  kernel")
-    for (k, c), v in sorted(agg.items(), key=lambda x: -sum(x[1]))[:15]:
-        print(f"{c:>12} {len(v):>10} {sum(v) / len(v):14.1f}  {k[:110]}")
+    print(f"{'counter':>12} {'dispatches':>10} {'avg_KB':>14} {'workgroups':>10}  kernel")
+    for (k, c, wg), v in sorted(agg.items(), key=lambda x: -sum(x[1]))[:20]:
+        print(f"{c:>12} {len(v):>10} {sum(v) / len(v):14.1f} {wg:>10}  {k[:100]}")
 
 
 if __name__ == "__main__":
