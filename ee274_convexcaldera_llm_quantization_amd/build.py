@@ -11,8 +11,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcaldera_hip.so")
-SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_codebook.hip", "cq_calib.hip",
-           "cq_bjacobi.hip"]
+SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_qupdate.hip", "cq_codebook.hip",
+           "cq_calib.hip", "cq_bjacobi.hip"]
+# per-source extra flags: the row-panel Q update keeps its per-element epilogue in scalar fp32
+# (packed fp32 VALU beside MFMAs costs more issue cycles than the scalar pair it replaces)
+EXTRA = {"cq_qupdate.hip": ["-fno-slp-vectorize"]}
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          # bit-exact quantiser: no FMA contraction, IEEE-correct fp32 division/sqrt
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"]
@@ -29,13 +32,13 @@ STAMP = OUT + ".srchash"  # content hash of the sources the .so was built from
 
 
 def _deps():
-    return ([os.path.join(CSRC, s) for s in SOURCES + ["cq_common.h"]]
+    return ([os.path.join(CSRC, s) for s in SOURCES + ["cq_common.h", "cq_x3.h"]]
             + [os.path.join(HERE, "..", "include", "caldera_hip.h")])
 
 
 def source_hash() -> str:
     """SHA-256 over the kernel sources, the public header and the compile flags."""
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256((" ".join(FLAGS) + repr(sorted(EXTRA.items()))).encode())
     for d in _deps():
         if os.path.exists(d):
             with open(d, "rb") as f:
@@ -68,7 +71,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        cmd = [hipcc(), *[f for f in FLAGS if f != "-shared"], "-c", "-o", obj, os.path.join(CSRC, src)]
+        cmd = [hipcc(), *[f for f in FLAGS if f != "-shared"], *EXTRA.get(src, []), "-c", "-o", obj,
+               os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((subprocess.Popen(cmd), src))

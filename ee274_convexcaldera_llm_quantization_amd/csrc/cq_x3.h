@@ -1,0 +1,64 @@
+// Shared definitions of the split-fp16 kernels (cq_x3.hip) and the row-panel fused Q update
+// (cq_qupdate.hip): operand-tile argument blocks and vector types.
+#pragma once
+
+#include "cq_common.h"
+
+namespace cq {
+
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x16v = __attribute__((ext_vector_type(16))) float;
+
+struct X3K {
+    int64_t M, N, K, batch;
+    const _Float16 *Ah, *Al; int64_t lda, sa;
+    const _Float16 *Bh, *Bl; int64_t ldb, sb;
+    const float* inv_scale;       // per batch
+    float* C; int64_t ldc, sc;
+    const float* P; int64_t ldp, sp;    // prev (may alias C)
+    const float* D; int64_t ldd, sd;    // cur
+    const float *alpha_v, *beta_v, *gamma_v;
+    _Float16 *Oh, *Ol; int64_t ldo, so;
+    float out_scale;
+    int* overflow;
+    int tri;  // skip tiles entirely below the diagonal (C symmetric; M == N)
+    int b_blocked;  // B halves in K-blocked layout [K/32][ldb rows][32] (cq_sym_split_f16 blocked)
+    const int* active;  // per batch (NULL = all): inactive entries skip the product, C = D
+    int a_blocked;  // A halves K-blocked [K/32][lda rows][32] (lda = rows)
+    int o_blocked;  // split output halves K-blocked over C's columns: (col/32)*M*32 + row*32 + col%32
+    int64_t tiles_n, tiles_m;
+    int64_t tiles_live;        // sym_out: launched tiles per matrix (on or above the diagonal)
+    int single;                // one product hi x hi (lo halves not read): ~2^-11 relative
+    int sym_out;               // tri Gram: write the blocked split of the symmetric C (mirrored upper)
+    const double* out_bound;   // [batch] bound on max|C|: split scale 2^(14 - e)
+    float* scale_out;          // [batch] that scale
+    float* inv_out;            // [batch] 1 / (scale * out_scale)
+};
+
+using f16x8g = __attribute__((ext_vector_type(8))) _Float16;
+using f32x4v = __attribute__((ext_vector_type(4))) float;
+
+// Fused Q update arguments (maybe_update_Q alg.py:253-283 + quantize_matrix alg.py:245-250)
+struct QUK {
+    X3K x;                       // A = L halves, B = R^T halves, inv_scale, K = r, tiling
+    const void* W; int wf16;     // W (m x n), fp16 or fp32
+    int64_t m, n;
+    uint32_t* absmax;            // [batch] bits, zeroed before pass 0
+    float eps;
+    void* codes;                 // int8 / int16 (m x n), or NULL
+    uint8_t* packed;             // packed bytes (m n bits / 8), or NULL
+    float* scale;                // [batch] out (pass 1)
+    const float* ew;             // error column weights [n] or NULL (= 1)
+    double* part;                // [batch * tiles] error partials
+};
+
+constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
+constexpr int QP_KMAX = 256;              // row-panel Q update: largest r
+
+// Row-panel fused Q update (cq_qupdate.hip): both passes of q_update_p_kernel for K = r <= 256,
+// m % 16 == 0, n % 32 == 0 and 16-byte aligned operands; q.absmax zeroed, q.part sized for
+// the pass-1 panels.  Returns the number of pass-1 panels per matrix (the error partials).
+int64_t qp_launch(QUK& q, int dtype, int bits, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth,
+                  const uint16_t* Rtl, int K, int64_t batch, hipStream_t s);
+
+}  // namespace cq
