@@ -487,17 +487,32 @@ def main():
                            else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")}
     if gprobe:
         # the LR update's MFMA-bound kernel (north_star: "MFMA utilisation on the LR update"):
-        # the split-fp16 Gram G = Y Y^T (gemm_x3v_kernel<false>, sym_out), 3 fp16 MFMA products
-        # over the upper half of the symmetric k x k output; fp32-equivalent flops k^2 n
-        gp = gprobe["gram"]
-        t = gp["avg_ms"] * 1e-3
-        ach = gp["flops_per_launch"] / t / 1e12
-        result["roofline_gram"] = {
-            "bound": "mfma", "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s (fp16 MFMA)",
-            "frac": ach / PEAK_F16_MFMA_TFLOPS, "launches_timed": gp["count"], "avg_launch_ms": gp["avg_ms"],
-            "f16_flops_per_launch": gp["flops_per_launch"], "fp32_equiv_tflops": ach / 3.0,
-            "bytes_per_launch": gp["bytes_per_launch"],
-            "kernel": "gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"}
+        # the split-fp16 Gram (gemm_x3v_kernel<false>, sym_out), 3 fp16 MFMA products over the
+        # upper half of the symmetric k x k output (fp32-equivalent flops k^2 n).  With sparse
+        # 2-bit codes (sgram.py) it runs once per run on W's halves (A = W W^T, kind gram_A) and
+        # every LR step forms G = A - s (P + P^T) from the codes (kind gram_sparse, HBM-bound)
+        kind = "gram" if "gram" in gprobe else "gram_A" if "gram_A" in gprobe else None
+        if kind is not None:
+            gp = gprobe[kind]
+            t = gp["avg_ms"] * 1e-3
+            ach = gp["flops_per_launch"] / t / 1e12
+            result["roofline_gram"] = {
+                "bound": "mfma", "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s (fp16 MFMA)",
+                "frac": ach / PEAK_F16_MFMA_TFLOPS, "launches_timed": gp["count"], "avg_launch_ms": gp["avg_ms"],
+                "f16_flops_per_launch": gp["flops_per_launch"], "fp32_equiv_tflops": ach / 3.0,
+                "bytes_per_launch": gp["bytes_per_launch"],
+                "operand": "Y = (W - Q) diag(ycol) per LR step" if kind == "gram" else
+                           "W diag(ycol), once per decomposition (A of the sparse-code Gram)",
+                "kernel": "gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"}
+        if "gram_sparse" in gprobe:
+            gp = gprobe["gram_sparse"]
+            t = gp["avg_ms"] * 1e-3
+            ach = gp["bytes_per_launch"] / t / 1e9
+            result["roofline_gram_sparse"] = {
+                "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                "launches_timed": gp["count"], "avg_launch_ms": gp["avg_ms"],
+                "bytes_per_launch": gp["bytes_per_launch"],
+                "kernels": "sgram_fill + sgram_spmm + sgram_combine (G = A - s (P + P^T) from the 2-bit codes)"}
     if world > 1:
         result["gather"] = {"collective": "torch.distributed.gather (RCCL) of packed (codes, L, R) to rank 0",
                             "gathered_bytes_per_step": gather_stats["bytes"], "ranks": gather_stats["ranks"],

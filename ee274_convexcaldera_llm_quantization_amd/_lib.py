@@ -116,6 +116,13 @@ _SIGS = {
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "cq_sgram_rows": (c_int, [c_i64]),
+    "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
+                              c_vp]),
+    "cq_sgram_combine": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                 c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_product_error": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
@@ -696,6 +703,48 @@ def absmax(X: torch.Tensor) -> torch.Tensor:
     out = torch.empty(B, dtype=torch.float32, device=X.device)
     _check(load().cq_absmax(dt, _p(X), X.numel() // B, B, _p(out), _stream(X.device)), "cq_absmax")
     return out
+
+
+def sgram_count(packed, k, L, row_nnz, perm, slice_off, total):
+    """Sliced-ELL layout of the nonzero 2-bit codes per row (cq_sgram_count): packed (B, k*L/4)."""
+    _require_hip(packed, row_nnz, perm, slice_off, total)
+    B = total.numel()
+    assert row_nnz.numel() >= B * k and perm.numel() >= B * k and slice_off.numel() >= B * (-(-k // 64) + 1)
+    _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total),
+                                 _stream(packed.device)), "cq_sgram_count")
+
+
+def sgram_fill(packed, k, L, perm, slice_off, ell, stride):
+    _require_hip(packed, perm, slice_off, ell)
+    B = slice_off.numel() // (-(-k // 64) + 1)
+    assert ell.numel() >= B * stride
+    _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(perm), _p(slice_off), stride, _p(ell),
+                                _stream(packed.device)), "cq_sgram_fill")
+
+
+def sgram_rows(L: int) -> int:
+    return int(load().cq_sgram_rows(L))
+
+
+def sgram_spmm(W, packed, qscale, wcol, ell, perm, slice_off, stride, P):
+    """P (B, k, k) = (W - (s/2) c) diag(wcol) c^T over the ELL codes (cq_sgram_spmm); wcol = the Gram's
+    column weights w = ycol^2 (None: 1)."""
+    _require_hip(W, packed, qscale, wcol, ell, perm, slice_off, P)
+    B, k, L = W.shape
+    assert W.dtype == torch.float16 and W.is_contiguous() and P.shape == (B, k, k) and P.is_contiguous()
+    assert wcol is None or (wcol.numel() == L and wcol.dtype == torch.float32)
+    _check(load().cq_sgram_spmm(CQ_F16, _p(W), _p(packed), _p(qscale), _p(wcol), B, k, L, _p(ell), _p(perm),
+                                _p(slice_off), stride, _p(P), _stream(W.device)), "cq_sgram_spmm")
+
+
+def sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, scale_out, inv_out, G32=None):
+    """G = A - s (P + P^T) -> K-blocked split halves (cq_sgram_combine)."""
+    _require_hip(A, P, qscale, bound, Gh, Gl, scale_out, inv_out, G32)
+    B, k, _ = P.shape
+    assert A.shape == P.shape and Gh.numel() >= B * k * k and Gl.numel() >= B * k * k
+    assert G32 is None or G32.shape == (B, k, k)
+    _check(load().cq_sgram_combine(_p(A), _p(P), _p(qscale), B, k, _p(bound), float(out_scale), _p(Gh), _p(Gl),
+                                   _p(scale_out), _p(inv_out), _p(G32), _stream(P.device)), "cq_sgram_combine")
 
 
 def residual_split(Ws, packed, qscale, bits, wmax, *, ycol=None, ycol_max=1.0, res=None, Y=None, hi=None, lo=None,

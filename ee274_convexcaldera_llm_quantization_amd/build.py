@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcaldera_hip.so")
 SOURCES = ["cq_quant.hip", "cq_gemm.hip", "cq_small.hip", "cq_x3.hip", "cq_qupdate.hip", "cq_codebook.hip",
-           "cq_calib.hip", "cq_bjacobi.hip"]
+           "cq_calib.hip", "cq_bjacobi.hip", "cq_sgram.hip"]
 # per-source extra flags: the row-panel Q update keeps its per-element epilogue in scalar fp32
 # (packed fp32 VALU beside MFMAs costs more issue cycles than the scalar pair it replaces)
 EXTRA = {"cq_qupdate.hip": ["-fno-slp-vectorize"]}

@@ -1,0 +1,448 @@
+// The solver's Gram G = Y Y^T from the sparse 2-bit codes (the LR step's SVD operand,
+// alg.py:211-217, Y = (W - Q) diag(ycol), m <= n).
+//
+// With 2-bit whole-matrix absmax codes (quantization.py:93-105, k = 1) Q = s c, c in {-1, 0, 1},
+// and |c| = 1 only where |x| > s / 2: ~1 % of the codes.  With w = ycol^2 and E = W - (s/2) c:
+//   G = W diag(w) W^T - s (P + P^T),   P = E diag(w) c^T        (k x k, k = m, contraction n)
+// because E c^T + c E^T = W c^T + c W^T - s c c^T.  A = W diag(w) W^T does not depend on Q: the
+// engine forms it once per run (cq_gemm_x3 Gram of W's halves, fp32 upper triangle).  Each LR
+// step then only needs the sparse product P (~1 % of a dense product's work) and one elementwise
+// pass that writes G's K-blocked split halves (the operand layout of the Chebyshev filter,
+// identical to cq_gemm_x3's sym_out output):
+//   sgram_count_kernel   nonzero codes per row of c;
+//   sgram_slices_kernel  rows sorted by count, per 64-row slice the widest -> sliced-ELL offsets;
+//   sgram_fill_kernel    the ELL entries (l << 2 | code + 1), per row in increasing l;
+//                        (a slice holds 64 rows of similar count: padding ~ a few %)
+//   sgram_spmm_kernel    P[i, j] = sum_{l in row j of c} c_jl (E_il w_l): a workgroup stages R
+//                        rows of E (fp32, l-major, R values per l) in LDS and sweeps every row j
+//                        of c with one lane per j (64 rows per wave, coalesced ELL reads);
+//   sgram_combine_kernel G = A - s (P + P^T) per 64 x 64 tile pair (I <= J), P^T through LDS,
+//                        split halves written at (i, j) and mirrored (j, i).
+// Every sum runs in a fixed order (per row j in increasing l): results are deterministic.
+#include "cq_common.h"
+
+namespace cq {
+
+constexpr int SG_SLICE = 64;
+
+// nonzero 2-bit offset-binary fields (code != 0 <=> field != 1) in a 32-bit word of 16 codes
+__device__ __forceinline__ uint32_t sg_nz_mask(uint32_t word) {
+    const uint32_t x = word ^ 0x55555555u;
+    return (x | (x >> 1)) & 0x55555555u;
+}
+
+// code u (0..15) of a little-endian word: byte u / 4, MSB-first within the byte
+__device__ __forceinline__ uint32_t sg_field(uint32_t word, int u) {
+    return (word >> (8 * (u >> 2) + 6 - 2 * (u & 3))) & 3u;
+}
+
+__global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
+                                                          int32_t* __restrict__ row_nnz) {
+    const int lane = threadIdx.x & 63;
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t b = blockIdx.y;
+    if (j >= k) return;
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
+    const int64_t nw = L / 16;
+    uint32_t cnt = 0;
+    for (int64_t w = lane; w < nw; w += 64) cnt += __popc(sg_nz_mask(row[w]));
+    cnt = wave_sum(cnt);
+    if (lane == 0) row_nnz[b * k + j] = (int32_t)cnt;
+}
+
+// one workgroup per matrix: the rows sorted by nonzero count (descending; ties in row order --
+// a deterministic counting sort), so a 64-row slice's width (its widest row) wastes little
+// padding; perm[b, p] = the row at sorted position p; slice widths and their exclusive prefix
+// (in 64-entry rows): slice_off has ns + 1 entries per matrix, total[b] = entries of matrix b
+constexpr int SG_BINS = 1024;
+
+__global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __restrict__ row_nnz, int64_t k,
+                                                           int32_t* __restrict__ perm, int64_t* __restrict__ slice_off,
+                                                           int64_t* __restrict__ total) {
+    __shared__ int32_t hist[SG_BINS];
+    const int64_t b = blockIdx.x;
+    const int32_t* nz = row_nnz + b * k;
+    int32_t* pm = perm + b * k;
+    for (int v = threadIdx.x; v < SG_BINS; v += blockDim.x) hist[v] = 0;
+    __syncthreads();
+    for (int64_t j = threadIdx.x; j < k; j += blockDim.x) atomicAdd(&hist[min(nz[j], SG_BINS - 1)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t acc = 0;  // descending: bin v starts after every row with a larger count
+        for (int v = SG_BINS - 1; v >= 0; --v) {
+            const int32_t c = hist[v];
+            hist[v] = acc;
+            acc += c;
+        }
+        for (int64_t j = 0; j < k; ++j) pm[hist[min(nz[j], SG_BINS - 1)]++] = (int32_t)j;
+    }
+    __syncthreads();
+    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
+    int64_t* so = slice_off + b * (ns + 1);
+    for (int64_t s = threadIdx.x; s < ns; s += blockDim.x) {
+        int32_t w = 0;
+        for (int64_t p = s * SG_SLICE; p < (s + 1) * SG_SLICE && p < k; ++p) w = max(w, nz[pm[p]]);
+        so[s + 1] = w;  // widths, prefixed below
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t acc = 0;
+        so[0] = 0;
+        for (int64_t s = 1; s <= ns; ++s) {
+            acc += so[s];
+            so[s] = acc;
+        }
+        total[b] = acc * SG_SLICE;
+    }
+}
+
+__global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int64_t* __restrict__ slice_off, int64_t stride_ell,
+                                                         uint32_t* __restrict__ ell) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // sorted position
+    const int64_t b = blockIdx.y;
+    if (p >= k) return;
+    const int64_t j = perm[b * k + p];
+    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
+    const int64_t s = p / SG_SLICE;
+    const int64_t off = slice_off[b * (ns + 1) + s], width = slice_off[b * (ns + 1) + s + 1] - off;
+    uint32_t* out = ell + b * stride_ell + off * SG_SLICE + (p % SG_SLICE);
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
+    const int64_t nw = L / 16;
+    int64_t base = 0;
+    for (int64_t w0 = 0; w0 < nw; w0 += 64) {
+        const int64_t w = w0 + lane;
+        const uint32_t word = w < nw ? row[w] : 0x55555555u;
+        const uint32_t msk = sg_nz_mask(word);
+        const uint32_t cnt = __popc(msk);
+        uint32_t incl = cnt;  // inclusive scan over the lanes: the row's entries in increasing l
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        int64_t pos = base + incl - cnt;
+        if (msk) {
+            for (int u = 0; u < 16; ++u) {
+                const uint32_t f = sg_field(word, u);
+                if (f != 1u) {
+                    out[pos * SG_SLICE] = (uint32_t)((16 * w + u) << 2) | f;
+                    ++pos;
+                }
+            }
+        }
+        base += __shfl(incl, 63, 64);
+    }
+    for (int64_t t = base + 0; t < width; ++t) out[t * SG_SLICE] = 1u;  // padding: l = 0, code 0
+}
+
+// one 64-row slice of the sorted ELL for the R staged rows: acc[r] = P[i0 + r, perm[64 s + lane]].
+// The ELL loads (L2) are software-pipelined SG_PF entries ahead of the LDS reads and FMAs.
+constexpr int SG_PF = 6;
+constexpr int SG_WAVES = 16, SG_THREADS = 64 * SG_WAVES;
+
+template <int R>
+__device__ __forceinline__ void sg_slice(const float* __restrict__ slab, const uint32_t* __restrict__ ep, int64_t width,
+                                         float (&acc)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    auto fma_entry = [&](uint32_t e) {
+        const float c = (float)((int)(e & 3u) - 1);
+        const float* v = slab + (e >> 2) * R;
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = __builtin_fmaf(c, v[r], acc[r]);
+    };
+    int64_t t = 0;
+    if (width >= SG_PF) {
+        uint32_t cur[SG_PF];
+#pragma unroll
+        for (int q = 0; q < SG_PF; ++q) cur[q] = ep[q * SG_SLICE];
+        for (t = SG_PF; t + SG_PF <= width; t += SG_PF) {
+            uint32_t nxt[SG_PF];
+#pragma unroll
+            for (int q = 0; q < SG_PF; ++q) nxt[q] = ep[(t + q) * SG_SLICE];
+#pragma unroll
+            for (int q = 0; q < SG_PF; ++q) fma_entry(cur[q]);
+#pragma unroll
+            for (int q = 0; q < SG_PF; ++q) cur[q] = nxt[q];
+        }
+#pragma unroll
+        for (int q = 0; q < SG_PF; ++q) fma_entry(cur[q]);
+    }
+    for (; t < width; ++t) fma_entry(ep[t * SG_SLICE]);
+}
+
+// P[b, i0 + r, j] for r < R and every row j of c.  LDS: E rows i0 .. i0 + R - 1 as
+// slab[l * R + r] (fp32), E_il = (W_il - (s/2) c_il) * w_l.  Wave wv takes the slices wv,
+// wv + 16, ...; with NSW > 0 (ceil(ns / 16) <= NSW) it keeps all of its results in registers and
+// the R output rows are assembled in LDS (the slab's space, k <= L) and stored row by row --
+// the sorted slices' rows are scattered over j, so direct stores would be 4-byte scatters
+template <int R, int NSW>
+__global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __restrict__ W, const uint8_t* __restrict__ packed,
+                                                         const float* __restrict__ qscale, const float* __restrict__ wcol,
+                                                         int64_t k, int64_t L, const uint32_t* __restrict__ ell,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int64_t* __restrict__ slice_off, int64_t stride_ell,
+                                                         float* __restrict__ P) {
+    extern __shared__ __attribute__((aligned(16))) float slab[];
+    const int64_t b = blockIdx.y;
+    const int64_t i0 = (int64_t)blockIdx.x * R;
+    const float hs = 0.5f * qscale[b];
+    const int64_t KL = k * L;
+    // stage: 8 consecutive l per thread and row
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = i0 + r;
+        for (int64_t l0 = (int64_t)threadIdx.x * 8; l0 < L; l0 += SG_THREADS * 8) {
+            float e[8];
+            if (i < k) {
+                const uint4 raw = *reinterpret_cast<const uint4*>(W + b * KL + i * L + l0);
+                const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
+                const uint16_t two = *reinterpret_cast<const uint16_t*>(packed + (b * KL + i * L + l0) / 4);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t byte = (u < 4) ? (two & 0xffu) : (two >> 8);
+                    const float c = (float)((int)((byte >> (6 - 2 * (u & 3))) & 3u) - 1);
+                    e[u] = (float)hv[u] - hs * c;
+                    if (wcol) e[u] *= wcol[l0 + u];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) e[u] = 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) slab[(l0 + u) * R + r] = e[u];
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
+    const int64_t* so = slice_off + b * (ns + 1);
+    const uint32_t* eb = ell + b * stride_ell + lane;
+    const int32_t* pm = perm + b * k;
+    float* Pb = P + b * k * k;
+    if constexpr (NSW > 0) {
+        float acc[NSW][R];
+#pragma unroll
+        for (int q = 0; q < NSW; ++q) {
+            const int64_t s = wv + SG_WAVES * q;
+            if (s < ns) sg_slice<R>(slab, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc[q]);
+        }
+        __syncthreads();  // every wave is done with the slab: it becomes the R x k output rows
+#pragma unroll
+        for (int q = 0; q < NSW; ++q) {
+            const int64_t p = (wv + SG_WAVES * q) * SG_SLICE + lane;
+            if (p < k) {
+                const int64_t j = pm[p];
+#pragma unroll
+                for (int r = 0; r < R; ++r) slab[r * k + j] = acc[q][r];
+            }
+        }
+        __syncthreads();
+        for (int r = 0; r < R; ++r) {
+            if (i0 + r >= k) break;
+            for (int64_t j = (int64_t)threadIdx.x * 4; j < k; j += SG_THREADS * 4)
+                *reinterpret_cast<float4*>(Pb + (i0 + r) * k + j) = *reinterpret_cast<const float4*>(slab + r * k + j);
+        }
+    } else {
+        for (int64_t s = wv; s < ns; s += SG_WAVES) {
+            float acc[R];
+            sg_slice<R>(slab, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc);
+            const int64_t p = s * SG_SLICE + lane;
+            if (p < k) {
+                const int64_t j = pm[p];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (i0 + r < k) Pb[(i0 + r) * k + j] = acc[r];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ float sg_split_scale(double bound) {
+    int e = 0;
+    if (bound > 0.0 && isfinite(bound)) frexp(bound, &e);
+    return ldexpf(1.f, 14 - e);
+}
+
+// G = A - s (P + P^T) for the 64 x 64 tile pair (I, J), I <= J: halves at (i, j) and (j, i)
+// of the K-blocked split (element (i, j) at (j / 32) k 32 + i 32 + j % 32); fp32 G too if given
+__global__ __launch_bounds__(256) void sgram_combine_kernel(const float* __restrict__ A, const float* __restrict__ P,
+                                                            const float* __restrict__ qscale, int64_t k,
+                                                            const double* __restrict__ bound, float out_scale,
+                                                            _Float16* __restrict__ Gh, _Float16* __restrict__ Gl,
+                                                            float* __restrict__ scale_out, float* __restrict__ inv_out,
+                                                            float* __restrict__ G32) {
+    __shared__ float pt[64][65];  // pt[a][c] = P[J0 + a][I0 + c], then the G tile v[i][j]
+    const int64_t b = blockIdx.y;
+    const int64_t nt = k / 64;
+    int64_t t = blockIdx.x, I = 0;
+    while (t >= nt - I) { t -= nt - I; ++I; }
+    const int64_t J = I + t;
+    const int64_t I0 = I * 64, J0 = J * 64;
+    const float s = qscale[b];
+    const float gs = sg_split_scale(bound[b]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        scale_out[b] = gs;
+        inv_out[b] = 1.f / (gs * out_scale);
+    }
+    const int64_t KK = k * k;
+    const float* Pb = P + b * KK;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 16 threads, 4 columns each
+    for (int a = ty; a < 64; a += 16) {
+        const float4 v = *reinterpret_cast<const float4*>(Pb + (J0 + a) * k + I0 + 4 * tx);
+        pt[a][4 * tx] = v.x; pt[a][4 * tx + 1] = v.y; pt[a][4 * tx + 2] = v.z; pt[a][4 * tx + 3] = v.w;
+    }
+    __syncthreads();
+    float g[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = ty + 16 * q;                 // row i = I0 + a, columns j = J0 + 4 tx .. + 3
+        const float4 av = *reinterpret_cast<const float4*>(A + b * KK + (I0 + a) * k + J0 + 4 * tx);
+        const float4 pv = *reinterpret_cast<const float4*>(Pb + (I0 + a) * k + J0 + 4 * tx);
+        const float aa[4] = {av.x, av.y, av.z, av.w}, pp[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[q][u] = aa[u] - s * (pp[u] + pt[4 * tx + u][a]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pt[ty + 16 * q][4 * tx + u] = g[q][u];
+    __syncthreads();
+    _Float16* Ohb = Gh + b * KK;
+    _Float16* Olb = Gl + b * KK;
+    // (i, j), i <= j: row i = I0 + a, 4 columns j
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = ty + 16 * q;
+        const int64_t i = I0 + a, j = J0 + 4 * tx;
+        _Float16 h[4], l[4];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float hsv = pt[a][4 * tx + u] * gs;
+            h[u] = (_Float16)hsv;
+            l[u] = (_Float16)(hsv - (float)h[u]);
+            any |= j + u >= i;
+        }
+        const int64_t o = (j >> 5) * (k * 32) + i * 32 + (j & 31);
+        if (j >= i) {
+            *reinterpret_cast<uint2*>(Ohb + o) = *reinterpret_cast<const uint2*>(h);
+            *reinterpret_cast<uint2*>(Olb + o) = *reinterpret_cast<const uint2*>(l);
+        } else if (any) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j + u >= i) { Ohb[o + u] = h[u]; Olb[o + u] = l[u]; }
+        }
+        if (G32) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j + u >= i) G32[b * KK + i * k + j + u] = pt[a][4 * tx + u];
+        }
+    }
+    // mirror (j, i), j > i: row j = J0 + a, 4 columns i = I0 + 4 tx .. + 3
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = ty + 16 * q;
+        const int64_t j = J0 + a, i = I0 + 4 * tx;
+        _Float16 h[4], l[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float hsv = pt[4 * tx + u][a] * gs;
+            h[u] = (_Float16)hsv;
+            l[u] = (_Float16)(hsv - (float)h[u]);
+        }
+        const int64_t o = (i >> 5) * (k * 32) + j * 32 + (i & 31);
+        if (i + 3 < j) {
+            *reinterpret_cast<uint2*>(Ohb + o) = *reinterpret_cast<const uint2*>(h);
+            *reinterpret_cast<uint2*>(Olb + o) = *reinterpret_cast<const uint2*>(l);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u < j) { Ohb[o + u] = h[u]; Olb[o + u] = l[u]; }
+        }
+        if (G32) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u < j) G32[b * KK + j * k + i + u] = pt[4 * tx + u][a];
+        }
+    }
+}
+
+}  // namespace cq
+
+using namespace cq;
+
+extern "C" {
+
+int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
+                   int32_t* perm, int64_t* slice_off, int64_t* total, void* stream) {
+    CQ_REQUIRE(packed && row_nnz && perm && slice_off && total, "cq_sgram_count: null argument");
+    CQ_REQUIRE(bits == 2, "cq_sgram_count: 2-bit codes only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0, "cq_sgram_count: bad shape");
+    hipStream_t s = as_stream(stream);
+    sgram_count_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, s>>>(packed, k, L, row_nnz);
+    sgram_slices_kernel<<<(unsigned)batch, 256, 0, s>>>(row_nnz, k, perm, slice_off, total);
+    return check_launch("cq_sgram_count");
+}
+
+int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* perm,
+                  const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream) {
+    CQ_REQUIRE(packed && perm && slice_off && ell, "cq_sgram_fill: null argument");
+    CQ_REQUIRE(bits == 2, "cq_sgram_fill: 2-bit codes only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0 && L < (1ll << 29),
+               "cq_sgram_fill: bad shape");
+    sgram_fill_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, as_stream(stream)>>>(
+        packed, k, L, perm, slice_off, stride_ell, ell);
+    return check_launch("cq_sgram_fill");
+}
+
+int cq_sgram_rows(int64_t L) {
+    for (int r : {8, 4, 2})
+        if ((size_t)L * r * sizeof(float) <= 150 * 1024) return r;
+    return 0;
+}
+
+int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
+                  int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
+                  const int64_t* slice_off, int64_t stride_ell, float* P, void* stream) {
+    CQ_REQUIRE(W && packed && qscale && ell && perm && slice_off && P, "cq_sgram_spmm: null argument");
+    CQ_REQUIRE(dtype == CQ_F16, "cq_sgram_spmm: fp16 W only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L % 64 == 0, "cq_sgram_spmm: bad shape");
+    const int R = cq_sgram_rows(L);
+    CQ_REQUIRE(R > 0, "cq_sgram_spmm: rows of %lld values do not fit the LDS", (long long)L);
+    const size_t lds = (size_t)L * R * sizeof(float);
+    hipStream_t s = as_stream(stream);
+    const dim3 grid((unsigned)ceil_div(k, R), (unsigned)batch);
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
+    const int64_t nsw = ceil_div(ceil_div(k, SG_SLICE), SG_WAVES);  // slices per wave
+    // the register-held form needs k % 4 == 0 (float4 row stores) and k <= L (LDS reuse)
+    const bool held = k % 4 == 0 && k <= L && nsw * R <= 32;
+#define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
+                                                                             perm, slice_off, stride_ell, P)
+    if (R == 8) {
+        if (held) CQ_SP(8, 4); else CQ_SP(8, 0);
+    } else if (R == 4) {
+        if (held) CQ_SP(4, 8); else CQ_SP(4, 0);
+    } else {
+        if (held) CQ_SP(2, 16); else CQ_SP(2, 0);
+    }
+#undef CQ_SP
+    return check_launch("cq_sgram_spmm");
+}
+
+int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_t batch, int64_t k,
+                     const double* bound, float out_scale, uint16_t* Gh, uint16_t* Gl, float* scale_out,
+                     float* inv_out, float* G32, void* stream) {
+    CQ_REQUIRE(A && P && qscale && bound && Gh && Gl && scale_out && inv_out, "cq_sgram_combine: null argument");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && k % 64 == 0 && out_scale > 0.f, "cq_sgram_combine: bad shape");
+    const int64_t nt = k / 64;
+    sgram_combine_kernel<<<dim3((unsigned)(nt * (nt + 1) / 2), (unsigned)batch), 256, 0, as_stream(stream)>>>(
+        A, P, qscale, k, bound, out_scale, reinterpret_cast<_Float16*>(Gh), reinterpret_cast<_Float16*>(Gl),
+        scale_out, inv_out, G32);
+    return check_launch("cq_sgram_combine");
+}
+
+}  // extern "C"

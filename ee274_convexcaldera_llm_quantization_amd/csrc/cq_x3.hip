@@ -317,29 +317,58 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
     }
 }
 
+// Gram tile order.  Only the tiles on or above the diagonal are launched: 384 x 384 blocks
+// (I, J >= I) of tiles tm = 2I, 2I + 1 (192 rows) by tn = J.  The blocks are enumerated per
+// matrix in 4 x 4 super-blocks (row-major over super-blocks, then over their blocks), and
+// the launch index is dealt to the XCDs (workgroup i runs on XCD i % 8) in runs of
+// GRAM_RUN consecutive tiles of that order: the 32 tiles an XCD holds at a time share 8 row
+// and 4 column panels of Y instead of ~30 of each, so their K slices are re-read from the
+// XCD's L2 rather than from the memory-side cache, and all XCDs stay on the same one or two
+// matrices (whose operands fit that 256 MB cache).  The order changes nothing in a tile's
+// arithmetic.
+constexpr int GRAM_SB = 4, GRAM_RUN = 32;
+
+__device__ __forceinline__ int64_t gram_block_tiles(int64_t I, int64_t tiles_m) {
+    return 2 * I + 1 < tiles_m ? 2 : 1;
+}
+
+__device__ void gram_tile(const X3K& a, int64_t orig, int64_t& b, int64_t& tm, int64_t& tn) {
+    const int64_t live = a.tiles_live, total = live * a.batch;
+    constexpr int64_t S = 8 * GRAM_RUN;
+    int64_t lin = orig;
+    if (orig < total / S * S) {
+        const int64_t k = orig / 8, x = orig % 8;
+        lin = (k / GRAM_RUN) * S + x * GRAM_RUN + k % GRAM_RUN;
+    }
+    b = lin / live;
+    int64_t j = lin % live;
+    const int64_t nb = a.tiles_n, nsb = (nb + GRAM_SB - 1) / GRAM_SB;
+    for (int64_t si = 0; si < nsb; ++si) {
+        for (int64_t sj = si; sj < nsb; ++sj) {
+            const int64_t i1 = min<int64_t>(GRAM_SB * si + GRAM_SB, nb), j1 = min<int64_t>(GRAM_SB * sj + GRAM_SB, nb);
+            for (int64_t I = GRAM_SB * si; I < i1; ++I) {
+                const int64_t per = gram_block_tiles(I, a.tiles_m);
+                const int64_t jb = max<int64_t>(GRAM_SB * sj, I);
+                const int64_t cnt = (j1 > jb ? j1 - jb : 0) * per;
+                if (j < cnt) {
+                    tn = jb + j / per;
+                    tm = 2 * I + j % per;
+                    return;
+                }
+                j -= cnt;
+            }
+        }
+    }
+    tm = tn = 0;  // unreachable for lin < total
+}
+
 template <bool X1>
 __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     extern __shared__ __attribute__((aligned(16))) char xv_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(xv_smem_raw);
     int64_t tn, tm, b;
     if (a.sym_out) {
-        // Gram: only the tiles on or above the diagonal are launched (tn >= tm / 2 with the
-        // 192 x 384 tile), in plain launch order, so the tiles of one or two matrices run on
-        // all XCDs at once: their re-reads of the Gram operand (64 MB of halves per 4096^2
-        // matrix) stay inside the shared 256 MB memory-side cache instead of the eight
-        // matrices the XCD-blocked order keeps in flight (measured: 2 x FETCH_SIZE of 217 GB
-        // per B = 256 Gram against 17 GB of operand, 47 ms)
-        const int64_t live = a.tiles_live;
-        b = (int64_t)blockIdx.x / live;
-        int64_t j = (int64_t)blockIdx.x % live;
-        tm = 0;
-        for (;;) {
-            const int64_t row = a.tiles_n - (tm >> 1);
-            if (j < row) break;
-            j -= row;
-            ++tm;
-        }
-        tn = (tm >> 1) + j;
+        gram_tile(a, blockIdx.x, b, tm, tn);
     } else {
         const int64_t total = a.tiles_n * a.tiles_m * a.batch;
         const int64_t orig = blockIdx.x;
@@ -1472,7 +1501,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && (!g->out_h || g->sym_out)),
                "cq_gemm_x3: tri needs a square plain product");
     a.single = g->single;
-    CQ_REQUIRE(!g->single || !g->sym_out, "cq_gemm_x3: single-product mode is for the filter");
+    // single + sym_out: the Gram of an exactly-fp16 operand (lo = 0; A = W W^T of the sparse-code
+    // Gram, sgram.py): the split products add exact zeros, so one product gives the same bits
     a.sym_out = g->sym_out;
     a.out_bound = g->out_bound;
     a.scale_out = g->scale_out;

@@ -27,7 +27,8 @@ from . import _lib as K
 from . import qlog
 from .overlap import run_to_end
 from . import scratch
-from .solver import LPLR_PROBE, QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
+from . import sgram
+from .solver import GRAM_PROBE, LPLR_PROBE, QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
 
 
 @dataclass
@@ -244,6 +245,7 @@ class CalderaEngine:
         self.solver = None
         self.lplr_fused_err = True   # LPLR error from the normal-equation pieces (False: error GEMM)
         self.lplr_x3 = True          # LPLR m x n x r products on split-fp16 MFMAs where the halves exist
+        self.sparse_gram = True      # G from the sparse 2-bit codes where it applies (sgram.py)
         self.lplr_trace = None       # list -> per-LPLR-iteration errors are appended (diagnostics)
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
@@ -362,6 +364,7 @@ class CalderaEngine:
                 self.solver.valid_k = self._n_true
         sv = self.solver
         y_split = None
+        gram = None
         ysq = None
         lplr_halves = None
         if st.dense_q and st.has_Q:
@@ -385,11 +388,30 @@ class CalderaEngine:
                 self._yl = scratch.get("lr.yl", gshape, torch.float16, dev)
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
-            halves = dict(hi=self._yh, lo=self._yl) if sv.left else dict(thi=self._yh, tlo=self._yl)
             x3_r = sv.left and not quantized and p.activation_aware_LR
             # quantised factors with unweighted Y (= res): the LPLR loop's m x n x r products run
             # on split-fp16 MFMAs from these halves (Y for Y R^T, res^T = Y^T for L^T res)
             x3_lplr = sv.left and quantized and not weighted and self.lplr_x3
+            # sparse 2-bit codes: G = A - s (P + P^T) (sgram.py) instead of the dense Gram of
+            # Y's halves, which are then only written where another product reads them
+            sparse_g = (self.sparse_gram and sv.left and st.has_Q and st.q_packed and not st.dense_q
+                        and sgram.applicable(m, n, Ws, p.Q_bits, True, wts.dense))
+            if sparse_g and self._sg_A is None:  # once per run: A = W diag(w) W^T
+                self._sg_A = scratch.get("sgram.A", (B, m, m), torch.float32, dev)
+                self._sg = sgram.SparseGram(B, m, n, dev)
+                self._sg_w = (wts.ycol * wts.ycol).contiguous() if weighted else None
+                sv._alloc(dev)
+                gev = GRAM_PROBE.start("gram_A", 3.0 * m * m * n * B, 4.0 * m * n * B + 4.0 * m * m * B)
+                if gev is not None:
+                    gev[0].record()
+                sgram.gram_A(Ws, wts.ycol if weighted else None, wts.ycol_max if weighted else 1.0, self._wmax,
+                             self._sg_A, sv._Gh, sv._Gl, X3_SCALE, self._yh, self._yl)
+                if gev is not None:
+                    gev[1].record()
+            if sparse_g and self._sg.count(st.Qc) > sgram.MAX_DENSITY * m * n:
+                sparse_g = False  # too many nonzero codes this step: dense Gram
+            halves = ({} if sparse_g and not x3_lplr else dict(hi=self._yh, lo=self._yl)) if sv.left else \
+                dict(thi=self._yh, tlo=self._yl)
             if x3_r or x3_lplr:
                 if self._yth is None:
                     self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
@@ -406,14 +428,22 @@ class CalderaEngine:
                              ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
                              res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
                              scale=self._ys, sq=ysq, **halves)
-            y_split = (self._yh, self._yl, self._ys, ysq)
+            if sparse_g:
+                qc, qs, A, SG, w = st.Qc, st.Qs, self._sg_A, self._sg, self._sg_w
+
+                def fill(Gh, Gl, gscale, ginv, G32=None):
+                    SG.gram(Ws, qc, qs, w, A, ysq, Gh, Gl, gscale, ginv, X3_SCALE, G32=G32, counted=True)
+
+                gram = dict(fill=fill, ysq=ysq)
+            else:
+                y_split = (self._yh, self._yl, self._ys, ysq)
             if x3_lplr:
                 lplr_halves = dict(yh=self._yh, yl=self._yl, ys=self._ys, yth=self._yth, ytl=self._ytl)
         else:
             K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
         Y = Ysrc
-        vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split)
+        vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split, gram=gram)
         rand = isinstance(sv, RandSVD)
         r = sv.r
         S = torch.sqrt(theta.clamp_min(0.0))  # singular values (fp64)
@@ -777,6 +807,7 @@ class CalderaEngine:
         wts = _Weights(h, n, p, dev)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
         self._w_finite = None
+        self._sg_A = self._sg = self._sg_w = None  # sparse-code Gram (sgram.py): A per run
         self._yh = self._yl = self._ys = None
         self._yth = self._ytl = None
         self._yrh = self._yrl = None

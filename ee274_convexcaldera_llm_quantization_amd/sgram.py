@@ -1,0 +1,90 @@
+"""The LR step's Gram G = Y Y^T from the sparse 2-bit Q codes (csrc/cq_sgram.hip).
+
+Y = (W - Q) diag(ycol) is the operand the reference's SVD factors (alg.py:211-217).  With
+2-bit whole-matrix absmax codes (quantization.py:93-105: k = 1, Q = s c, c in {-1, 0, 1}) only
+the elements with |x| > s/2 carry a nonzero code -- about 1 % at the bench's configuration --
+so with w = ycol^2 and E = W - (s/2) c
+
+    G = A - s (P + P^T),    A = W diag(w) W^T,    P = E diag(w) c^T.
+
+A does not depend on Q: it is one split-fp16 Gram of W's halves per run (`gram_A`).  Every LR
+step then costs the sparse product P and one elementwise pass instead of a dense Gram
+(`sparse_gram`).  Scope: m <= n (G is m x m, the contraction runs over the n columns), fp16 W,
+2-bit packed codes, diagonal or no H; anything else keeps the dense Gram."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as K
+from . import scratch
+
+# above this fraction of nonzero codes (padded sliced-ELL entries / (m n)) the dense Gram is
+# cheaper (the sparse product's cost grows with the entries, the dense Gram's does not)
+MAX_DENSITY = 0.03
+
+
+def applicable(m: int, n: int, W: torch.Tensor, q_bits: int, packed: bool, dense_h: bool) -> bool:
+    return (m <= n and m % 64 == 0 and n % 64 == 0 and W.dtype == torch.float16 and q_bits == 2 and packed
+            and not dense_h and K.sgram_rows(n) > 0)
+
+
+def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch.Tensor, Gh, Gl, out_scale: float,
+           yh: torch.Tensor, yl: torch.Tensor):
+    """A (B, m, m) fp32 upper triangle = (W diag(ycol)) (W diag(ycol))^T on split-fp16 products
+    (cq_gemm_x3 Gram of W's K-blocked halves, written into yh/yl (B, m, n); H = I makes them
+    exact, lo = 0).  Gh/Gl receive a split of A that the caller overwrites later."""
+    B, m, n = Ws.shape
+    dev = Ws.device
+    ys = torch.empty(B, dtype=torch.float32, device=dev)
+    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=yl, scale=ys)
+    bound = torch.full((B,), 2.0 ** 60, dtype=torch.float64, device=dev)  # any bound >= max|A|: halves unused
+    so = torch.empty(B, dtype=torch.float32, device=dev)
+    io = torch.empty(B, dtype=torch.float32, device=dev)
+    # H = I: W's halves are W itself (fp16) and zeros -- one fp16 product gives the same bits
+    K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), A, tri=True, a_blocked=True, b_blocked=True, out_h=Gh, out_l=Gl,
+              out_scale=out_scale, sym_bound=bound, scale_out=so, inv_out=io, single=ycol is None)
+
+
+class SparseGram:
+    """Per-batch workspace of the sparse Gram (row counts, ELL, P)."""
+
+    def __init__(self, B: int, m: int, n: int, dev):
+        self.B, self.m, self.n = B, m, n
+        self.ns = -(-m // 64)
+        self.row_nnz = torch.empty(B * m, dtype=torch.int32, device=dev)
+        self.perm = torch.empty(B * m, dtype=torch.int32, device=dev)
+        self.slice_off = torch.empty(B * (self.ns + 1), dtype=torch.int64, device=dev)
+        self.total = torch.empty(B, dtype=torch.int64, device=dev)
+        self.density = None
+        self.stats = {"sparse": 0, "dense": 0}
+
+    def count(self, packed: torch.Tensor) -> int:
+        """ELL entries per matrix (max over the batch) -- one host read-back."""
+        K.sgram_count(packed, self.m, self.n, self.row_nnz, self.perm, self.slice_off, self.total)
+        mx = int(self.total.max().item())
+        self.density = mx / float(self.m * self.n)
+        return mx
+
+    def gram(self, Ws, packed, qscale, w, A, bound, Gh, Gl, gscale, ginv, out_scale, G32=None,
+             max_density: float = MAX_DENSITY, counted: bool = False) -> bool:
+        """G's K-blocked split halves (and G32) from the codes; False (nothing written) when the
+        codes are too dense for the sparse product to pay.  counted: count() already ran on
+        these codes (the caller decided on its density)."""
+        B, m, n = self.B, self.m, self.n
+        dev = Ws.device
+        if not counted:
+            self.count(packed)
+        elif self.density is None:
+            raise RuntimeError("SparseGram.gram(counted=True) before count()")
+        if self.density > max_density:
+            self.stats["dense"] += 1
+            return False
+        # fixed capacity per matrix (a stable scratch shape across LR steps)
+        stride = -(-int(max(MAX_DENSITY, self.density) * m * n) // 4096) * 4096
+        ell = scratch.get("sgram.ell", (B * stride,), torch.int32, dev)
+        K.sgram_fill(packed, m, n, self.perm, self.slice_off, ell, stride)
+        P = scratch.get("sgram.P", (B, m, m), torch.float32, dev)
+        K.sgram_spmm(Ws, packed, qscale, w, ell, self.perm, self.slice_off, stride, P)
+        K.sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, gscale, ginv, G32=G32)
+        self.stats["sparse"] += 1
+        return True

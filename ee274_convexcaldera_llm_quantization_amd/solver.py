@@ -272,6 +272,9 @@ class RankRSolver:
     def _fill_G(self, Y):
         """fp32 G = Y Y^T (m <= n) or Y^T Y: from the Gram operand's split halves when the
         caller provided them (Y itself may not exist in fp32), else on the fp32 MFMA GEMM."""
+        if self._gram_fill is not None:  # caller-formed G (sgram.py): its fp32 form
+            self._gram_fill(self._Gh, self._Gl, self._gscale, self._ginv, G32=self._G)
+            return
         if self._y_halves is not None:
             yh, yl, ys = self._y_halves
             K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), self._G, tri=True, a_blocked=True, b_blocked=True)
@@ -424,11 +427,13 @@ class RankRSolver:
         """Y (B, m, n) fp32 -> (vecs (B, k, r), theta (B, r) fp64 eigenvalues of G, descending)."""
         return run_to_end(self.solve_iter(Y, warm))
 
-    def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None):
+    def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None, gram=None):
         """Generator form of solve(): yields before each host synchronisation (overlap.py).
         y_split: optional (hi, lo, scale, sq) K-blocked split-fp16 halves of the Gram operand (Y
         for m <= n, Y^T otherwise) and ||Y||_F^2 (fp64, or None) already produced by the caller
-        (cq_residual_split)."""
+        (cq_residual_split).  gram: optional dict(fill, ysq) -- the caller forms G itself
+        (sgram.py): fill(Gh, Gl, gscale, ginv, G32=None) writes G's K-blocked split halves
+        (and fp32 G when asked), ysq = ||Y||_F^2; Y is then not read."""
         B, k, p = self.B, self.k, self.p
         dev = Y.device
         self.stats.calls += 1
@@ -441,7 +446,22 @@ class RankRSolver:
         self._Y = Y
         self._y_halves = None
         g_split = False
-        if self.x3 and (self.n if self.left else self.m) % 32 == 0:
+        self._gram_fill = None
+        if gram is not None:
+            assert self.x3, "solver: a caller-formed Gram needs the split-fp16 path"
+            self._gram_fill = gram["fill"]
+            self._ysq = gram["ysq"]
+            # algorithmic bytes of the sparse Gram: W and its codes once (E slabs), P written
+            # and read back, A's upper triangle, G's split halves written
+            kk, nn = k, Y.shape[1] + Y.shape[2] - k
+            gev = GRAM_PROBE.start("gram_sparse", 0.0, B * (2.25 * kk * nn + 14.0 * kk * kk))
+            if gev is not None:
+                gev[0].record()
+            self._gram_fill(self._Gh, self._Gl, self._gscale, self._ginv)
+            if gev is not None:
+                gev[1].record()
+            g_split = True
+        elif self.x3 and (self.n if self.left else self.m) % 32 == 0:
             # G = Y Y^T (or Y^T Y) on split-fp16 products, Y scaled per matrix by a power of two;
             # the Gram writes G's K-blocked split halves itself (scale from ||Y||_F^2 >= max|G|)
             ysq = None

@@ -323,6 +323,35 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
                       uint16_t* thi, uint16_t* tlo, float* scale_out, double* sq_out, void* ws,
                       size_t ws_bytes, void* stream);
 
+/* Gram of the LR step's Y from sparse 2-bit codes (cq_sgram.hip).  Replaces, for m <= n,
+ * Q_bits = 2 and a diagonal (or no) H, the Gram Y Y^T of Y = (W - Q) diag(ycol) that the SVD
+ * at alg.py:211-217 factors: with Q = s c (c in {-1, 0, 1}, ~1 % nonzero), w = ycol^2 and
+ * E = W - (s/2) c, G = W diag(w) W^T - s (P + P^T) with P = E diag(w) c^T.
+ *   cq_sgram_count:   row_nnz (batch x k, int32) nonzero codes per row of the packed codes
+ *                     (batch x k x L, offset-binary MSB-first), perm (batch x k, int32: rows
+ *                     sorted by count, descending, ties in row order), slice_off (batch x (ceil(k/64)
+ *                     + 1), int64: sliced-ELL offsets per 64-row slice, in 64-entry rows), total[b] entries;
+ *   cq_sgram_fill:    the ELL entries (uint32: l << 2 | code + 1) of matrix b at ell + b stride_ell;
+ *   cq_sgram_rows:    rows of E a workgroup stages for contraction length L (0: too long);
+ *   cq_sgram_spmm:    P (batch x k x k fp32) from W (fp16, batch x k x L), the codes, qscale[b] = s
+ *                     and wcol (L, may be NULL = 1);
+ *   cq_sgram_combine: G = A - s (P + P^T) with A (batch x k x k fp32, upper triangle read) =
+ *                     W diag(w) W^T, written as the K-blocked split halves Gh/Gl with
+ *                     cq_gemm_x3 sym_out's scale rule (scale_out[b] from bound[b] >= max|G|,
+ *                     inv_out[b] = 1 / (scale_out[b] out_scale)); G32 (full fp32 G) optional.
+ * k % 64 == 0, L % 64 == 0. */
+int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
+                   int32_t* perm, int64_t* slice_off, int64_t* total, void* stream);
+int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* perm,
+                  const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream);
+int cq_sgram_rows(int64_t L);
+int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
+                  int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
+                  const int64_t* slice_off, int64_t stride_ell, float* P, void* stream);
+int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_t batch, int64_t k,
+                     const double* bound, float out_scale, uint16_t* Gh, uint16_t* Gl, float* scale_out,
+                     float* inv_out, float* G32, void* stream);
+
 /* Fused Q update.  Replaces alg.py:253-283 (maybe_update_Q / update_Q_non_data_aware:
  * res = W - L@R, quantize_matrix) + quantization.py:244-269 (whole-matrix uniform quantise):
  * res is recomputed per tile from the split-fp16 halves of L (m x r) and R^T (n x r,

@@ -1,0 +1,92 @@
+"""The sparse-code Gram (csrc/cq_sgram.hip, sgram.py) against fp64: G = Y Y^T for
+Y = (W - Q) diag(ycol), Q = s c the 2-bit whole-matrix codes of the LR step (alg.py:211-217,
+quantization.py:93-105), assembled as A - s (P + P^T) with A = W diag(w) W^T (split-fp16 Gram
+of W) and P = (W - (s/2) c) diag(w) c^T over the sliced-ELL codes.  Checked: the per-row
+nonzero counts (exact), the fp32 G and its K-blocked split halves (fp32-grade against fp64,
+and against the dense split-fp16 Gram of Y that it replaces), for every LDS slab height
+(R = 8 / 4 / 2 rows of E by contraction length) and with and without column weights."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _unblock(h, k):
+    B = h.shape[0]
+    return h.view(B, k // 32, k, 32).permute(0, 2, 1, 3).reshape(B, k, k)
+
+
+@pytest.mark.parametrize("B,m,n,weighted", [(3, 256, 512, False), (2, 512, 512, True), (2, 256, 4608, False),
+                                            (2, 128, 6400, True), (2, 64, 12800, False)])
+def test_sparse_gram_matches_fp64(B, m, n, weighted):
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    from ee274_convexcaldera_llm_quantization_amd import sgram
+    from ee274_convexcaldera_llm_quantization_amd.solver import X3_SCALE
+    g = torch.Generator(device=DEV).manual_seed(m + n + weighted)
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.7).half()
+    ycol = (torch.rand(n, device=DEV, generator=g) + 0.5) if weighted else None
+    w = ycol * ycol if weighted else None
+    q = K.quantize_uniform(W.float().reshape(B, -1), m * n, 2, codes=True, packed=True, deq=False)
+    codes, packed, s = q["codes"].view(B, m, n), q["packed"], q["scale"].view(B)
+    Y = (W.double() - codes.double() * s.double().view(B, 1, 1)) * (ycol.double() if weighted else 1.0)
+    G64 = Y @ Y.transpose(1, 2)
+    ysq = (Y * Y).sum(dim=(1, 2))
+
+    assert sgram.applicable(m, n, W, 2, True, False)
+    SG = sgram.SparseGram(B, m, n, DEV)
+    SG.count(packed)
+    nnz = (codes != 0).sum(dim=2).to(torch.int32).reshape(-1)
+    assert torch.equal(SG.row_nnz, nnz)
+    # rows sorted by count (descending, ties in row order) per matrix
+    perm = SG.perm.view(B, m).long()
+    ref = torch.stack([torch.sort(-nnz.view(B, m)[b].long() * m + torch.arange(m, device=DEV))[1] for b in range(B)])
+    assert torch.equal(perm, ref)
+    print(f"density (padded ELL) {SG.density:.4f}, nonzero codes {float((codes != 0).float().mean()):.4f}")
+
+    wmax = K.absmax(W)
+    A = torch.empty(B, m, m, device=DEV)
+    Gh = torch.empty(B, m, m, device=DEV, dtype=torch.float16)
+    Gl = torch.empty_like(Gh)
+    yh = torch.empty(B, m, n, device=DEV, dtype=torch.float16)
+    yl = torch.empty_like(yh)
+    sgram.gram_A(W, ycol, float(ycol.max()) if weighted else 1.0, wmax, A, Gh, Gl, X3_SCALE, yh, yl)
+    if not weighted:  # A from one fp16 product (lo = 0) equals the three-product Gram bit for bit
+        A3 = torch.zeros_like(A)
+        ys0 = torch.empty(B, device=DEV)
+        K.residual_split(W, None, None, 2, wmax, hi=yh, lo=yl, scale=ys0)
+        assert int(yl.view(torch.int16).abs().max()) == 0
+        t = torch.empty(B, device=DEV)
+        K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys0 * ys0), A3, tri=True, a_blocked=True, b_blocked=True,
+                  out_h=Gh, out_l=Gl, out_scale=X3_SCALE, sym_bound=torch.full((B,), 2.0 ** 60, device=DEV,
+                                                                          dtype=torch.float64),
+                  scale_out=t, inv_out=t.clone())
+        up = torch.ones(m, m, dtype=torch.bool, device=DEV).triu()
+        assert torch.equal(A[:, up], A3[:, up])
+    gs = torch.empty(B, device=DEV)
+    ginv = torch.empty(B, device=DEV)
+    G32 = torch.empty(B, m, m, device=DEV)
+    assert SG.gram(W, packed, s, w, A, ysq, Gh, Gl, gs, ginv, X3_SCALE, G32=G32, max_density=1.0)
+    scale = G64.abs().amax(dim=(1, 2))
+    err32 = ((G32.double() - G64).abs().amax(dim=(1, 2)) / scale).max().item()
+    Gs = (_unblock(Gh, m).double() + _unblock(Gl, m).double()) / gs.double().view(B, 1, 1)
+    errs = ((Gs - G64).abs().amax(dim=(1, 2)) / scale).max().item()
+    Uh = _unblock(Gh, m)
+    assert torch.equal(G32, G32.transpose(1, 2)) and torch.equal(Uh, Uh.transpose(1, 2))
+    assert torch.allclose(ginv, 1.0 / (gs * X3_SCALE))
+
+    # the dense split-fp16 Gram of Y it replaces (cq_residual_split halves + cq_gemm_x3 sym_out)
+    ys = torch.empty(B, device=DEV)
+    K.residual_split(W, packed, s, 2, wmax, ycol=ycol, ycol_max=float(ycol.max()) if weighted else 1.0,
+                     hi=yh, lo=yl, scale=ys)
+    Dh, Dl = torch.empty_like(Gh), torch.empty_like(Gl)
+    ds, di = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), None, tri=True, a_blocked=True, b_blocked=True, out_h=Dh, out_l=Dl,
+              out_scale=X3_SCALE, sym_bound=ysq, scale_out=ds, inv_out=di)
+    assert torch.equal(ds, gs)
+    Gd = (_unblock(Dh, m).double() + _unblock(Dl, m).double()) / ds.double().view(B, 1, 1)
+    errd = ((Gd - G64).abs().amax(dim=(1, 2)) / scale).max().item()
+    print(f"B={B} m={m} n={n} w={weighted}: max|G - G64| / max|G64|: sparse fp32 {err32:.2e}, sparse halves "
+          f"{errs:.2e}, dense split Gram {errd:.2e}")
+    # fp32-grade: within 1.5x (+2e-7) of the dense split-fp16 Gram's own error, on every shape
+    assert err32 < 1.5 * errd + 2e-7 and errs < 1.5 * errd + 2e-7
