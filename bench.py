@@ -503,7 +503,9 @@ def main():
                 "bytes_per_launch": gp["bytes_per_launch"],
                 "operand": "Y = (W - Q) diag(ycol) per LR step" if kind == "gram" else
                            "W diag(ycol), once per decomposition (A of the sparse-code Gram)",
-                "kernel": "gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"}
+                "kernel": ("gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"
+                           if kind == "gram" else "gemm_x3v_kernel<true|false> (Gram of W: one fp16 product when "
+                           "H = I, W being exact in fp16; split-fp16 otherwise)")}
         if "gram_sparse" in gprobe:
             gp = gprobe["gram_sparse"]
             t = gp["avg_ms"] * 1e-3

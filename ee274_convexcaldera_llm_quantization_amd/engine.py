@@ -401,7 +401,11 @@ class CalderaEngine:
                 self._sg = sgram.SparseGram(B, m, n, dev)
                 self._sg_w = (wts.ycol * wts.ycol).contiguous() if weighted else None
                 sv._alloc(dev)
-                gev = GRAM_PROBE.start("gram_A", 3.0 * m * m * n * B, 4.0 * m * n * B + 4.0 * m * m * B)
+                # fp16 MFMA work: one product over the upper half (H = I: W's halves are W and 0),
+                # else the three split products; bytes: the operand halves read once, A written
+                nprod = 3.0 if weighted else 1.0
+                gev = GRAM_PROBE.start("gram_A", nprod * m * m * n * B, (4.0 if weighted else 2.0) * m * n * B
+                                       + 4.0 * m * m * B)
                 if gev is not None:
                     gev[0].record()
                 sgram.gram_A(Ws, wts.ycol if weighted else None, wts.ycol_max if weighted else 1.0, self._wmax,
@@ -443,7 +447,10 @@ class CalderaEngine:
             K.build_residual(Ws, qsrc, qsc, qbits, wts.ycol, Y=Y if weighted else None, res=res)
         Ysrc = Y if weighted else res  # Y = res * sqrt(h) (alg.py:211); identity H: Y = res
         Y = Ysrc
-        vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split, gram=gram)
+        if gram is not None:
+            vecs, theta = yield from sv.solve_iter(Ysrc, gram=gram)
+        else:
+            vecs, theta = yield from sv.solve_iter(Ysrc, y_split=y_split)
         rand = isinstance(sv, RandSVD)
         r = sv.r
         S = torch.sqrt(theta.clamp_min(0.0))  # singular values (fp64)
@@ -459,7 +466,7 @@ class CalderaEngine:
                 # R = (U^T Y) diag(1/sqrt(lam))   (alg.py:219-225); randomized: S Vh as returned
                 if rand:
                     R.copy_(sv.SVh)
-                elif y_split is not None and self._yth is not None:
+                elif (y_split is not None or gram is not None) and self._yth is not None:
                     self._ut_y(sv, R)
                 else:
                     K.gemm(U, Ysrc, ta=True, C=R)
@@ -472,7 +479,7 @@ class CalderaEngine:
                 K.scale_rc(U, colscale=sq, out=L)  # L = U sqrt(S)
                 if rand:
                     R.copy_(sv.SVh)
-                elif y_split is not None and self._yth is not None:
+                elif (y_split is not None or gram is not None) and self._yth is not None:
                     self._ut_y(sv, R)  # S Vh
                 else:
                     K.gemm(U, Ysrc, ta=True, C=R)  # S Vh
