@@ -25,7 +25,7 @@ fe, wr = vals(fetch_dir, "FETCH_SIZE"), vals(write_dir, "WRITE_SIZE")
 w_bytes, code_bytes = 2 * m * n, m * n * bits // 8
 res = {}
 for k in sorted(fe):
-    if k not in wr:
+    if k not in wr or not any(t in k for t in ("quant_w_stream", "q_update_p", "q_update_v")):
         continue
     fk, wk = statistics.mean(fe[k]), statistics.mean(wr[k])
     if "quant_w_stream" in k:
