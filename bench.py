@@ -524,7 +524,7 @@ def main():
     result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0), "stalled_matrices": st.get("stalls", 0),
                         "jacobi_unconverged": st.get("jacobi_unconverged", 0),
-                        "jacobi_budget_redos": st.get("jacobi_redo", 0)}
+                        "block_jacobi_readbacks": st.get("bj_readbacks", 0)}
     if rank == 0 and not args.no_parity:
         # parity of the LAST TIMED STEP's own results (rank 0: batch positions 0-3 = seeds 0-3)
         par = parity_of_timed_step(args.workload, decs, wl)

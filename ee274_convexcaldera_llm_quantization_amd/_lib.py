@@ -100,6 +100,8 @@ _SIGS = {
     "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_size, c_vp]),
+    "cq_jacobi_eigh_staged": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_double, c_int, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
                                  c_vp]),
@@ -500,6 +502,39 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
     _check(lib.cq_jacobi_eigh(_p(A), p, B, max_sweeps, tol, _p(ev), _p(V32), _p(V64), _p(sw), _p(ws),
                               ws.numel(), _stream(A.device)), "cq_jacobi_eigh")
     return ev, V32, V64, sw
+
+
+class BlockJacobi:
+    """cq_jacobi_eigh_staged for p > 192: begin + a first batch of sweeps, then further sweeps
+    only while the device count of unconverged matrices (read back by the caller) is nonzero."""
+    BEGIN, SWEEPS, END = 1, 2, 4
+
+    def __init__(self, A: torch.Tensor, tol: float, want_vectors: bool = True):
+        _require_hip(A)
+        self.A, self.tol, self.want = A, tol, bool(want_vectors)
+        self.B, self.p, _ = A.shape
+        self.ws = workspace(load().cq_jacobi_workspace(self.p, self.B), A.device)
+        self.pending = torch.zeros(1, dtype=torch.int32, device=A.device)
+        self.swept = 0
+
+    def _call(self, phase, nsweeps=0, ev=None, V32=None, sw=None):
+        _check(load().cq_jacobi_eigh_staged(_p(self.A), self.p, self.B, phase, nsweeps, self.tol, int(self.want),
+                                            _p(ev), _p(V32), None, _p(sw), _p(self.pending), _p(self.ws),
+                                            self.ws.numel(), _stream(self.A.device)), "cq_jacobi_eigh_staged")
+
+    def sweeps(self, n: int, begin: bool = False) -> int:
+        """n more sweeps; returns the number of matrices still unconverged (host read-back)."""
+        self._call((self.BEGIN if begin else 0) | self.SWEEPS, n)
+        self.swept += n
+        return int(self.pending.item())
+
+    def finish(self):
+        dev = self.A.device
+        ev = torch.empty((self.B, self.p), dtype=torch.float64, device=dev)
+        V32 = torch.empty((self.B, self.p, self.p), dtype=torch.float32, device=dev) if self.want else None
+        sw = torch.empty(self.B, dtype=torch.int32, device=dev)
+        self._call(self.END, 0, ev, V32, sw)
+        return ev, V32, None, sw
 
 
 def ritz_residual(X, Z, theta, r):

@@ -391,17 +391,26 @@ size_t bj_workspace(int64_t p, int64_t batch) {
     return s;
 }
 
-// Block-Jacobi eigensolver, stream-ordered: max_sweeps sweeps are launched without any host
-// read-back.  A matrix whose off-norm test passed (bj_check_kernel) has done[b] set, and every
-// later workgroup of that matrix exits at entry; the per-matrix sweep counts reach the caller
-// through sweeps_out (the solver reads them with its convergence check and sizes the next
-// call's budget from them, redoing an outer iteration whose budget ran out).
-int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
-            double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s) {
+__global__ void bj_pending_kernel(const int* __restrict__ done, int64_t batch, int* __restrict__ pending) {
+    int c = 0;
+    for (int64_t b = threadIdx.x; b < batch; b += blockDim.x) c += done[b] ? 0 : 1;
+    c = wave_sum(c);
+    if (threadIdx.x == 0) *pending = c;
+}
+
+// Block-Jacobi eigensolver in stages, every stage stream-ordered (no host read-back inside):
+//   BJ_BEGIN   V = I, per-matrix done flags and sweep counts cleared;
+//   BJ_SWEEPS  nsweeps sweeps; a matrix whose off-norm test passed (bj_check_kernel) has
+//              done[b] set and every later workgroup of it exits at entry; pending_out (device
+//              int, optional) = matrices still unconverged after these sweeps;
+//   BJ_END     eigenvalues (descending) and eigenvectors out, per-matrix sweep counts.
+// The state (A in place, Vt, flags) lives in the caller's workspace between stages, so a
+// caller that reads pending_out can launch further sweeps only where they are needed.
+int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double tol, bool want_v, double* evals,
+             float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws, size_t ws_bytes, hipStream_t s) {
     if (ws_bytes < bj_workspace(p, batch)) return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh: workspace too small");
     const int nblk = (int)(ceil_div(p, NB) + (ceil_div(p, NB) & 1));
     const int npair = nblk / 2, noff = npair * (npair - 1), nslots = npair + noff;
-    const bool want_v = V32 || V64;
     const int nch = (int)ceil_div(p, D);  // 64-column chunks of the eigenvector rows
     char* w = reinterpret_cast<char*>(ws);
     auto take = [&](size_t bytes) { char* r = w; w += align_up(bytes, 256); return r; };
@@ -414,19 +423,30 @@ int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, dou
     int* sweeps = reinterpret_cast<int*>(take((size_t)batch * sizeof(int)));
     int* ranks = reinterpret_cast<int*>(take((size_t)batch * p * sizeof(int)));
     const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
-    bj_init_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
-    for (int sw = 0; sw < max_sweeps; ++sw) {
-        for (int st = 0; st < nblk - 1; ++st) {
-            bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
-                                                                                   done, poff, pdg, nslots);
-            bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair * nch : 0)), (unsigned)batch), BT, 0, s>>>(
-                A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
+    if (phase & BJ_BEGIN)
+        bj_init_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
+    if (phase & BJ_SWEEPS) {
+        for (int sw = 0; sw < nsweeps; ++sw) {
+            for (int st = 0; st < nblk - 1; ++st) {
+                bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
+                                                                                       done, poff, pdg, nslots);
+                bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair * nch : 0)), (unsigned)batch), BT, 0, s>>>(
+                    A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
+            }
+            bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
         }
-        bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
+        if (pending_out) bj_pending_kernel<<<1, 64, 0, s>>>(done, batch, pending_out);
     }
-    bj_finish_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64, sweeps,
-                                                     sweeps_out, ranks);
+    if (phase & BJ_END)
+        bj_finish_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64, sweeps,
+                                                         sweeps_out, ranks);
     return check_launch("cq_jacobi_eigh (block Jacobi)");
+}
+
+int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
+            double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s) {
+    return bj_stage(A, p, batch, BJ_BEGIN | BJ_SWEEPS | BJ_END, max_sweeps, tol, V32 || V64, evals, V32, V64,
+                    sweeps_out, nullptr, ws, ws_bytes, s);
 }
 
 }  // namespace cq

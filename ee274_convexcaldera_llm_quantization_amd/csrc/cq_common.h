@@ -112,6 +112,9 @@ constexpr int64_t kBlockJacobiMinP = 192;
 size_t bj_workspace(int64_t p, int64_t batch);
 int bj_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol, double* evals, float* V32,
             double* V64, int* sweeps_out, void* ws, size_t ws_bytes, hipStream_t s);
+constexpr int BJ_BEGIN = 1, BJ_SWEEPS = 2, BJ_END = 4;
+int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double tol, bool want_v, double* evals,
+             float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace cq
 

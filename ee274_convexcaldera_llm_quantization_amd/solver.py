@@ -130,10 +130,10 @@ MAX_OUTER = 40  # outer iterations per solve (the schedule's last degree repeats
 
 
 JACOBI_MAX_SWEEPS = 30
-# block Jacobi (p > 192) launches its whole sweep budget stream-ordered (no host read-back
-# inside cq_jacobi_eigh); the solver sizes the budget from the sweep counts it reads with
-# each convergence check and redoes an outer iteration whose budget ran out
-BJ_BUDGET_START, BJ_BUDGET_MIN, BJ_BUDGET_MARGIN = 12, 4, 3
+# block Jacobi (p > 192) runs in caller-driven stages (cq_jacobi_eigh_staged, each stage
+# stream-ordered): a first batch of sweeps sized from the previous call, then BJ_STEP more at a
+# time while the device count of unconverged matrices (one int read back) is nonzero
+BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
 STALL_RATIO = 0.98
 
 
@@ -143,7 +143,7 @@ class SolverStats:
         self.matvecs = 0
         self.x3_fallbacks = 0
         self.jacobi_unconverged = 0  # Rayleigh-Ritz eigensolves that used all JACOBI_MAX_SWEEPS
-        self.jacobi_redo = 0         # outer iterations redone after a block-Jacobi budget ran out
+        self.bj_readbacks = 0        # block-Jacobi stage read-backs (one int each)
         self.stalls = 0              # matrices whose solve ended at the products' precision floor
         self.calls = 0
         self.max_resid = 0.0
@@ -152,7 +152,7 @@ class SolverStats:
 
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
-                    jacobi_unconverged=self.jacobi_unconverged, jacobi_redo=self.jacobi_redo, stalls=self.stalls,
+                    jacobi_unconverged=self.jacobi_unconverged, bj_readbacks=self.bj_readbacks, stalls=self.stalls,
                     max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks)
 
 
@@ -198,7 +198,7 @@ class RankRSolver:
         # Rayleigh-Ritz sweep budget: fixed for the one-workgroup Jacobi (its sweep loop runs
         # inside one kernel), adaptive for the block Jacobi (each sweep is a set of launches)
         self.block_jacobi = self.p > 192
-        self.jac_budget = BJ_BUDGET_START if self.block_jacobi else JACOBI_MAX_SWEEPS
+        self.bj_first = BJ_FIRST  # block Jacobi: sweeps launched before the first read-back
         self._bufs = None
         self._G = None
         self._yh = self._yl = None
@@ -314,17 +314,32 @@ class RankRSolver:
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps
-            theta, _, _, sw = K.jacobi_eigh(T, max_sweeps=self.jac_budget, tol=self.jacobi_tol_values,
-                                            want_vectors=False)
+            theta, _, _, sw = self._eigh(T, self.jacobi_tol_values, want_vectors=False)
             self._last_sw = sw
             return theta, X, None
-        theta, V32, _, sw = K.jacobi_eigh(T, max_sweeps=self.jac_budget, tol=self.jacobi_tol)
+        theta, V32, _, sw = self._eigh(T, self.jacobi_tol)
         self._last_sw = sw
         Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
         Zo = self._free(X, Z, Xo, *keep)
         K.gemm(Z, V32, C=Zo)
         return theta, Xo, Zo
+
+    def _eigh(self, T, tol, want_vectors=True):
+        """Rayleigh-Ritz eigensolve (descending).  p <= 192: one launch to convergence (A in
+        one CU's LDS).  p > 192: block Jacobi in stages -- bj_first sweeps, then BJ_STEP at a
+        time while matrices remain unconverged (one int read back per stage); bj_first follows
+        what the last call needed, so a warm call usually reads back once."""
+        if not self.block_jacobi:
+            return K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=tol, want_vectors=want_vectors)
+        bj = K.BlockJacobi(T, tol, want_vectors)
+        first = min(self.bj_first, JACOBI_MAX_SWEEPS)
+        left = bj.sweeps(first, begin=True)
+        while left and bj.swept < JACOBI_MAX_SWEEPS:
+            left = bj.sweeps(min(BJ_STEP, JACOBI_MAX_SWEEPS - bj.swept))
+        self.bj_first = bj.swept if bj.swept > first else max(BJ_MIN_FIRST, first - 1)
+        self.stats.bj_readbacks += 1 + (bj.swept - first + BJ_STEP - 1) // BJ_STEP
+        return bj.finish()
 
     def _cheb_coeffs(self, ends, deg, dev):
         """Coefficients of the scaled 3-term recurrence, from the host copy of the Ritz values
@@ -580,24 +595,13 @@ class RankRSolver:
                     res = K.ritz_residual(Xn, Zn, theta_n, self.r).double()
                 ovf = (self._ovf.max().double() if self.x3 and self._x3f
                        else torch.zeros((), dtype=torch.float64, device=dev))
-                # matrices whose Jacobi used its whole sweep budget, and the most sweeps any
-                # matrix needed (read back with the residuals)
-                budget = self.jac_budget
-                unconv = (self._last_sw >= budget).sum().double().view(1)
-                maxsw = self._last_sw.max().double().view(1)
-                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res, unconv, maxsw])
+                # matrices whose Jacobi used all JACOBI_MAX_SWEEPS (read back with the residuals)
+                unconv = (self._last_sw >= JACOBI_MAX_SWEEPS).sum().double().view(1)
+                chk = torch.cat([ovf.view(1), theta_n[:, 0], theta_n[:, p - 1], res, unconv])
                 yield
                 chk = chk.cpu().numpy()
-                n_unconv, maxsw = int(chk[-2]), int(chk[-1])
-                chk = chk[:-2]
-                if self.block_jacobi:
-                    if n_unconv and budget < JACOBI_MAX_SWEEPS:
-                        # the block Jacobi's budget ran out: redo this outer iteration (same
-                        # inputs, deterministic kernels) with the full budget
-                        self.jac_budget = JACOBI_MAX_SWEEPS
-                        self.stats.jacobi_redo += 1
-                        continue
-                    self.jac_budget = min(JACOBI_MAX_SWEEPS, max(BJ_BUDGET_MIN, maxsw + BJ_BUDGET_MARGIN))
+                n_unconv = int(chk[-1])
+                chk = chk[:-1]
                 self.stats.jacobi_unconverged += n_unconv
                 if self.x3 and self._x3f and chk[0] != 0:
                     # an fp16 half overflowed (a Ritz value far below the true top of the

@@ -220,6 +220,16 @@ size_t cq_jacobi_workspace(int64_t p, int64_t batch);
 int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol,
                    double* evals, float* V32, double* V64, int* sweeps_out, void* ws,
                    size_t ws_bytes, void* stream);
+/* The same eigensolve for p > 192 (block Jacobi over many workgroups) in caller-driven
+ * stages, each stream-ordered: phase bit 1 = begin (V = I), 2 = nsweeps sweeps (matrices that
+ * converged skip the rest; pending_out, a device int, = matrices still unconverged), 4 = end
+ * (evals, V32/V64, sweeps_out).  The state stays in ws (cq_jacobi_workspace) between calls,
+ * so a caller reading pending_out launches further sweeps only while some are needed (the
+ * Rayleigh-Ritz eigensolve of alg.py:217's replacement at rank > 136, e.g. main.py:176's
+ * rank 200 and config 5's rank 256).  want_vectors must be the same in every stage. */
+int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double tol, int want_vectors,
+                          double* evals, float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws,
+                          size_t ws_bytes, void* stream);
 
 /* Ritz residuals: out[b] = max_{i<r} ||Z[:,i] - theta_i X[:,i]||_2 / |theta_0|
  * (X, Z: k x p row-major with ld p).  theta fp64 [b*p..]. */

@@ -311,6 +311,30 @@ def test_jacobi_block_path_ragged_batch(K, p):
     assert res.abs().max().item() < 1e-10 * ref.max().item()
 
 
+@pytest.mark.parametrize("want_vectors", [True, False])
+def test_jacobi_block_staged_equals_one_shot(K, want_vectors):
+    """cq_jacobi_eigh_staged (begin + 2 sweeps, then 2 at a time while the device count of
+    unconverged matrices is nonzero, then end) runs the same kernel sequence as the one-shot
+    cq_jacobi_eigh: eigenvalues, vectors and per-matrix sweep counts are identical, and the
+    pending count reaches 0 no later than the slowest matrix's sweep count."""
+    torch.manual_seed(41)
+    p = 288
+    X = torch.randn(3, 1024, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    _, U = torch.linalg.eigh(S[1])
+    Qp, _ = torch.linalg.qr(U + 1e-5 * torch.randn_like(U))
+    S[1] = 0.5 * ((Qp.T @ S[1] @ Qp) + (Qp.T @ S[1] @ Qp).T)
+    ev1, V1, _, sw1 = K.jacobi_eigh(S.clone().to(DEV), tol=1e-9, want_vectors=want_vectors)
+    bj = K.BlockJacobi(S.clone().to(DEV), 1e-9, want_vectors)
+    left = bj.sweeps(2, begin=True)
+    while left and bj.swept < 30:
+        left = bj.sweeps(2)
+    ev2, V2, _, sw2 = bj.finish()
+    assert left == 0 and bj.swept - int(sw1.max()) in (0, 1)
+    assert torch.equal(ev1, ev2) and torch.equal(sw1, sw2)
+    assert (V1 is None and V2 is None) or torch.equal(V1, V2)
+
+
 @pytest.mark.parametrize("p", [64, 128, 180, 192])
 def test_jacobi_register_path_accuracy(K, p):
     """p <= 192: fp64 A in LDS + fp32 V in registers (the solver's Rayleigh-Ritz path):
