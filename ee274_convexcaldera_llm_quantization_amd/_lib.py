@@ -119,7 +119,7 @@ _SIGS = {
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cq_sgram_rows": (c_int, [c_i64]),
     "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
                               c_vp]),
@@ -749,11 +749,11 @@ def sgram_count(packed, k, L, row_nnz, perm, slice_off, total):
                                  _stream(packed.device)), "cq_sgram_count")
 
 
-def sgram_fill(packed, k, L, perm, slice_off, ell, stride):
-    _require_hip(packed, perm, slice_off, ell)
+def sgram_fill(packed, k, L, row_nnz, perm, slice_off, ell, stride):
+    _require_hip(packed, row_nnz, perm, slice_off, ell)
     B = slice_off.numel() // (-(-k // 64) + 1)
     assert ell.numel() >= B * stride
-    _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(perm), _p(slice_off), stride, _p(ell),
+    _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), stride, _p(ell),
                                 _stream(packed.device)), "cq_sgram_fill")
 
 

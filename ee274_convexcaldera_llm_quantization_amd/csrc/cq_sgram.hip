@@ -11,14 +11,15 @@
 // identical to cq_gemm_x3's sym_out output):
 //   sgram_count_kernel   nonzero codes per row of c;
 //   sgram_slices_kernel  rows sorted by count, per 64-row slice the widest -> sliced-ELL offsets;
-//   sgram_fill_kernel    the ELL entries (l << 2 | code + 1), per row in increasing l;
-//                        (a slice holds 64 rows of similar count: padding ~ a few %)
+//   sgram_fill_kernel    the ELL entries (l << 2 | code + 1), per row in an order that keeps the
+//                        lanes of a step in different LDS bank groups (l mod 16); a slice holds
+//                        64 rows of similar count (padding ~ a few %)
 //   sgram_spmm_kernel    P[i, j] = sum_{l in row j of c} c_jl (E_il w_l): a workgroup stages R
 //                        rows of E (fp32, l-major, R values per l) in LDS and sweeps every row j
 //                        of c with one lane per j (64 rows per wave, coalesced ELL reads);
 //   sgram_combine_kernel G = A - s (P + P^T) per 64 x 64 tile pair (I <= J), P^T through LDS,
 //                        split halves written at (i, j) and mirrored (j, i).
-// Every sum runs in a fixed order (per row j in increasing l): results are deterministic.
+// Every sum runs in a fixed order (per row j the fill order): results are deterministic.
 #include "cq_common.h"
 
 namespace cq {
@@ -96,7 +97,10 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
     }
 }
 
+constexpr int SG_FILL_CAP = 512;
+
 __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
+                                                         const int32_t* __restrict__ row_nnz,
                                                          const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ slice_off, int64_t stride_ell,
                                                          uint32_t* __restrict__ ell) {
@@ -111,29 +115,53 @@ __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restri
     uint32_t* out = ell + b * stride_ell + off * SG_SLICE + (p % SG_SLICE);
     const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
     const int64_t nw = L / 16;
+    // Entry order.  The SpMM reads E's l-th 16-byte slab entry (LDS bank group l mod 16) for the
+    // 64 rows of a slice at once, one lane per row; lanes whose entries share a bank group at the
+    // same step serialise.  Step t of the row at lane q therefore takes an entry of residue
+    // (q + t) mod 16 while it has one (neighbouring lanes then read different groups), else one
+    // of the residue with the most entries left (ties: the smaller residue); within a residue in
+    // increasing l.  Rows longer than SG_FILL_CAP fall back to the plain residue-rotated order.
+    const int q = (int)(p & 15);
+    __shared__ uint32_t buf[4][SG_FILL_CAP];
+    uint32_t* wb = buf[threadIdx.x >> 6];
     int64_t base = 0;
-    for (int64_t w0 = 0; w0 < nw; w0 += 64) {
-        const int64_t w = w0 + lane;
-        const uint32_t word = w < nw ? row[w] : 0x55555555u;
-        const uint32_t msk = sg_nz_mask(word);
-        const uint32_t cnt = __popc(msk);
-        uint32_t incl = cnt;  // inclusive scan over the lanes: the row's entries in increasing l
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += o;
-        }
-        int64_t pos = base + incl - cnt;
-        if (msk) {
-            for (int u = 0; u < 16; ++u) {
-                const uint32_t f = sg_field(word, u);
-                if (f != 1u) {
-                    out[pos * SG_SLICE] = (uint32_t)((16 * w + u) << 2) | f;
-                    ++pos;
-                }
+    int rstart = 0, rcnt = 0;  // lane u < 16: residue u's entries in wb
+    const bool fits = row_nnz[b * k + j] <= SG_FILL_CAP;
+    for (int i = 0; i < 16; ++i) {
+        const int u = (q + i) & 15;
+        const int64_t b0 = base;
+        for (int64_t w0 = 0; w0 < nw; w0 += 64) {
+            const int64_t w = w0 + lane;
+            const uint32_t f = w < nw ? sg_field(row[w], u) : 1u;
+            const bool nz = f != 1u;
+            const uint64_t msk = __ballot(nz);
+            if (nz) {
+                const int64_t pos = base + __popcll(msk & ((1ull << lane) - 1ull));
+                const uint32_t e = (uint32_t)((16 * w + u) << 2) | f;
+                if (fits) wb[pos] = e;
+                else out[pos * SG_SLICE] = e;
             }
+            base += __popcll(msk);
         }
-        base += __shfl(incl, 63, 64);
+        if (lane == u) { rstart = (int)b0; rcnt = (int)(base - b0); }
+    }
+    if (fits) {
+        __builtin_amdgcn_wave_barrier();
+        int taken = 0;
+        for (int64_t t = 0; t < base; ++t) {
+            const int d = (int)((q + t) & 15);
+            int u = d;
+            if (__shfl(rcnt - taken, d, 64) <= 0) {
+                // the residue with the most entries left: key = remaining * 16 + (15 - residue)
+                int key = lane < 16 ? ((rcnt - taken) << 4) | (15 - lane) : -1;
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) key = max(key, __shfl_xor(key, o, 64));
+                u = 15 - (__shfl(key, 0, 64) & 15);
+            }
+            const int at = __shfl(rstart + taken, u, 64);
+            if (lane == 0) out[t * SG_SLICE] = wb[at];
+            if (lane == u) ++taken;
+        }
     }
     for (int64_t t = base + 0; t < width; ++t) out[t * SG_SLICE] = 1u;  // padding: l = 0, code 0
 }
@@ -143,16 +171,29 @@ __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restri
 constexpr int SG_PF = 6;
 constexpr int SG_WAVES = 16, SG_THREADS = 64 * SG_WAVES;
 
+// E slab layout: planes of SG_PL rows, each plane l-major with SG_PL floats per l (16 bytes
+// for R >= 4: the l-th entry starts in LDS bank group l mod 16)
 template <int R>
-__device__ __forceinline__ void sg_slice(const float* __restrict__ slab, const uint32_t* __restrict__ ep, int64_t width,
-                                         float (&acc)[R]) {
+__device__ __forceinline__ int64_t sg_slab_at(int64_t L, int64_t l, int r) {
+    constexpr int PL = R < 4 ? R : 4;
+    return (int64_t)(r / PL) * PL * L + l * PL + (r % PL);
+}
+
+template <int R>
+__device__ __forceinline__ void sg_slice(const float* __restrict__ slab, int64_t L, const uint32_t* __restrict__ ep,
+                                         int64_t width, float (&acc)[R]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    constexpr int PL = R < 4 ? R : 4;
     auto fma_entry = [&](uint32_t e) {
         const float c = (float)((int)(e & 3u) - 1);
-        const float* v = slab + (e >> 2) * R;
+        const int64_t l = e >> 2;
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = __builtin_fmaf(c, v[r], acc[r]);
+        for (int pl = 0; pl < R / PL; ++pl) {
+            const float* v = slab + (int64_t)pl * PL * L + l * PL;
+#pragma unroll
+            for (int r = 0; r < PL; ++r) acc[pl * PL + r] = __builtin_fmaf(c, v[r], acc[pl * PL + r]);
+        }
     };
     int64_t t = 0;
     if (width >= SG_PF) {
@@ -175,10 +216,10 @@ __device__ __forceinline__ void sg_slice(const float* __restrict__ slab, const u
 }
 
 // P[b, i0 + r, j] for r < R and every row j of c.  LDS: E rows i0 .. i0 + R - 1 as
-// slab[l * R + r] (fp32), E_il = (W_il - (s/2) c_il) * w_l.  Wave wv takes the slices wv,
+// the l-major slab (sg_slab_at, fp32), E_il = (W_il - (s/2) c_il) * w_l.  Wave wv takes the slices wv,
 // wv + 16, ...; with NSW > 0 (ceil(ns / 16) <= NSW) it keeps all of its results in registers and
-// the R output rows are assembled in LDS (the slab's space, k <= L) and stored row by row --
-// the sorted slices' rows are scattered over j, so direct stores would be 4-byte scatters
+// the R output rows are assembled in LDS (the slab's space, k <= L, j-major) and stored over j
+// -- the sorted slices' rows are scattered over j, so direct stores would be 4-byte scatters
 template <int R, int NSW>
 __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __restrict__ W, const uint8_t* __restrict__ packed,
                                                          const float* __restrict__ qscale, const float* __restrict__ wcol,
@@ -191,28 +232,55 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
     const int64_t i0 = (int64_t)blockIdx.x * R;
     const float hs = 0.5f * qscale[b];
     const int64_t KL = k * L;
-    // stage: 8 consecutive l per thread and row
-    for (int r = 0; r < R; ++r) {
-        const int64_t i = i0 + r;
+    // stage: per plane, a thread loads 8 consecutive l of each of its PL rows (16-byte W and
+    // 2-byte code loads) and stores the 8 l-entries (PL floats each) in an order rotated by its
+    // lane (t mod 8): the 8 lanes of a ds_write_b128 group then hit 8 different bank groups
+    // instead of one (the entries of consecutive lanes lie 128 bytes apart)
+    constexpr int PL = R < 4 ? R : 4;
+#pragma unroll
+    for (int pl = 0; pl < R / PL; ++pl) {
         for (int64_t l0 = (int64_t)threadIdx.x * 8; l0 < L; l0 += SG_THREADS * 8) {
-            float e[8];
-            if (i < k) {
-                const uint4 raw = *reinterpret_cast<const uint4*>(W + b * KL + i * L + l0);
-                const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
-                const uint16_t two = *reinterpret_cast<const uint16_t*>(packed + (b * KL + i * L + l0) / 4);
+            float e[PL][8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t byte = (u < 4) ? (two & 0xffu) : (two >> 8);
-                    const float c = (float)((int)((byte >> (6 - 2 * (u & 3))) & 3u) - 1);
-                    e[u] = (float)hv[u] - hs * c;
-                    if (wcol) e[u] *= wcol[l0 + u];
+            for (int r = 0; r < PL; ++r) {
+                const int64_t i = i0 + pl * PL + r;
+                if (i < k) {
+                    const int64_t el = b * KL + i * L + l0;
+                    const uint4 raw = *reinterpret_cast<const uint4*>(W + el);
+                    const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
+                    const uint16_t two = *reinterpret_cast<const uint16_t*>(packed + el / 4);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t byte = (u < 4) ? (two & 0xffu) : (two >> 8);
+                        const float c = (float)((int)((byte >> (6 - 2 * (u & 3))) & 3u) - 1);
+                        e[r][u] = (float)hv[u] - hs * c;
+                        if (wcol) e[r][u] *= wcol[l0 + u];
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) e[r][u] = 0.f;
                 }
-            } else {
+            }
+            const int rot = threadIdx.x & 7;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) e[u] = 0.f;
+            for (int sh = 1; sh < 8; sh <<= 1) {  // e[r][u] <- e[r][(u + rot) & 7], log shifter
+                if (rot & sh) {
+#pragma unroll
+                    for (int r = 0; r < PL; ++r) {
+                        float t8[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) t8[u] = e[r][(u + sh) & 7];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) e[r][u] = t8[u];
+                    }
+                }
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) slab[(l0 + u) * R + r] = e[u];
+            for (int u = 0; u < 8; ++u) {
+                float* dst = slab + (int64_t)pl * PL * L + (l0 + ((u + rot) & 7)) * PL;
+                if constexpr (PL == 4) *reinterpret_cast<float4*>(dst) = make_float4(e[0][u], e[1][u], e[2][u], e[3][u]);
+                else *reinterpret_cast<float2*>(dst) = make_float2(e[0][u], e[1][u]);
+            }
         }
     }
     __syncthreads();
@@ -227,28 +295,46 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
 #pragma unroll
         for (int q = 0; q < NSW; ++q) {
             const int64_t s = wv + SG_WAVES * q;
-            if (s < ns) sg_slice<R>(slab, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc[q]);
+            if (s < ns) sg_slice<R>(slab, L, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc[q]);
         }
-        __syncthreads();  // every wave is done with the slab: it becomes the R x k output rows
+        __syncthreads();  // every wave is done with the slab: it becomes the k x R output block
+        // (j-major, one 16- or 8-byte store per PL rows: few LDS writes for the scattered j)
 #pragma unroll
         for (int q = 0; q < NSW; ++q) {
             const int64_t p = (wv + SG_WAVES * q) * SG_SLICE + lane;
             if (p < k) {
-                const int64_t j = pm[p];
+                float* dst = slab + pm[p] * R;
 #pragma unroll
-                for (int r = 0; r < R; ++r) slab[r * k + j] = acc[q][r];
+                for (int pl = 0; pl < R / PL; ++pl) {
+                    if constexpr (PL == 4)
+                        *reinterpret_cast<float4*>(dst + 4 * pl) = make_float4(acc[q][4 * pl], acc[q][4 * pl + 1],
+                                                                              acc[q][4 * pl + 2], acc[q][4 * pl + 3]);
+                    else *reinterpret_cast<float2*>(dst) = make_float2(acc[q][0], acc[q][1]);
+                }
             }
         }
         __syncthreads();
-        for (int r = 0; r < R; ++r) {
-            if (i0 + r >= k) break;
-            for (int64_t j = (int64_t)threadIdx.x * 4; j < k; j += SG_THREADS * 4)
-                *reinterpret_cast<float4*>(Pb + (i0 + r) * k + j) = *reinterpret_cast<const float4*>(slab + r * k + j);
+        // one j per thread: its R values (contiguous in LDS) to the R rows of P, coalesced over j
+        for (int64_t j = threadIdx.x; j < k; j += SG_THREADS) {
+            float v[R];
+#pragma unroll
+            for (int pl = 0; pl < R / PL; ++pl) {
+                if constexpr (PL == 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(slab + j * R + 4 * pl);
+                    v[4 * pl] = x.x; v[4 * pl + 1] = x.y; v[4 * pl + 2] = x.z; v[4 * pl + 3] = x.w;
+                } else {
+                    const float2 x = *reinterpret_cast<const float2*>(slab + j * R);
+                    v[0] = x.x; v[1] = x.y;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (i0 + r < k) Pb[(i0 + r) * k + j] = v[r];
         }
     } else {
         for (int64_t s = wv; s < ns; s += SG_WAVES) {
             float acc[R];
-            sg_slice<R>(slab, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc);
+            sg_slice<R>(slab, L, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc);
             const int64_t p = s * SG_SLICE + lane;
             if (p < k) {
                 const int64_t j = pm[p];
@@ -388,14 +474,14 @@ int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, in
     return check_launch("cq_sgram_count");
 }
 
-int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* perm,
-                  const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream) {
-    CQ_REQUIRE(packed && perm && slice_off && ell, "cq_sgram_fill: null argument");
+int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
+                  const int32_t* perm, const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream) {
+    CQ_REQUIRE(packed && row_nnz && perm && slice_off && ell, "cq_sgram_fill: null argument");
     CQ_REQUIRE(bits == 2, "cq_sgram_fill: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0 && L < (1ll << 29),
                "cq_sgram_fill: bad shape");
     sgram_fill_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, as_stream(stream)>>>(
-        packed, k, L, perm, slice_off, stride_ell, ell);
+        packed, k, L, row_nnz, perm, slice_off, stride_ell, ell);
     return check_launch("cq_sgram_fill");
 }
 
@@ -418,8 +504,8 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     const dim3 grid((unsigned)ceil_div(k, R), (unsigned)batch);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const int64_t nsw = ceil_div(ceil_div(k, SG_SLICE), SG_WAVES);  // slices per wave
-    // the register-held form needs k % 4 == 0 (float4 row stores) and k <= L (LDS reuse)
-    const bool held = k % 4 == 0 && k <= L && nsw * R <= 32;
+    // the register-held form needs k <= L (the output block reuses the slab's LDS)
+    const bool held = k <= L && nsw * R <= 32;
 #define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
                                                                              perm, slice_off, stride_ell, P)
     if (R == 8) {

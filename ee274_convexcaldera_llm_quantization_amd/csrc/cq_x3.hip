@@ -374,8 +374,11 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
         const int64_t orig = blockIdx.x;
         const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
         const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-        tn = lin % a.tiles_n;
-        tm = (lin / a.tiles_n) % a.tiles_m;
+        // row tiles fastest: when A has more than one 192-row tile (the filter at p > 192), the
+        // tiles sharing one 384-row panel of B (G) run together on one XCD and read its K slices
+        // once from HBM and again from L2
+        tm = lin % a.tiles_m;
+        tn = (lin / a.tiles_m) % a.tiles_n;
         b = lin / (a.tiles_n * a.tiles_m);
     }
     const int64_t m0 = tm * XW_BM, n0 = tn * XW_BN;

@@ -82,7 +82,7 @@ class SparseGram:
         # fixed capacity per matrix (a stable scratch shape across LR steps)
         stride = -(-int(max(MAX_DENSITY, self.density) * m * n) // 4096) * 4096
         ell = scratch.get("sgram.ell", (B * stride,), torch.int32, dev)
-        K.sgram_fill(packed, m, n, self.perm, self.slice_off, ell, stride)
+        K.sgram_fill(packed, m, n, self.row_nnz, self.perm, self.slice_off, ell, stride)
         P = scratch.get("sgram.P", (B, m, m), torch.float32, dev)
         K.sgram_spmm(Ws, packed, qscale, w, ell, self.perm, self.slice_off, stride, P)
         K.sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, gscale, ginv, G32=G32)

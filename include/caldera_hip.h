@@ -341,7 +341,8 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  *                     (batch x k x L, offset-binary MSB-first), perm (batch x k, int32: rows
  *                     sorted by count, descending, ties in row order), slice_off (batch x (ceil(k/64)
  *                     + 1), int64: sliced-ELL offsets per 64-row slice, in 64-entry rows), total[b] entries;
- *   cq_sgram_fill:    the ELL entries (uint32: l << 2 | code + 1) of matrix b at ell + b stride_ell;
+ *   cq_sgram_fill:    the ELL entries (uint32: l << 2 | code + 1) of matrix b at ell + b stride_ell
+ *                     (row_nnz, perm, slice_off from cq_sgram_count);
  *   cq_sgram_rows:    rows of E a workgroup stages for contraction length L (0: too long);
  *   cq_sgram_spmm:    P (batch x k x k fp32) from W (fp16, batch x k x L), the codes, qscale[b] = s
  *                     and wcol (L, may be NULL = 1);
@@ -352,8 +353,8 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  * k % 64 == 0, L % 64 == 0. */
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
                    int32_t* perm, int64_t* slice_off, int64_t* total, void* stream);
-int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* perm,
-                  const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream);
+int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
+                  const int32_t* perm, const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream);
 int cq_sgram_rows(int64_t L);
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
                   int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,

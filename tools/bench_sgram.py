@@ -58,7 +58,7 @@ stride = -(-int(max(sgram.MAX_DENSITY, SG.density) * m * n) // 4096) * 4096
 ell = scratch.get("sgram.ell", (B * stride,), torch.int32, dev)
 P = scratch.get("sgram.P", (B, m, m), torch.float32, dev)
 t_c = timed(lambda: K.sgram_count(packed, m, n, SG.row_nnz, SG.perm, SG.slice_off, SG.total))
-t_f = timed(lambda: K.sgram_fill(packed, m, n, SG.perm, SG.slice_off, ell, stride))
+t_f = timed(lambda: K.sgram_fill(packed, m, n, SG.row_nnz, SG.perm, SG.slice_off, ell, stride))
 t_p = timed(lambda: K.sgram_spmm(W, packed, s, None, ell, SG.perm, SG.slice_off, stride, P))
 t_g = timed(lambda: K.sgram_combine(A, P, s, ysq, X3_SCALE, Gh, Gl, gs, gi))
 t_all = timed(lambda: SG.gram(W, packed, s, None, A, ysq, Gh, Gl, gs, gi, X3_SCALE))
