@@ -674,7 +674,10 @@ class CalderaEngine:
         cb = p.method_LR != "uniform"
         best_items = [None] * B
         resH = None
-        best = dict(L=torch.zeros((B, m, r), device=dev), R=torch.zeros((B, r, n), device=dev),
+        # uniform quantisers keep only the kept iterate's codes and scales (its L, R are their
+        # dequantisation, rebuilt once after the loop); codebook methods keep the floats
+        best = dict(L=torch.zeros((B, m, r), device=dev) if cb else None,
+                    R=torch.zeros((B, r, n), device=dev) if cb else None,
                     Lc=torch.zeros((B, m * r), dtype=K.code_dtype(p.L_bits), device=dev),
                     Rc=torch.zeros((B, r * n), dtype=K.code_dtype(p.R_bits), device=dev),
                     Ls=torch.zeros(B, device=dev), Rs=torch.zeros(B, device=dev))
@@ -737,10 +740,7 @@ class CalderaEngine:
             if not cb:
                 # device-side selection: no host round trip per LPLR iteration
                 bm = better.view(B, 1)
-                best["L"] = torch.where(bm.view(B, 1, 1), L, best["L"])
-                best["R"] = torch.where(bm.view(B, 1, 1), R, best["R"])
-                best["Lc"] = torch.where(bm, qL["codes"].view(B, m, r).transpose(1, 2).reshape(B, m * r),
-                                         best["Lc"])  # L^T order
+                best["Lc"] = torch.where(bm, qL["codes"].view(B, m * r), best["Lc"])  # L layout
                 best["Rc"] = torch.where(bm, qR["codes"].view(B, r * n), best["Rc"])
                 best["Ls"] = torch.where(better, qL["scale"].view(B), best["Ls"])
                 best["Rs"] = torch.where(better, qR["scale"].view(B), best["Rs"])
@@ -759,7 +759,11 @@ class CalderaEngine:
             st.R_idxs = [it[1][0] if it else None for it in best_items]
             st.R_scale = [it[1][1] if it else None for it in best_items]
         else:
-            st.L_idxs, st.R_idxs = best["Lc"], best["Rc"]
+            # the kept L, R are exactly the dequantised kept codes (qL/qR["deq"] is (c / k) s)
+            best["L"] = K.dequantize_uniform(best["Lc"], best["Ls"], p.L_bits).view(B, m, r)
+            best["R"] = K.dequantize_uniform(best["Rc"], best["Rs"], p.R_bits).view(B, r, n)
+            st.L_idxs = best["Lc"].view(B, m, r).transpose(1, 2).reshape(B, m * r)  # L^T order
+            st.R_idxs = best["Rc"]
             st.L_scale, st.R_scale = best["Ls"], best["Rs"]
         self._lplr_err2 = best_err2
         return best["L"], best["R"]
