@@ -607,10 +607,33 @@ class CalderaEngine:
             ev[1].record()
         return Bm, K.gram_f64(Rw, Rw, ta=True, tb=True)     # r x r
 
-    def lplr_L_from(self, Bm, Mr, n, L):
+    @staticmethod
+    def _mm_x3(A, B_nk, C, tB=False):
+        """C = A B_nk^T (tB: A B_nk, B_nk then given as K x N) on split-fp16 MFMAs (three fp16
+        products, fp32 accumulation; per-matrix power-of-two scales): the LPLR loop's
+        normal-equation GEMMs (m x r x r, r x r x n), fp32-grade at a fraction of the fp32 MFMA
+        time.  A (B, M, K), C (B, M, N) fp32."""
+        sA = K.pow2_scale(A, 14)
+        ah, al = K.split_f16(A, sA)
+        sB = K.pow2_scale(B_nk, 14)
+        if tB:
+            Bt, kk, nn = B_nk.shape
+            bh = torch.empty((Bt, nn, kk), dtype=torch.float16, device=A.device)
+            bl = torch.empty_like(bh)
+            K.transpose_split(B_nk, hi=bh, lo=bl, scale=sB)
+        else:
+            bh, bl = K.split_f16(B_nk, sB)
+        return K.gemm_x3(ah, al, bh, bl, 1.0 / (sA * sB), C)
+
+    def lplr_L_from(self, Bm, Mr, n, L, x3=False):
         """L = Bm Mr^{-1} through the whitening Wr Wr^T = Mr^{-1} (rank-revealing at gelsy's
-        rcond for A = (R H_sqrt)^T, n x r).  Mr is overwritten."""
+        rcond for A = (R H_sqrt)^T, n x r).  Mr is overwritten.  x3: the two m x r x r GEMMs on
+        split-fp16 MFMAs."""
         Wr, _ = self._solve_normal(Mr, n)
+        if x3:
+            T1 = self._mm_x3(Bm, Wr, torch.empty_like(L), tB=True)  # (Y Rw^T) Wr
+            self._mm_x3(T1, Wr, L)                                   # ... Wr^T
+            return L
         T1 = K.gemm(Bm, Wr, C=torch.empty_like(L))          # (Y Rw^T) Wr
         K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
         return L
@@ -649,6 +672,11 @@ class CalderaEngine:
             Ct = K.gemm(L, res, ta=True, C=tmp_rn)         # r x n
         if ev is not None:
             ev[1].record()
+        if halves is not None and r % 32 == 0:  # the two r x r x n GEMMs on split-fp16 MFMAs
+            Wlt = K.transpose_split(Wl, out=torch.empty_like(Wl))[0]
+            T2 = self._mm_x3(Wlt, Ct, torch.empty_like(tmp_rn), tB=True)   # Wl^T Ct
+            self._mm_x3(Wl, T2, R, tB=True)                                 # Wl T2
+            return R, Ml
         T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
         K.gemm(Wl, T2, C=R)
         return R, Ml
@@ -700,7 +728,7 @@ class CalderaEngine:
         best_err2 = ysq.clone() if fused_err and not cb else None
         for _ in range(p.lplr_iters):
             # --- L = lstsq((R H_sqrt)^T, (res H_sqrt)^T)^T   (alg.py:162-169)
-            self.lplr_L_from(Bm, Mr, n, L)
+            self.lplr_L_from(Bm, Mr, n, L, x3=halves is not None and r % 32 == 0)
             # --- quantise L^T as one block (alg.py:171-172)
             if cb:
                 Lt = K.transpose_split(L, out=torch.empty((B, r, m), dtype=torch.float32, device=dev))[0]

@@ -77,8 +77,8 @@ def test_lplr_split_products_vs_fp64(m, n, r):
 
 
 def test_lplr_loop_split_vs_fp32_engine(monkeypatch):
-    """The engine end to end on H = I with quantised factors: split-fp16 LPLR products on
-    (default) and off give final errors within 1e-3 relative (the loop itself is chaotic --
+    """The engine end to end on H = I with quantised factors: split-fp16 LPLR products (and
+    normal-equation GEMMs) on (default) and off give final errors within 1e-3 relative (the loop itself is chaotic --
     tests/test_gpu_lplr_teacher.py)."""
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
@@ -100,8 +100,9 @@ def test_lplr_loop_split_vs_fp32_engine(monkeypatch):
         eng.lplr_x3 = x3
         calls.clear()
         out = eng.run(W)
-        # per LR update: lplr_iters + 1 Y R^T products (m x r); lplr_iters L^T res plus LR_init's
-        # U^T Y (r x n, from the same Y^T halves)
-        assert (calls.count((2, 512, 64)), calls.count((2, 64, 1024))) == ((2 * 4, 2 * 4) if x3 else (0, 0))
+        # per LR update: lplr_iters + 1 Y R^T products and 2 lplr_iters normal-equation GEMMs
+        # (Bm Wr, T1 Wr^T) with m x r outputs; lplr_iters L^T res, LR_init's U^T Y (from the
+        # same Y^T halves) and 2 lplr_iters normal-equation GEMMs (Wl^T Ct, Wl T2), r x n
+        assert (calls.count((2, 512, 64)), calls.count((2, 64, 1024))) == ((2 * 10, 2 * 10) if x3 else (0, 0))
         errs[x3] = np.array([o["errors"]["LR"][-1] for o in out], dtype=np.float64)
     np.testing.assert_allclose(errs[True], errs[False], rtol=1e-3)
