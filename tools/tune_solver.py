@@ -39,8 +39,11 @@ for spec in sys.argv[3:]:
     el = time.perf_counter() - t0
     par = bench.parity_of_timed_step(name, decs, wl)
     st = eng.solver.stats
-    ps = " ".join(f"{k}={v:.1e}" for k, v in par.items() if k.startswith("seed"))
+    rels = [v for k, v in par.items() if k.startswith("seed") and isinstance(v, float)]
+    fc = par.get("final_codes_summary", {})
     print(f"{spec:44s} {B / el:7.1f} matrices/s {1000 * el:8.1f} ms  matvecs {st.matvecs:4d} outer {st.outer:3d}  "
-          f"{ps}  hist {[(hh[1], ['%.1e' % x for x in hh[2]]) for hh in st.history]}", flush=True)
+          f"stalls {st.stalls}  rel(seeds) max {max(rels):.2e} median {sorted(rels)[len(rels) // 2]:.2e}  "
+          f"codes bit-exact {fc.get('bit_exact')}/{fc.get('matrices')} near-tie flips {fc.get('flips_at_near_ties')} "
+          f"unexplained rows {fc.get('rows_unexplained')}", flush=True)
     del decs, eng
     torch.cuda.empty_cache()
