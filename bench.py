@@ -456,7 +456,9 @@ def main():
     for kind, g in qprobe.items():
         t = g["avg_ms"] * 1e-3
         gbs = g["bytes_per_launch"] / t / 1e9
-        f16 = 2 * 3 * g["flops_per_launch"]  # two passes, three fp16 products each
+        # one recompute of L R per call, three fp16 products each: the 2-bit
+        # list path (cq_q_update_x3 scale_hint) recomputes once; other widths take two passes
+        f16 = 3 * g["flops_per_launch"]
         t_mfma = f16 / (PEAK_F16_MFMA_TFLOPS * 1e12)
         t_hbm = g["bytes_per_launch"] / (PEAK_HBM_GBS * 1e9)
         qroof["first_Q" if kind == "w" else "Q_with_LR"] = {
@@ -465,7 +467,10 @@ def main():
             "frac_of_bound": max(t_hbm, t_mfma) / t, "launches_timed": g["count"], "avg_call_ms": g["avg_ms"],
             "bytes_per_call": g["bytes_per_launch"],
             "kernel": ("quant_w_stream_kernel (cq_q_update_x3, r = 0, max|W| known)" if kind == "w"
-                       else "q_update_p_kernel<0|1, bits> (cq_q_update_x3 row panels; q_update_v_kernel past r = 256)")}
+                       else "q_update_p_kernel<2> + qp_codes_kernel (2-bit: one L R recompute, candidate lists; "
+                            "q_update_p_kernel<0|1> two passes otherwise or on fallback)")}
+        if kind != "w":
+            qroof["Q_with_LR"]["second_recomputes_last_step"] = eng.q_fallbacks
     if qroof:
         result["roofline_quantise"] = qroof
     if lprobe:

@@ -12,6 +12,8 @@ import os
 
 import torch
 
+from . import scratch
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcaldera_hip.so")
 
@@ -126,7 +128,7 @@ _SIGS = {
     "cq_sgram_combine": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_product_error": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_batched_dot": (c_int, [c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_act_sqsum_workspace": (c_size, [c_i64, c_i64]),
@@ -696,11 +698,15 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
 
 
 def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None, bits: int, *, eps: float = 1e-8,
-                codes=None, packed=None, scale=None, err_w=None, err_out=None, events=None, absmax_in=None):
+                codes=None, packed=None, scale=None, err_w=None, err_out=None, events=None, absmax_in=None,
+                scale_hint=None, fallback_out=None):
     """Fused Q update: quantise res = W - L R (W alone if L is None) per matrix, never
     materialising res.  W (B, m, n) fp16/fp32, L (B, m, r), R (B, r, n) fp32 with r % 32 == 0.
-    Fills packed (B, m*n*bits/8) uint8 and/or codes, scale (B,), err_out (B,) fp64."""
-    _require_hip(W, L, R, codes, packed, scale, err_w, err_out)
+    Fills packed (B, m*n*bits/8) uint8 and/or codes, scale (B,), err_out (B,) fp64.
+    scale_hint (B,) fp32 (may be `scale` itself): the previous Q update's scales -- 2-bit
+    packed codes are then produced with one recompute of L R (candidate lists, see
+    include/caldera_hip.h); fallback_out (B,) int32 reports matrices that needed the second."""
+    _require_hip(W, L, R, codes, packed, scale, err_w, err_out, scale_hint, fallback_out)
     assert W.is_contiguous()
     B, m, n = W.shape
     dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[W.dtype]
@@ -718,12 +724,13 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         inv = 1.0 / (sL * sR)
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
-    ws = workspace(lib.cq_q_update_workspace(m, n, B), dev)
+    # the candidate lists make this workspace ~m n / 2 bytes per matrix: cached (scratch.py)
+    ws = scratch.get("q_update.ws", (max(int(lib.cq_q_update_workspace(m, n, B)), 16),), torch.uint8, dev)
     if events is not None:  # HIP events around the quantise kernels only (bench roofline)
         events[0].record()
     _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),
                               _p(packed), _p(scale), _p(err_w), _p(err_out), _p(absmax_in if r == 0 else None),
-                              _p(ws), ws.numel(), _stream(dev)),
+                              _p(scale_hint if r else None), _p(fallback_out), _p(ws), ws.numel(), _stream(dev)),
            "cq_q_update_x3")
     if events is not None:
         events[1].record()

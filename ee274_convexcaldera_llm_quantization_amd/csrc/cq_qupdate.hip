@@ -29,6 +29,7 @@ namespace cq {
 constexpr int QP_WAVES = 8;               // default waves per workgroup (template parameter NW)
 constexpr int QP_WD = 5;                  // W ring slots (WL path)
 constexpr size_t QP_LDS_MAX = 156 * 1024;
+constexpr int QP_CBUF = 112;              // pass 2: a wave's LDS buffer of one chunk's candidates (8 B each)
 
 // LDS halves of one R^T stage (hi rows, then lo rows; RROW = 32 KSMAX halves per R^T row) and
 // of one W ring slot (NW waves x RB row blocks x 16 rows x 32 columns)
@@ -70,6 +71,17 @@ __device__ __forceinline__ f16x8g qp_frag(const _Float16* stage, int half, int r
     return *reinterpret_cast<const f16x8g*>(stage + (half * QP_BN + row) * RROW + 8 * (chunk ^ qp_swz(row)));
 }
 
+// The single-recompute path's completeness test for matrix b with scale s: every nonzero
+// 2-bit code needs |res| > s / 2, and the list holds every |res| >= tau, so the list is
+// complete when 2 tau <= s (exact), no wave's list overflowed, and the quotients take the
+// branch-free division (as pass 1 would).  Otherwise pass 1 recomputes the matrix.
+__device__ __forceinline__ bool qp_fallback(const QUK& q, int64_t b, float s) {
+    const float h = q.hint[b];
+    if (!(h > 0.f && h <= 0x1p127f)) return true;
+    const float tau = QP_TAU * h;
+    return q.ovf[b] != 0u || !div_fast_ok(s) || !(2.f * tau <= s);
+}
+
 // RB row-blocks of 16 rows per wave; K = r <= 32 KSMAX.  FAST (pass 1): the scale is a
 // finite normal number and |res| <= scale, so x / s and c / k take the branch-free correctly
 // rounded division (div_fast; same results as IEEE division), and 2-bit dequantisation is
@@ -81,8 +93,9 @@ __device__ __forceinline__ f16x8g qp_frag(const _Float16* stage, int half, int r
 template <int PASS, int BITS, int DT, int RB, int KSMAX, bool FAST, int NW, bool WL>
 __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict__ Lh, const uint16_t* __restrict__ Ll,
                                         const uint16_t* __restrict__ Rh, const uint16_t* __restrict__ Rl, int K,
-                                        int panels, _Float16* smem) {
+                                        int panels, _Float16* smem, int64_t orig) {
     static_assert(!WL || DT == CQ_F16, "the W ring carries fp16 W");
+    static_assert(PASS != 2 || (WL && BITS == 2), "the candidate pass runs on the W ring, 2-bit codes");
     constexpr int ROWS = NW * 16 * RB;
     constexpr int WV = DT == CQ_F16 ? 1 : 2;        // uint4 per lane-run of 8 W elements
     constexpr int RROW = 32 * KSMAX;                 // halves per R^T row in LDS
@@ -94,7 +107,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const int64_t m = q.m, n = q.n, MN = m * n;
     // XCD-aware order: the panels of one matrix run on one XCD (R^T chunks shared in its L2)
     const int64_t total = (int64_t)panels * q.x.batch;
-    const int64_t orig = blockIdx.x;
     const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
     const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
     const int64_t b = lin / panels, panel = lin % panels;
@@ -134,6 +146,19 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const float ys = 1.f / s, yk = 1.f / kq;
     uint32_t mx = 0;
     double err = 0.0;
+    // pass 2: candidate threshold (|res| >= tau as order-preserving bits; an invalid hint keeps
+    // only non-finite values and the matrix falls back), this wave's list region and cursor
+    uint32_t tb = 0x7f800000u;
+    if (PASS == 2) {
+        const float h = q.hint[b];
+        if (h > 0.f && h <= 0x1p127f) tb = abs_bits(QP_TAU * h);
+    }
+    const int64_t region = (b * panels + panel) * NW + wid;
+    uint2* lst = PASS == 2 ? q.list + region * q.cap : nullptr;
+    int64_t wcur = 0;   // entries this wave has listed
+    int ccnt = 0;       // entries of the current chunk staged in this wave's LDS buffer
+    uint2* cbuf = reinterpret_cast<uint2*>(reinterpret_cast<char*>(smem) + qp_lds_bytes(NW, RB, KSMAX, WL)) +
+                  wid * QP_CBUF;
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -216,12 +241,12 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     uint2 seg[RB][E];   // pass 1, 2-bit packed: a row's code bytes of the current GRP-chunk group
     // chunk ch's products and epilogue on W wc and R^T stage st; returns whether it issued
     // global stores (then only a full vmcnt drain is a safe wait)
-    // pass 0, K <= 128 (UPF): the chunk's R^T fragments (both halves, every K step: 64 VGPRs) are read
+    // passes 0 and 2, K <= 128 (UPF): the chunk's R^T fragments (both halves, every K step: 64 VGPRs) are read
     // from LDS once, behind one wait, and each row block's MFMAs are followed by its epilogue,
     // so the epilogue's VALU work of row block rb overlaps the MFMAs of rb + 1 (independent
     // registers) instead of waiting for all of them; the MFMA order per accumulator (K steps,
     // then al x lh, ah x ll, ah x lh) is the same as mma()'s, so the sums are bit-identical.
-    constexpr bool UPF = KSMAX <= 4 && PASS == 0;
+    constexpr bool UPF = KSMAX <= 4 && (PASS == 0 || PASS == 2);
     auto compute = [&](int64_t ch, const uint4 (&wc)[RB][WV], const _Float16* st) -> bool {
         const int64_t n0 = ch * QP_BN;
         bool stored = false;
@@ -264,6 +289,48 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             resid(wc, acc, rb, v);
             if (PASS == 0) {
                 mx = vmax(v, mx);
+                continue;
+            }
+            if constexpr (PASS == 2) {
+                // absmax, the error every element has with code 0 (d = 0 - x: the same fp32
+                // runs as pass 1's), and the candidates, stored after the chunk's wait (flush)
+                mx = vmax(v, mx);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    float e4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) e4[t] = v[4 * h + t] * v[4 * h + t];
+                    err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));
+                }
+                // the candidates go to the wave's LDS buffer in (row block, lane, element)
+                // order: a lane's slot from bit-sliced ballots of its count (<= 8), so the
+                // list order, hence every later sum, is deterministic; flush() copies the
+                // buffer to the list after the chunk's counted wait (a global store issued
+                // behind the newest W loads would leave only a full drain safe)
+                uint32_t fl = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) fl |= (uint32_t)(abs_bits(v[u]) >= tb) << u;
+                const int c = __builtin_popcount(fl);
+                int pre = 0, tot = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t mk = __ballot((c >> k) & 1);
+                    pre += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u)) << k;
+                    tot += __builtin_popcountll(mk) << k;
+                }
+                if (fl) {
+                    int pos = ccnt + pre;
+                    const uint32_t ib = (uint32_t)e;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if ((fl >> u) & 1u) {
+                            if (pos < QP_CBUF) cbuf[pos] = make_uint2(ib + u, __float_as_uint(v[u]));
+                            ++pos;
+                        }
+                    }
+                }
+                ccnt += tot;
                 continue;
             }
             float cf[8];   // codes (integral floats)
@@ -372,6 +439,15 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         }
         return stored;
     };
+    // pass 2: the chunk's staged candidates to this wave's list (coalesced 8-B stores); a chunk
+    // with more than QP_CBUF candidates counts as an overflow (the matrix falls back)
+    auto flush = [&]() {
+        const int nc = ccnt < QP_CBUF ? ccnt : QP_CBUF;
+        for (int i = lane; i < nc; i += 64)
+            if (wcur + i < q.cap) lst[wcur + i] = cbuf[i];
+        wcur += ccnt > QP_CBUF ? q.cap + 1 : ccnt;
+        ccnt = 0;
+    };
     // vmcnt(N) with expcnt / lgkmcnt at their maxima (not waited); vmcnt in bits [3:0], [15:14]
     auto wait_vm = [](auto n_c) {
         constexpr int nw = decltype(n_c)::value;
@@ -400,6 +476,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             // stay in flight); after stores only a full drain is safe
             if (!stored && wlive) wait_vm(std::integral_constant<int, RB>{});
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (PASS == 2) flush();
             __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
             sw = sw + 1 == QP_WD ? 0 : sw + 1;
         }
@@ -439,16 +516,27 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             }
         }
     }
-    if (PASS == 0) {
+    if (PASS == 0 || PASS == 2) {
         mx = wave_max_u32(mx);
         if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
-    } else if (q.part) {
+    }
+    if (PASS == 2) {
+        if (lane == 0) {
+            q.cnt[region] = (uint32_t)(wcur < q.cap ? wcur : q.cap + 1);
+            if (wcur > q.cap) q.ovf[b] = 1u;
+        }
+        __shared__ double red2[16];
+        const double tsum = block_sum_f64(err, red2);
+        if (tid == 0) q.part0[b * panels + panel] = tsum;
+    } else if (PASS == 1 && q.part) {
         __shared__ double red[16];
         const double tsum = block_sum_f64(err, red);
         if (tid == 0) q.part[b * panels + panel] = tsum;
     }
 }
 
+static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) + QP_WAVES * QP_CBUF * 8 + 256 <= 160 * 1024,
+              "pass 2: ring, stages and candidate buffers fit one CU's LDS");
 static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) <= QP_LDS_MAX && qp_lds_bytes(QP_WAVES, 2, 8, true) <= QP_LDS_MAX,
               "Q-update LDS: R^T stages + W ring fit one CU (160 KB, static reduction scratch aside)");
 
@@ -460,20 +548,131 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
                                                                    int panels) {
     extern __shared__ __attribute__((aligned(16))) char qp_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(qp_smem_raw);
-    if (PASS == 0) {
-        qp_body<PASS, BITS, DT, RB, KSMAX, false, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    if (PASS == 0 || PASS == 2) {
+        qp_body<PASS, BITS, DT, RB, KSMAX, false, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem, blockIdx.x);
         return;
     }
-    // which matrix this workgroup serves (same mapping as qp_body) decides the division path
+    // which matrix a panel serves (same mapping as qp_body) decides the division path.  The
+    // fallback launch of the list path is a grid of one workgroup per CU looping over the panels
+    // (gridDim a multiple of 8: a panel keeps its XCD), so that matrices that took the list
+    // path cost a check, not a dispatch of a 150-KB-LDS workgroup
     const int64_t total = (int64_t)panels * q.x.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
-    const float sb = quant_scale(q.absmax[lin / panels], q.eps);
-    if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem);
-    else qp_body<PASS, BITS, DT, RB, KSMAX, false, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem);
+    for (int64_t orig = blockIdx.x; orig < total; orig += gridDim.x) {
+        const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
+        const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
+        const float sb = quant_scale(q.absmax[lin / panels], q.eps);
+        if (q.only_fallback && !qp_fallback(q, lin / panels, sb)) continue;   // codes came from the list
+        if (div_fast_ok(sb)) qp_body<PASS, BITS, DT, RB, KSMAX, true, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem, orig);
+        else qp_body<PASS, BITS, DT, RB, KSMAX, false, NW, WL>(q, Lh, Ll, Rh, Rl, K, panels, smem, orig);
+    }
 }
 
+
+// ------------------------------------------------------------------ list path: codes + error
+// One workgroup per wave region of pass 2 (rpw rows x n): the region's packed 2-bit codes are
+// built in LDS (all code 0 = offset-binary 01, then each nonzero candidate's 2 bits flipped by
+// an LDS xor: 01 -> 10 for c = 1, 01 -> 00 for c = -1) and stored whole; the error correction
+// of a nonzero code, (c s - x)^2 - x^2, with pass 1's fp32 arithmetic, summed in fp64 in list
+// order (deterministic).  Codes: the same quotient as pass 1 (div_fast of the same residual).
+__global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw, int rpw) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t qc_lds[];
+    const int64_t region = blockIdx.x;
+    const int64_t b = region / ((int64_t)panels * nw);
+    const int64_t rem = region % ((int64_t)panels * nw);
+    const int64_t r0 = (rem / nw) * (int64_t)nw * rpw + (rem % nw) * (int64_t)rpw;
+    const float s = quant_scale(q.absmax[b], q.eps);
+    if (qp_fallback(q, b, s)) return;   // pass 1 writes this matrix's codes and errors
+    const int tid = threadIdx.x;
+    const int64_t m = q.m, n = q.n;
+    const int64_t nr = r0 < m ? (m - r0 < rpw ? m - r0 : rpw) : 0;
+    __shared__ double red[16];
+    double delta = 0.0;
+    if (nr > 0) {
+        const int64_t words = nr * n / 16;   // 16 codes per 32-bit word
+        for (int64_t i = tid; i < words; i += 256) qc_lds[i] = 0x55555555u;
+        __syncthreads();
+        const float ys = 1.f / s;
+        const int64_t cnt = q.cnt[region];
+        const uint2* lst = q.list + region * q.cap;
+        const int64_t base = r0 * n;
+        for (int64_t i = tid; i < cnt; i += 256) {
+            const uint2 en = lst[i];
+            const float x = __uint_as_float(en.y);
+            const float qd = x * ys;
+            const float rr = __builtin_fmaf(-qd, s, x);
+            const float c = rintf(__builtin_fmaf(rr, ys, qd) * 1.f);
+            if (c != 0.f) {
+                const int64_t loc = (int64_t)en.x - base;
+                // element loc: byte loc / 4 (bits 6 - 2 (loc % 4), MSB-first) of word loc / 16
+                const uint32_t sh = 8u * (uint32_t)((loc >> 2) & 3) + 6u - 2u * (uint32_t)(loc & 3);
+                atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
+                const float d = c * s - x;
+                delta += (double)(d * d) - (double)(x * x);
+            }
+        }
+        __syncthreads();
+        uint32_t* dst = reinterpret_cast<uint32_t*>(q.packed + (b * m * n + base) / 4);
+        for (int64_t i = tid; i < words; i += 256) dst[i] = qc_lds[i];
+    }
+    const double t = block_sum_f64(delta, red);
+    if (tid == 0) q.partF[region] = t;
+}
+
+// scale, error and fallback flag per matrix of the list path: pass-2 partials + the code
+// kernel's corrections, or pass 1's partials where the matrix fell back (fixed order)
+__global__ void qp_finalize_cand_kernel(QUK q, int panels, int nw, float* scale, double* err_out) {
+    const int64_t b = blockIdx.x;
+    const float s = quant_scale(q.absmax[b], q.eps);
+    const bool fb = qp_fallback(q, b, s);
+    double acc = 0.0;
+    if (fb) {
+        for (int t = threadIdx.x; t < panels; t += 64) acc += q.part[b * panels + t];
+    } else {
+        for (int t = threadIdx.x; t < panels; t += 64) acc += q.part0[b * panels + t];
+        for (int t = threadIdx.x; t < panels * nw; t += 64) acc += q.partF[(b * panels) * nw + t];
+    }
+    acc = wave_sum(acc);
+    if (threadIdx.x == 0) {
+        if (scale) scale[b] = s;
+        if (err_out) err_out[b] = acc;
+        if (q.fb_out) q.fb_out[b] = fb ? 1 : 0;
+    }
+}
+
+int qp_cand_rows(int K) { return 16 * (K <= 128 ? 3 : 2); }
+
+bool qp_cand_ok(int64_t m, int64_t n, int K) {
+    // the code kernel holds a wave region's packed codes (rows x n / 4 bytes) in LDS
+    return K > 0 && K <= QP_KMAX && m % 16 == 0 && n % QP_BN == 0 && m * n < (1ll << 31) &&
+           (int64_t)qp_cand_rows(K) * n / 4 <= 144 * 1024;
+}
+
+int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
+                       int K, int64_t batch, float eps, float* scale_out, double* err_out, hipStream_t s) {
+    const int64_t m = q.m, n = q.n;
+    const bool small = K <= 128;
+    const int rb = small ? 3 : 2;
+    const int64_t panels = ceil_div(m, (int64_t)QP_WAVES * 16 * rb);
+    if (panels * batch * QP_WAVES >= (1ll << 31)) return -1;
+    const unsigned g = (unsigned)(panels * batch);
+    const unsigned gf = (unsigned)std::min<int64_t>(panels * batch, kCUs);   // fallback pass 1
+    const int rpw = 16 * rb;
+    const size_t lds = (size_t)rpw * n / 4;
+    q.only_fallback = 0;
+#define CQ_QPC(PS, RBV, KSV)                                                               \
+    q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, QP_WAVES, true><<<PS == 2 ? g : gf, QP_WAVES * 64, \
+        qp_lds_bytes(QP_WAVES, RBV, KSV, true) + (PS == 2 ? QP_WAVES * QP_CBUF * 8 : 0), s>>>(  \
+        q, Lh, Ll, Rth, Rtl, K, (int)panels)
+    if (small) CQ_QPC(2, 3, 4); else CQ_QPC(2, 2, 8);
+    qp_codes_kernel<<<(unsigned)(panels * batch * QP_WAVES), 256, lds, s>>>(q, (int)panels, QP_WAVES, rpw);
+    q.only_fallback = 1;
+    if (small) CQ_QPC(1, 3, 4); else CQ_QPC(1, 2, 8);
+#undef CQ_QPC
+    q.only_fallback = 0;
+    qp_finalize_cand_kernel<<<(unsigned)batch, 64, 0, s>>>(q, (int)panels, QP_WAVES, scale_out, err_out);
+    (void)eps;
+    return panels;
+}
 
 int64_t qp_launch(QUK& q, int dtype, int bits, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth,
                   const uint16_t* Rtl, int K, int64_t batch, hipStream_t s) {

@@ -50,7 +50,23 @@ struct QUK {
     float* scale;                // [batch] out (pass 1)
     const float* ew;             // error column weights [n] or NULL (= 1)
     double* part;                // [batch * tiles] error partials
+    // single-recompute 2-bit path (qp_launch cand = true): pass 2 = pass 0 + the error of
+    // all-zero codes + a list of the candidates |res| >= tau (tau = QP_TAU x the previous
+    // scale); qp_codes_kernel writes the codes from the lists; pass 1 runs only for matrices
+    // whose lists cannot be complete (qp_fallback)
+    const float* hint;           // [batch] previous Q scale (candidate threshold), or NULL
+    uint32_t* ovf;               // [batch] a wave's list overflowed (zeroed before pass 2)
+    uint32_t* cnt;               // [batch * panels * waves] list entries per wave region
+    uint2* list;                 // [batch * panels * waves * cap] (element index, res bits)
+    int64_t cap;                 // entries per wave region
+    double* part0;               // [batch * panels] pass-2 error partials (all codes zero)
+    double* partF;               // [batch * panels * waves] code-kernel error corrections
+    int only_fallback;           // pass 1: skip matrices that took the list path
+    int* fb_out;                 // [batch] 1 = took the two-pass fallback, or NULL
 };
+
+constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
+constexpr int QP_CAP_DIV = 16;            // list capacity: 1 / 16 of a wave region's elements
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
 constexpr int QP_KMAX = 256;              // row-panel Q update: largest r
@@ -60,5 +76,14 @@ constexpr int QP_KMAX = 256;              // row-panel Q update: largest r
 // the pass-1 panels.  Returns the number of pass-1 panels per matrix (the error partials).
 int64_t qp_launch(QUK& q, int dtype, int bits, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth,
                   const uint16_t* Rtl, int K, int64_t batch, hipStream_t s);
+// The single-recompute 2-bit path's geometry (rows per wave) and whether it applies: fp16 W,
+// K <= 256, no error weights, a wave region's packed codes fit the code kernel's LDS.
+int qp_cand_rows(int K);
+bool qp_cand_ok(int64_t m, int64_t n, int K);
+// Launches pass 2, the code kernel, the fallback pass 1 and the finalize (scale, error,
+// fallback flags); q.ovf / q.absmax zeroed, q.list / q.cnt / q.part0 / q.partF sized by
+// qp_cand_ws.  Returns the panels per matrix, or -1 when the grid is too large.
+int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
+                       int K, int64_t batch, float eps, float* scale_out, double* err_out, hipStream_t s);
 
 }  // namespace cq

@@ -1312,18 +1312,35 @@ static int64_t qu_tiles(int64_t m, int64_t n) {
     return std::max(ceil_div(n, XW_BM) * ceil_div(m, XW_BN), ceil_div(m, XW_BM) * ceil_div(n, XW_BN));
 }
 
+// the single-recompute 2-bit path's buffers (qp_launch_cand) for the larger of its two
+// geometries (rows per wave 32 or 48): overflow flags | counts | pass-2 partials |
+// corrections | lists (1 / QP_CAP_DIV of the elements plus a region of rounding)
+static size_t qu_cand_bytes(int64_t m, int64_t n, int64_t batch, int64_t* regions_out, int64_t* cap_out) {
+    int64_t regions = 0, cap = 0;
+    for (int rpw : {32, 48}) {
+        regions = std::max(regions, ceil_div(m, (int64_t)rpw * 8) * 8);
+        cap = std::max(cap, ceil_div((int64_t)rpw * n, QP_CAP_DIV));
+    }
+    if (regions_out) *regions_out = regions;
+    if (cap_out) *cap_out = cap;
+    return align_up((size_t)batch * 4, 256) + align_up((size_t)batch * regions * 4, 256) +
+           align_up((size_t)batch * regions * 8, 256) * 2 + (size_t)batch * regions * cap * 8;
+}
+
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
     // tile counts of both Q-update kernels (q_update_v_kernel tiles W as m x n, the 32x32
     // kernel as n x m)
     const int64_t tiles = qu_tiles(m, n);
-    // absmax bits | error partials
-    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) + (size_t)batch * tiles * sizeof(double);
+    // absmax bits | error partials | list path
+    return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) +
+           align_up((size_t)batch * tiles * sizeof(double), 256) + qu_cand_bytes(m, n, batch, nullptr, nullptr);
 }
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
                    const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl, const float* inv_scale, int bits,
                    float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w, double* err_out,
-                   const float* absmax_in, void* ws, size_t ws_bytes, void* stream) {
+                   const float* absmax_in, const float* scale_hint, int* fallback_out, void* ws, size_t ws_bytes,
+                   void* stream) {
     CQ_REQUIRE(W && m > 0 && n > 0 && batch > 0 && r >= 0, "cq_q_update_x3: bad shape");
     CQ_REQUIRE(dtype == CQ_F16 || dtype == CQ_F32, "cq_q_update_x3: dtype must be f16/f32");
     if (bits != 2 && bits != 4 && bits != 8 && bits != 16) return set_error(CQ_EINVAL, "Bit-width not supported!");
@@ -1335,7 +1352,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     if (!ws || ws_bytes < cq_q_update_workspace(m, n, batch)) return set_error(CQ_EWORKSPACE, "cq_q_update_x3: workspace too small");
     QUK q;
     X3K& a = q.x;
-    memset(&a, 0, sizeof(a));  // a_blocked = b_blocked = 0, no active mask
+    memset(&q, 0, sizeof(q));  // a_blocked = b_blocked = 0, no active mask, no list path
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool vk = n % 16 == 0 && al16(W) && (!codes || al16(codes)) && (!packed || al16(packed)) &&
                     (!err_w || al16(err_w));
@@ -1380,6 +1397,30 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     // row-panel kernel (q_update_p_kernel): K <= 256, m % 16 == 0, n % 32 == 0, 16-B aligned
     const bool pk = r > 0 && r <= QP_KMAX && m % 16 == 0 && n % QP_BN == 0 && vk && al16(Lh) && al16(Ll) &&
                     al16(Rth) && al16(Rtl);
+    // single recompute (2-bit packed codes, fp16 W, unit error weights, previous scale given):
+    // pass 2 + candidate lists + code kernel, pass 1 only where a list cannot be complete
+    if (pk && !known && scale_hint && bits == 2 && packed && !codes && !err_w && dtype == CQ_F16 &&
+        qp_cand_ok(m, n, (int)r)) {
+        int64_t regions = 0, cap = 0;
+        qu_cand_bytes(m, n, batch, &regions, &cap);
+        char* c = reinterpret_cast<char*>(q.part) + align_up((size_t)batch * tiles * sizeof(double), 256);
+        q.ovf = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * 4, 256);
+        q.cnt = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * 4, 256);
+        q.part0 = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
+        q.partF = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
+        q.list = reinterpret_cast<uint2*>(c);
+        q.cap = cap;
+        q.hint = scale_hint;
+        q.fb_out = fallback_out;
+        q.x.batch = batch;
+        if (hipMemsetAsync(q.ovf, 0, batch * sizeof(uint32_t), s) != hipSuccess)
+            return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
+        if (qp_launch_cand(q, Lh, Ll, Rth, Rtl, (int)r, batch, eps, scale_out, err_out, s) < 0)
+            return set_error(CQ_EINVAL, "cq_q_update_x3: grid too large");
+        return check_launch("cq_q_update_x3");
+    }
+    if (fallback_out && hipMemsetAsync(fallback_out, 0, batch * sizeof(int), s) != hipSuccess)
+        return set_error(CQ_EHIP, "cq_q_update_x3: memset failed");
     if (pk && !known) {
         q.x.batch = batch;
         const int64_t p1 = qp_launch(q, dtype, bits, Lh, Ll, Rth, Rtl, (int)r, batch, s);

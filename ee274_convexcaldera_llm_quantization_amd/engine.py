@@ -243,6 +243,8 @@ class CalderaEngine:
         self.profile = profile
         self.timings = {}
         self.solver = None
+        self._qfb = None  # (B,) int32 on the device: Q updates that took the second L R recompute
+        self.q_single_recompute = True  # 2-bit Q updates: one L R recompute + candidate lists
         self.lplr_fused_err = True   # LPLR error from the normal-equation pieces (False: error GEMM)
         self.lplr_x3 = True          # LPLR m x n x r products on split-fp16 MFMAs where the halves exist
         self.sparse_gram = True      # G from the sparse 2-bit codes where it applies (sgram.py)
@@ -250,6 +252,12 @@ class CalderaEngine:
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
                 raise NotImplementedError(f"Quantization method '{meth}' not supported yet.")
+
+    @property
+    def q_fallbacks(self) -> int:
+        """Q updates (summed over the batch) whose candidate list could not be complete, so
+        that L R was recomputed a second time (cq_q_update_x3); reads the device counter."""
+        return 0 if self._qfb is None else int(self._qfb.sum().item())
 
     # ------------------------------------------------------------------ pieces
     def _q_update(self, st: BatchState, Ws, res_buf, wts: _Weights, den):
@@ -272,8 +280,19 @@ class CalderaEngine:
             amax = self._wmax if not Kdim else None
             ew = None if wts.err_unit else wts.err  # unit weights: the same sums without the loads
             if st.q_packed:
+                # the previous scale (st.Qs, rewritten by this call) lets a 2-bit update
+                # recompute L R once (candidate lists; cq_q_update_x3); the per-matrix count of
+                # second recomputes is accumulated on the device (q_fallbacks)
+                hint = st.Qs if (Kdim and st.has_Q and self.q_single_recompute) else None
+                fb = None
+                if hint is not None:
+                    if self._qfb is None or self._qfb.numel() != B:
+                        self._qfb = torch.zeros(B, dtype=torch.int32, device=Ws.device)
+                    fb = torch.empty(B, dtype=torch.int32, device=Ws.device)
                 K.q_update_x3(Ws, Lm, Rm, p.Q_bits, packed=st.Qc, scale=st.Qs, err_w=ew, err_out=err, events=ev,
-                              absmax_in=amax)
+                              absmax_in=amax, scale_hint=hint, fallback_out=fb)
+                if fb is not None:
+                    self._qfb += fb
             else:
                 K.q_update_x3(Ws, Lm, Rm, p.Q_bits, codes=st.Qc, scale=st.Qs, err_w=ew, err_out=err, events=ev,
                               absmax_in=amax)

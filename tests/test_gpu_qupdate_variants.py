@@ -28,3 +28,59 @@ def test_q_update_matches_round2_kernel(case):
     assert got["packed_sha256"] == ref["packed_sha256"]
     assert got["scale"] == ref["scale"]
     assert got["err"] == ref["err"]
+
+
+LIST_CASES = [c for c in C.CASES if c[5] == 2 and c[6] == torch.float16]
+
+
+@pytest.mark.parametrize("case", LIST_CASES, ids=[c[0] for c in LIST_CASES])
+def test_q_update_single_recompute_matches_two_pass(case):
+    """The 2-bit single-recompute path (scale_hint given: one L R recompute, candidate lists
+    |res| >= 0.45 hint, codes from the lists) gives the two-pass kernel's packed codes and
+    scales bit for bit and its error sums to 1e-9 relative (the same fp32 terms, but a
+    candidate's term is summed in fp32 inside its run of 4 by pass 1 and alone in fp64 by the
+    list path: ~1e-10 measured); matrices whose list cannot be
+    complete (scale < 0.9 hint, an overflowing list, a non-finite hint) take pass 1 and give
+    the two-pass outputs exactly.  Mixed batches exercise both in one call, and the hint may
+    alias the scale output (the engine's use: st.Qs is both)."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    tag, B, m, n, r, bits, dt = case
+    dev = torch.device("cuda:0")
+    W, L, R = C.make(B, m, n, r, dt, seed=sum(map(ord, tag)) + 7)
+    W, L, R = W.to(dev), L.to(dev), R.to(dev)
+
+    def call(hint, alias=False):
+        packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=dev)
+        err = torch.empty(B, dtype=torch.float64, device=dev)
+        fb = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        if alias and hint is not None:
+            scale = hint.clone()
+            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=scale, fallback_out=fb)
+        else:
+            scale = torch.empty(B, device=dev)
+            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=hint, fallback_out=fb)
+        torch.cuda.synchronize()
+        return packed.cpu(), scale.cpu(), err.cpu(), fb.cpu()
+
+    p0, s0, e0, f0 = call(None)
+    assert (f0 == 0).all()
+    s = s0.to(dev)
+    variants = {
+        "exact": (s, [0] * B),
+        "hint 5% high": (s * 1.05, [0] * B),
+        "hint 20% high": (s * 1.2, [1] * B),            # 2 tau = 1.08 s > s: list incomplete
+        "hint 1e-3": (s * 1e-3, [1] * B),               # every element a candidate: overflow
+        "hint nan": (torch.full_like(s, float("nan")), [1] * B),
+        "mixed": (torch.stack([s[i] * (1.2 if i % 2 else 1.0) for i in range(B)]), [i % 2 for i in range(B)]),
+    }
+    for name, (hint, want_fb) in variants.items():
+        for alias in (False, True):
+            p, sc, e, fb = call(hint, alias)
+            assert fb.tolist() == want_fb, (name, fb.tolist())
+            assert torch.equal(p, p0), (name, alias, int((p != p0).sum()))
+            assert torch.equal(sc, s0), name
+            for i in range(B):
+                if want_fb[i]:
+                    assert e[i].item() == e0[i].item(), (name, i)
+                else:
+                    assert abs(e[i].item() - e0[i].item()) <= 1e-9 * e0[i].item(), (name, i, e[i].item(), e0[i].item())
