@@ -115,7 +115,7 @@ _SIGS = {
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
-    "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64]),
+    "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64, c_int]),
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
@@ -725,7 +725,9 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
     # the candidate lists make this workspace ~m n / 2 bytes per matrix: cached (scratch.py)
-    ws = scratch.get("q_update.ws", (max(int(lib.cq_q_update_workspace(m, n, B)), 16),), torch.uint8, dev)
+    hint = scale_hint is not None and r > 0
+    ws = scratch.get("q_update.ws_list" if hint else "q_update.ws",
+                     (max(int(lib.cq_q_update_workspace(m, n, B, int(hint))), 16),), torch.uint8, dev)
     if events is not None:  # HIP events around the quantise kernels only (bench roofline)
         events[0].record()
     _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),

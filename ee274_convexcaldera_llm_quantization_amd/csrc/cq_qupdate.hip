@@ -29,7 +29,6 @@ namespace cq {
 constexpr int QP_WAVES = 8;               // default waves per workgroup (template parameter NW)
 constexpr int QP_WD = 5;                  // W ring slots (WL path)
 constexpr size_t QP_LDS_MAX = 156 * 1024;
-constexpr int QP_CBUF = 112;              // pass 2: a wave's LDS buffer of one chunk's candidates (8 B each)
 
 // LDS halves of one R^T stage (hi rows, then lo rows; RROW = 32 KSMAX halves per R^T row) and
 // of one W ring slot (NW waves x RB row blocks x 16 rows x 32 columns)
@@ -147,18 +146,14 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     uint32_t mx = 0;
     double err = 0.0;
     // pass 2: candidate threshold (|res| >= tau as order-preserving bits; an invalid hint keeps
-    // only non-finite values and the matrix falls back), this wave's list region and cursor
+    // only non-finite values and the matrix falls back) and this wave's list region
     uint32_t tb = 0x7f800000u;
     if (PASS == 2) {
         const float h = q.hint[b];
         if (h > 0.f && h <= 0x1p127f) tb = abs_bits(QP_TAU * h);
     }
     const int64_t region = (b * panels + panel) * NW + wid;
-    uint2* lst = PASS == 2 ? q.list + region * q.cap : nullptr;
-    int64_t wcur = 0;   // entries this wave has listed
-    int ccnt = 0;       // entries of the current chunk staged in this wave's LDS buffer
-    uint2* cbuf = reinterpret_cast<uint2*>(reinterpret_cast<char*>(smem) + qp_lds_bytes(NW, RB, KSMAX, WL)) +
-                  wid * QP_CBUF;
+    int64_t gcur = 0;   // pass 2: groups this wave has listed
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -292,45 +287,37 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 continue;
             }
             if constexpr (PASS == 2) {
-                // absmax, the error every element has with code 0 (d = 0 - x: the same fp32
-                // runs as pass 1's), and the candidates, stored after the chunk's wait (flush)
-                mx = vmax(v, mx);
+                // absmax; the error every element has with code 0 (d = 0 - x; fp32 over the
+                // lane's 8 elements, fp64 across); and, where any of the lane's 8 elements has
+                // |res| >= tau, the whole group of 8 residuals to this wave's list (slot from
+                // one ballot: the list order, hence every later sum, is deterministic).  The
+                // stores are followed by a full drain at the chunk's end (compute() returns
+                // true), a wait that costs little next to a chunk's ~4 us of MFMA work.
+                uint32_t lm = 0u;
+                float e8 = 0.f;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    float e4[4];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) e4[t] = v[4 * h + t] * v[4 * h + t];
-                    err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));
+                for (int u = 0; u < 8; ++u) {
+                    lm = max(lm, abs_bits(v[u]));
+                    e8 = __builtin_fmaf(v[u], v[u], e8);
                 }
-                // the candidates go to the wave's LDS buffer in (row block, lane, element)
-                // order: a lane's slot from bit-sliced ballots of its count (<= 8), so the
-                // list order, hence every later sum, is deterministic; flush() copies the
-                // buffer to the list after the chunk's counted wait (a global store issued
-                // behind the newest W loads would leave only a full drain safe)
-                uint32_t fl = 0;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) fl |= (uint32_t)(abs_bits(v[u]) >= tb) << u;
-                const int c = __builtin_popcount(fl);
-                int pre = 0, tot = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint64_t mk = __ballot((c >> k) & 1);
-                    pre += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u)) << k;
-                    tot += __builtin_popcountll(mk) << k;
-                }
-                if (fl) {
-                    int pos = ccnt + pre;
-                    const uint32_t ib = (uint32_t)e;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if ((fl >> u) & 1u) {
-                            if (pos < QP_CBUF) cbuf[pos] = make_uint2(ib + u, __float_as_uint(v[u]));
-                            ++pos;
+                mx = max(mx, lm);
+                err += (double)e8;
+                const bool cand = lm >= tb;
+                const uint64_t mk = __ballot(cand);
+                if (mk) {
+                    stored = true;
+                    if (cand) {
+                        const int64_t pos = gcur + (int64_t)__builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                        if (pos < q.cap) {
+                            float4* dv = q.gval + 2 * (region * q.cap + pos);
+                            dv[0] = make_float4(v[0], v[1], v[2], v[3]);
+                            dv[1] = make_float4(v[4], v[5], v[6], v[7]);
+                            q.gid[region * q.cap + pos] = (uint32_t)e;
                         }
                     }
+                    gcur += __builtin_popcountll(mk);
                 }
-                ccnt += tot;
                 continue;
             }
             float cf[8];   // codes (integral floats)
@@ -439,15 +426,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         }
         return stored;
     };
-    // pass 2: the chunk's staged candidates to this wave's list (coalesced 8-B stores); a chunk
-    // with more than QP_CBUF candidates counts as an overflow (the matrix falls back)
-    auto flush = [&]() {
-        const int nc = ccnt < QP_CBUF ? ccnt : QP_CBUF;
-        for (int i = lane; i < nc; i += 64)
-            if (wcur + i < q.cap) lst[wcur + i] = cbuf[i];
-        wcur += ccnt > QP_CBUF ? q.cap + 1 : ccnt;
-        ccnt = 0;
-    };
     // vmcnt(N) with expcnt / lgkmcnt at their maxima (not waited); vmcnt in bits [3:0], [15:14]
     auto wait_vm = [](auto n_c) {
         constexpr int nw = decltype(n_c)::value;
@@ -476,7 +454,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             // stay in flight); after stores only a full drain is safe
             if (!stored && wlive) wait_vm(std::integral_constant<int, RB>{});
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr (PASS == 2) flush();
             __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
             sw = sw + 1 == QP_WD ? 0 : sw + 1;
         }
@@ -522,8 +499,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
     if (PASS == 2) {
         if (lane == 0) {
-            q.cnt[region] = (uint32_t)(wcur < q.cap ? wcur : q.cap + 1);
-            if (wcur > q.cap) q.ovf[b] = 1u;
+            q.cnt[region] = (uint32_t)(gcur < q.cap ? gcur : q.cap + 1);
+            if (gcur > q.cap) q.ovf[b] = 1u;
         }
         __shared__ double red2[16];
         const double tsum = block_sum_f64(err, red2);
@@ -535,8 +512,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
 }
 
-static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) + QP_WAVES * QP_CBUF * 8 + 256 <= 160 * 1024,
-              "pass 2: ring, stages and candidate buffers fit one CU's LDS");
 static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) <= QP_LDS_MAX && qp_lds_bytes(QP_WAVES, 2, 8, true) <= QP_LDS_MAX,
               "Q-update LDS: R^T stages + W ring fit one CU (160 KB, static reduction scratch aside)");
 
@@ -570,8 +545,8 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
 
 // ------------------------------------------------------------------ list path: codes + error
 // One workgroup per wave region of pass 2 (rpw rows x n): the region's packed 2-bit codes are
-// built in LDS (all code 0 = offset-binary 01, then each nonzero candidate's 2 bits flipped by
-// an LDS xor: 01 -> 10 for c = 1, 01 -> 00 for c = -1) and stored whole; the error correction
+// built in LDS (all code 0 = offset-binary 01, then each nonzero code of a listed group flips
+// its 2 bits by an LDS xor: 01 -> 10 for c = 1, 01 -> 00 for c = -1) and stored whole; the error correction
 // of a nonzero code, (c s - x)^2 - x^2, with pass 1's fp32 arithmetic, summed in fp64 in list
 // order (deterministic).  Codes: the same quotient as pass 1 (div_fast of the same residual).
 __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw, int rpw) {
@@ -593,21 +568,27 @@ __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw
         __syncthreads();
         const float ys = 1.f / s;
         const int64_t cnt = q.cnt[region];
-        const uint2* lst = q.list + region * q.cap;
+        const uint32_t* gid = q.gid + region * q.cap;
+        const float4* gv = q.gval + 2 * region * q.cap;
         const int64_t base = r0 * n;
         for (int64_t i = tid; i < cnt; i += 256) {
-            const uint2 en = lst[i];
-            const float x = __uint_as_float(en.y);
-            const float qd = x * ys;
-            const float rr = __builtin_fmaf(-qd, s, x);
-            const float c = rintf(__builtin_fmaf(rr, ys, qd) * 1.f);
-            if (c != 0.f) {
-                const int64_t loc = (int64_t)en.x - base;
-                // element loc: byte loc / 4 (bits 6 - 2 (loc % 4), MSB-first) of word loc / 16
-                const uint32_t sh = 8u * (uint32_t)((loc >> 2) & 3) + 6u - 2u * (uint32_t)(loc & 3);
-                atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
-                const float d = c * s - x;
-                delta += (double)(d * d) - (double)(x * x);
+            const float4 v0 = gv[2 * i], v1 = gv[2 * i + 1];
+            const float xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            const int64_t loc0 = (int64_t)gid[i] - base;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float x = xs[u];
+                const float qd = x * ys;
+                const float rr = __builtin_fmaf(-qd, s, x);
+                const float c = rintf(__builtin_fmaf(rr, ys, qd) * 1.f);
+                if (c != 0.f) {
+                    const int64_t loc = loc0 + u;
+                    // element loc: byte loc / 4 (bits 6 - 2 (loc % 4), MSB-first) of word loc / 16
+                    const uint32_t sh = 8u * (uint32_t)((loc >> 2) & 3) + 6u - 2u * (uint32_t)(loc & 3);
+                    atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
+                    const float d = c * s - x;
+                    delta += (double)(d * d) - (double)(x * x);
+                }
             }
         }
         __syncthreads();
@@ -661,7 +642,7 @@ int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uin
     q.only_fallback = 0;
 #define CQ_QPC(PS, RBV, KSV)                                                               \
     q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, QP_WAVES, true><<<PS == 2 ? g : gf, QP_WAVES * 64, \
-        qp_lds_bytes(QP_WAVES, RBV, KSV, true) + (PS == 2 ? QP_WAVES * QP_CBUF * 8 : 0), s>>>(  \
+        qp_lds_bytes(QP_WAVES, RBV, KSV, true), s>>>(                                              \
         q, Lh, Ll, Rth, Rtl, K, (int)panels)
     if (small) CQ_QPC(2, 3, 4); else CQ_QPC(2, 2, 8);
     qp_codes_kernel<<<(unsigned)(panels * batch * QP_WAVES), 256, lds, s>>>(q, (int)panels, QP_WAVES, rpw);

@@ -56,9 +56,10 @@ struct QUK {
     // whose lists cannot be complete (qp_fallback)
     const float* hint;           // [batch] previous Q scale (candidate threshold), or NULL
     uint32_t* ovf;               // [batch] a wave's list overflowed (zeroed before pass 2)
-    uint32_t* cnt;               // [batch * panels * waves] list entries per wave region
-    uint2* list;                 // [batch * panels * waves * cap] (element index, res bits)
-    int64_t cap;                 // entries per wave region
+    uint32_t* cnt;               // [batch * panels * waves] listed groups per wave region
+    uint32_t* gid;               // [batch * panels * waves * cap] first element index of a group
+    float4* gval;                // [.. * cap * 2] the group's 8 residuals (any |res| >= tau)
+    int64_t cap;                 // groups per wave region
     double* part0;               // [batch * panels] pass-2 error partials (all codes zero)
     double* partF;               // [batch * panels * waves] code-kernel error corrections
     int only_fallback;           // pass 1: skip matrices that took the list path
@@ -66,7 +67,7 @@ struct QUK {
 };
 
 constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
-constexpr int QP_CAP_DIV = 16;            // list capacity: 1 / 16 of a wave region's elements
+constexpr int QP_CAP_DIV = 2;             // list capacity: 1 / 2 of a wave region's 8-element groups
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
 constexpr int QP_KMAX = 256;              // row-panel Q update: largest r

@@ -1314,26 +1314,27 @@ static int64_t qu_tiles(int64_t m, int64_t n) {
 
 // the single-recompute 2-bit path's buffers (qp_launch_cand) for the larger of its two
 // geometries (rows per wave 32 or 48): overflow flags | counts | pass-2 partials |
-// corrections | lists (1 / QP_CAP_DIV of the elements plus a region of rounding)
-static size_t qu_cand_bytes(int64_t m, int64_t n, int64_t batch, int64_t* regions_out, int64_t* cap_out) {
-    int64_t regions = 0, cap = 0;
-    for (int rpw : {32, 48}) {
-        regions = std::max(regions, ceil_div(m, (int64_t)rpw * 8) * 8);
-        cap = std::max(cap, ceil_div((int64_t)rpw * n, QP_CAP_DIV));
-    }
+// corrections | group ids | group residuals (1 / QP_CAP_DIV of a region's 8-element groups)
+static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int64_t* regions_out, int64_t* cap_out) {
+    const int64_t regions = ceil_div(m, (int64_t)rpw * 8) * 8, cap = ceil_div((int64_t)rpw * n / 8, QP_CAP_DIV);
     if (regions_out) *regions_out = regions;
     if (cap_out) *cap_out = cap;
     return align_up((size_t)batch * 4, 256) + align_up((size_t)batch * regions * 4, 256) +
-           align_up((size_t)batch * regions * 8, 256) * 2 + (size_t)batch * regions * cap * 8;
+           align_up((size_t)batch * regions * 8, 256) * 2 + align_up((size_t)batch * regions * cap * 4, 256) +
+           (size_t)batch * regions * cap * 32;
+}
+static size_t qu_cand_bytes(int64_t m, int64_t n, int64_t batch) {
+    return std::max(qu_cand_geom(m, n, batch, 32, nullptr, nullptr), qu_cand_geom(m, n, batch, 48, nullptr, nullptr));
 }
 
-size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch) {
+size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint) {
     // tile counts of both Q-update kernels (q_update_v_kernel tiles W as m x n, the 32x32
     // kernel as n x m)
     const int64_t tiles = qu_tiles(m, n);
-    // absmax bits | error partials | list path
+    // absmax bits | error partials | list path (only when a scale hint will be passed)
     return (size_t)align_up((size_t)batch * sizeof(uint32_t), 256) +
-           align_up((size_t)batch * tiles * sizeof(double), 256) + qu_cand_bytes(m, n, batch, nullptr, nullptr);
+           align_up((size_t)batch * tiles * sizeof(double), 256) +
+           (with_hint ? qu_cand_bytes(m, n, batch) : 0);
 }
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
@@ -1349,7 +1350,8 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     CQ_REQUIRE(n % 4 == 0, "cq_q_update_x3: n must be a multiple of 4");
     CQ_REQUIRE(!packed || bits <= 4, "cq_q_update_x3: packing needs bits <= 4");
     CQ_REQUIRE(codes || packed, "cq_q_update_x3: no code output");
-    if (!ws || ws_bytes < cq_q_update_workspace(m, n, batch)) return set_error(CQ_EWORKSPACE, "cq_q_update_x3: workspace too small");
+    if (!ws || ws_bytes < cq_q_update_workspace(m, n, batch, scale_hint != nullptr))
+        return set_error(CQ_EWORKSPACE, "cq_q_update_x3: workspace too small");
     QUK q;
     X3K& a = q.x;
     memset(&q, 0, sizeof(q));  // a_blocked = b_blocked = 0, no active mask, no list path
@@ -1402,13 +1404,14 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     if (pk && !known && scale_hint && bits == 2 && packed && !codes && !err_w && dtype == CQ_F16 &&
         qp_cand_ok(m, n, (int)r)) {
         int64_t regions = 0, cap = 0;
-        qu_cand_bytes(m, n, batch, &regions, &cap);
+        qu_cand_geom(m, n, batch, qp_cand_rows((int)r), &regions, &cap);
         char* c = reinterpret_cast<char*>(q.part) + align_up((size_t)batch * tiles * sizeof(double), 256);
         q.ovf = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * 4, 256);
         q.cnt = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * 4, 256);
         q.part0 = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
         q.partF = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
-        q.list = reinterpret_cast<uint2*>(c);
+        q.gid = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * cap * 4, 256);
+        q.gval = reinterpret_cast<float4*>(c);
         q.cap = cap;
         q.hint = scale_hint;
         q.fb_out = fallback_out;

@@ -374,13 +374,15 @@ int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_
  * so the absmax pass is skipped and W is read once.
  * scale_hint (may be NULL; may alias scale_out): the previous Q update's scale per matrix.
  * With 2-bit packed codes, fp16 W and unit error weights, LR is then recomputed once: the
- * absmax pass also sums the all-zero-code error and lists every |res| >= 0.45 scale_hint;
- * the codes come from that list (a 2-bit code is nonzero only where |res| > scale / 2).  A
+ * absmax pass also sums the all-zero-code error and lists every 8-element group holding a
+ * |res| >= 0.45 scale_hint; the codes come from that list (a 2-bit code is nonzero only where
+ * |res| > scale / 2).  A
  * matrix whose list cannot be complete (scale < 0.9 scale_hint, list overflow, non-normal
- * scale) takes the second recompute; fallback_out[b] (may be NULL) reports it.  Codes and
+ * scale) takes the second recompute; fallback_out[b] (may be NULL) reports it.  The
+ * workspace is cq_q_update_workspace(m, n, batch, scale_hint != NULL) bytes.  Codes and
  * scales are those of the two-pass form bit for bit; err_out sums the same fp32 terms in
- * another fp64 order. */
-size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch);
+ * another order (~1e-8 relative). */
+size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint);
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
                    const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
                    const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,

@@ -37,9 +37,9 @@ LIST_CASES = [c for c in C.CASES if c[5] == 2 and c[6] == torch.float16]
 def test_q_update_single_recompute_matches_two_pass(case):
     """The 2-bit single-recompute path (scale_hint given: one L R recompute, candidate lists
     |res| >= 0.45 hint, codes from the lists) gives the two-pass kernel's packed codes and
-    scales bit for bit and its error sums to 1e-9 relative (the same fp32 terms, but a
-    candidate's term is summed in fp32 inside its run of 4 by pass 1 and alone in fp64 by the
-    list path: ~1e-10 measured); matrices whose list cannot be
+    scales bit for bit and its error sums to 1e-7 relative (the same fp32 terms, summed in
+    fp32 over runs of 4 by pass 1 and of 8 by the list path, whose nonzero codes' terms are
+    corrected in fp64); matrices whose list cannot be
     complete (scale < 0.9 hint, an overflowing list, a non-finite hint) take pass 1 and give
     the two-pass outputs exactly.  Mixed batches exercise both in one call, and the hint may
     alias the scale output (the engine's use: st.Qs is both)."""
@@ -83,4 +83,4 @@ def test_q_update_single_recompute_matches_two_pass(case):
                 if want_fb[i]:
                     assert e[i].item() == e0[i].item(), (name, i)
                 else:
-                    assert abs(e[i].item() - e0[i].item()) <= 1e-9 * e0[i].item(), (name, i, e[i].item(), e0[i].item())
+                    assert abs(e[i].item() - e0[i].item()) <= 1e-7 * e0[i].item(), (name, i, e[i].item(), e0[i].item())
