@@ -429,7 +429,7 @@ def main():
         t_mfma = flops / (mfma_peak * 1e12)
         t_hbm = nbytes / (PEAK_HBM_GBS * 1e9)
         traffic = None  # HBM bytes per launch from the committed PMC pass of this same config
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        pmc_path = os.path.join(ROOT, "bench_pmc_traffic.json")  # travels to the GPU box (profiles/ does not)
         solver_p = eng.solver.p if eng.solver is not None else None
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))

@@ -188,19 +188,15 @@ class BatchState:
         self.has_LR = False
         self.L_idxs = self.R_idxs = None
         self.L_scale = self.R_scale = None
+        self._vers = None  # best-state snapshots (snapshot_into / materialize)
+        self._pick = None
 
     def snapshot_into(self, dst: "BatchState", sel: list[int]):
-        """Copy the state of matrices `sel` into dst (one gather/scatter per tensor)."""
+        """Make the current state of matrices `sel` dst's best (alg.py:96-107).  Nothing is
+        copied: every Q and LR update writes fresh tensors (codes, scales, factors), so a
+        snapshot keeps references to the current tensors and, per matrix, which snapshot it
+        picked; materialize() assembles dst's tensors once, at the end of the run."""
         B = self.B
-        if dst.L.shape != self.L.shape:
-            dst.L = torch.zeros_like(self.L)
-            dst.R = torch.zeros_like(self.R)
-        if torch.is_tensor(self.L_idxs) and (dst.L_idxs is None or dst.L_idxs.shape != self.L_idxs.shape):
-            dst.L_idxs = torch.zeros_like(self.L_idxs)
-            dst.R_idxs = torch.zeros_like(self.R_idxs)
-            dst.L_scale = torch.zeros_like(self.L_scale)
-            dst.R_scale = torch.zeros_like(self.R_scale)
-        pairs = [(dst.Qc, self.Qc), (dst.Qs, self.Qs), (dst.L, self.L), (dst.R, self.R)]
         if self.dense_q and self.has_Q:
             # codebook Q: every Q update allocates fresh tensors, so the snapshot keeps views
             if dst.Qd is None:
@@ -215,19 +211,59 @@ class BatchState:
             for b in sel:
                 dst.L_idxs[b], dst.R_idxs[b] = self.L_idxs[b], self.R_idxs[b]
                 dst.L_scale[b], dst.R_scale[b] = self.L_scale[b], self.R_scale[b]
-        elif self.L_idxs is not None:
-            pairs += [(dst.L_idxs, self.L_idxs), (dst.R_idxs, self.R_idxs),
-                      (dst.L_scale, self.L_scale), (dst.R_scale, self.R_scale)]
-        if len(sel) == B:
-            for d, s in pairs:
-                d.copy_(s)
+            idxs = None
         else:
-            idx = torch.tensor(sel, dtype=torch.long, device=self.Qc.device)
-            for d, s in pairs:
-                d.index_copy_(0, idx, s.index_select(0, idx))
+            idxs = (self.L_idxs, self.R_idxs, self.L_scale, self.R_scale) if self.L_idxs is not None else None
+        if dst._vers is None:  # version 0: dst's own (zero) tensors, for matrices never picked
+            dst._vers = {0: (dst.Qc, dst.Qs, dst.L, dst.R, None)}
+            dst._pick = [0] * B
+        vid = max(dst._vers) + 1
+        dst._vers[vid] = (self.Qc, self.Qs, self.L, self.R, idxs)
+        for b in sel:
+            dst._pick[b] = vid
+        live = set(dst._pick)
+        dst._vers = {v: t for v, t in dst._vers.items() if v in live}
         for b in sel:
             dst.flag_Q[b] = self.has_Q
             dst.flag_LR[b] = self.has_LR
+
+    def materialize(self):
+        """The picked snapshot's tensors per matrix (snapshot_into): references when every
+        matrix picked the same snapshot, else one gather per snapshot used."""
+        if self._vers is None:
+            return
+        picks = self._pick
+        used = sorted(set(picks))
+        if len(used) == 1:
+            qc, qs, L, R, idxs = self._vers[used[0]]
+            self.Qc, self.Qs, self.L, self.R = qc, qs, L, R
+            if idxs is not None:
+                self.L_idxs, self.R_idxs, self.L_scale, self.R_scale = idxs
+        else:
+            # the snapshot most matrices picked becomes the result in place (the snapshots are
+            # dead after this); the others' matrices are gathered into it
+            base = max(used, key=lambda v: sum(1 for x in picks if x == v))
+            qc, qs, L, R, idxs = self._vers[base]
+            out = [qc, qs, L, R]
+            oidx = list(idxs) if idxs is not None else None
+            if oidx is None and any(self._vers[v][4] is not None for v in used):
+                ref = next(self._vers[v][4] for v in used if self._vers[v][4] is not None)
+                oidx = [torch.zeros_like(t) for t in ref]
+            for v in used:
+                if v == base:
+                    continue
+                sel = [b for b in range(self.B) if picks[b] == v]
+                idx = torch.tensor(sel, dtype=torch.long, device=qc.device)
+                src = self._vers[v]
+                for d, s in zip(out, src[:4]):
+                    d.index_copy_(0, idx, s.index_select(0, idx))
+                if oidx is not None and src[4] is not None:
+                    for d, s in zip(oidx, src[4]):
+                        d.index_copy_(0, idx, s.index_select(0, idx))
+            self.Qc, self.Qs, self.L, self.R = out
+            if oidx is not None:
+                self.L_idxs, self.R_idxs, self.L_scale, self.R_scale = oidx
+        self._vers = None
 
 
 class CalderaEngine:
@@ -267,6 +303,11 @@ class CalderaEngine:
         Kdim = st.L.shape[-1] if (p.compute_low_rank_factors and st.has_LR) else 0
         if st.dense_q:
             return self._q_update_codebook(st, Ws, res_buf, wts, Kdim)
+        # fresh code / scale tensors for every update: the best-state snapshots keep references
+        # to earlier ones instead of copying them (BatchState.snapshot_into)
+        prev_qs = st.Qs
+        st.Qc = torch.empty_like(st.Qc)
+        st.Qs = torch.empty_like(st.Qs)
         if Kdim % 32 == 0:
             # fused: res = W - L R recomputed per tile on split-fp16 products, never stored
             err = torch.empty(B, dtype=torch.float64, device=Ws.device)
@@ -280,10 +321,10 @@ class CalderaEngine:
             amax = self._wmax if not Kdim else None
             ew = None if wts.err_unit else wts.err  # unit weights: the same sums without the loads
             if st.q_packed:
-                # the previous scale (st.Qs, rewritten by this call) lets a 2-bit update
-                # recompute L R once (candidate lists; cq_q_update_x3); the per-matrix count of
-                # second recomputes is accumulated on the device (q_fallbacks)
-                hint = st.Qs if (Kdim and st.has_Q and self.q_single_recompute) else None
+                # the previous scale lets a 2-bit update recompute L R once (candidate lists;
+                # cq_q_update_x3); the per-matrix count of second recomputes is accumulated on
+                # the device (q_fallbacks)
+                hint = prev_qs if (Kdim and st.has_Q and self.q_single_recompute) else None
                 fb = None
                 if hint is not None:
                     if self._qfb is None or self._qfb.numel() != B:
@@ -931,6 +972,7 @@ class CalderaEngine:
         self._yrh = self._yrl = None
         if host_copy is not None:
             Ws_out = host_copy()  # joins the copy thread: the host tensor
+        best.materialize()
         out = self._finalize(best, st, W, Ws_out, gs, errors, wts, spare=(work, res))
         if pad:
             out = [self._cut_columns(d, m, n, n_true) for d in out]

@@ -649,9 +649,11 @@ class RankRSolver:
         # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
         # one CholQR pass restores orthonormality without moving the converged subspace
         X, _ = self._cholqr(X)
-        if self.X is None:
-            self.X = torch.empty((B, k, p), dtype=torch.float32, device=dev)
-        self.X.copy_(X)
+        # the final block becomes the warm start by a swap with the pool (no copy): X's pool
+        # slot takes the previous warm-start buffer (a fresh one on the first call)
+        i = next(j for j, t in enumerate(self._bufs) if t is X)
+        old = self.X if self.X is not None else torch.empty((B, k, p), dtype=torch.float32, device=dev)
+        self._bufs[i], self.X = old, X
         self.theta = theta.clone()
         self._ends = ends
         return self.X[:, :, : self.r], theta[:, : self.r]
