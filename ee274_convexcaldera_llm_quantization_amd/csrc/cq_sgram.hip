@@ -98,72 +98,170 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
 }
 
 constexpr int SG_FILL_CAP = 512;
+constexpr int SG_FILL_RW = 4;   // sorted positions (rows) per wave
+
+// Entry order.  The SpMM reads E's l-th 16-byte slab entry (LDS bank group l mod 16) for the 64
+// rows of a slice at once, one lane per row; lanes whose entries share a bank group at the same
+// step serialise.  Step t of the row at sorted position q (mod 16) therefore takes an entry of
+// residue (q + t) mod 16 while it has one (neighbouring lanes then read different groups), else
+// one of the residue with the most entries left (ties: the smaller residue); within a residue in
+// increasing l.  Rows longer than SG_FILL_CAP take the plain residue-rotated order
+// (sg_fill_plain).  One wave per SG_FILL_RW rows: each row's nonzeros are compacted in l order
+// (one pass over its words) and stably counting-sorted by residue; the greedy order then runs
+// for the SG_FILL_RW rows at once, 16 lanes (one per residue) each.
+__device__ void sg_fill_plain(const uint32_t* __restrict__ row, int64_t nw, int q, int lane, uint32_t* out) {
+    int64_t base = 0;
+    for (int i = 0; i < 16; ++i) {
+        const int u = (q + i) & 15;
+        for (int64_t w0 = 0; w0 < nw; w0 += 64) {
+            const int64_t w = w0 + lane;
+            const uint32_t f = w < nw ? sg_field(row[w], u) : 1u;
+            const bool nz = f != 1u;
+            const uint64_t msk = __ballot(nz);
+            if (nz) out[(base + __popcll(msk & ((1ull << lane) - 1ull))) * SG_SLICE] = (uint32_t)((16 * w + u) << 2) | f;
+            base += __popcll(msk);
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
                                                          const int32_t* __restrict__ row_nnz,
                                                          const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ slice_off, int64_t stride_ell,
                                                          uint32_t* __restrict__ ell) {
-    const int lane = threadIdx.x & 63;
-    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // sorted position
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wv) * SG_FILL_RW;
     const int64_t b = blockIdx.y;
-    if (p >= k) return;
-    const int64_t j = perm[b * k + p];
-    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
-    const int64_t s = p / SG_SLICE;
-    const int64_t off = slice_off[b * (ns + 1) + s], width = slice_off[b * (ns + 1) + s + 1] - off;
-    uint32_t* out = ell + b * stride_ell + off * SG_SLICE + (p % SG_SLICE);
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
+    if (p0 >= k) return;
+    __shared__ uint32_t nat[4][SG_FILL_CAP];
+    __shared__ uint32_t grp[4][SG_FILL_RW][SG_FILL_CAP];
+    __shared__ int rsb[4][SG_FILL_RW][16], rcb[4][SG_FILL_RW][16];
     const int64_t nw = L / 16;
-    // Entry order.  The SpMM reads E's l-th 16-byte slab entry (LDS bank group l mod 16) for the
-    // 64 rows of a slice at once, one lane per row; lanes whose entries share a bank group at the
-    // same step serialise.  Step t of the row at lane q therefore takes an entry of residue
-    // (q + t) mod 16 while it has one (neighbouring lanes then read different groups), else one
-    // of the residue with the most entries left (ties: the smaller residue); within a residue in
-    // increasing l.  Rows longer than SG_FILL_CAP fall back to the plain residue-rotated order.
-    const int q = (int)(p & 15);
-    __shared__ uint32_t buf[4][SG_FILL_CAP];
-    uint32_t* wb = buf[threadIdx.x >> 6];
-    int64_t base = 0;
-    int rstart = 0, rcnt = 0;  // lane u < 16: residue u's entries in wb
-    const bool fits = row_nnz[b * k + j] <= SG_FILL_CAP;
-    for (int i = 0; i < 16; ++i) {
-        const int u = (q + i) & 15;
-        const int64_t b0 = base;
+    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int cntr[SG_FILL_RW];   // entries of each row taking the greedy order (0: none / plain)
+    uint32_t* outr[SG_FILL_RW];
+    int64_t widr[SG_FILL_RW];
+#pragma unroll
+    for (int r = 0; r < SG_FILL_RW; ++r) {
+        cntr[r] = 0;
+        outr[r] = nullptr;
+        widr[r] = 0;
+        const int64_t p = p0 + r;
+        if (p >= k) continue;
+        const int64_t j = perm[b * k + p];
+        const int64_t s = p / SG_SLICE;
+        const int64_t off = slice_off[b * (ns + 1) + s];
+        widr[r] = slice_off[b * (ns + 1) + s + 1] - off;
+        outr[r] = ell + b * stride_ell + off * SG_SLICE + (p % SG_SLICE);
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
+        if (row_nnz[b * k + j] > SG_FILL_CAP) {
+            sg_fill_plain(row, nw, (int)(p & 15), lane, outr[r]);
+            cntr[r] = -row_nnz[b * k + j];   // written; padding below
+            continue;
+        }
+        // the row's nonzeros in increasing l: per word, codes u = 0..15 in order
+        int cnt = 0;
         for (int64_t w0 = 0; w0 < nw; w0 += 64) {
             const int64_t w = w0 + lane;
-            const uint32_t f = w < nw ? sg_field(row[w], u) : 1u;
-            const bool nz = f != 1u;
-            const uint64_t msk = __ballot(nz);
-            if (nz) {
-                const int64_t pos = base + __popcll(msk & ((1ull << lane) - 1ull));
-                const uint32_t e = (uint32_t)((16 * w + u) << 2) | f;
-                if (fits) wb[pos] = e;
-                else out[pos * SG_SLICE] = e;
-            }
-            base += __popcll(msk);
-        }
-        if (lane == u) { rstart = (int)b0; rcnt = (int)(base - b0); }
-    }
-    if (fits) {
-        __builtin_amdgcn_wave_barrier();
-        int taken = 0;
-        for (int64_t t = 0; t < base; ++t) {
-            const int d = (int)((q + t) & 15);
-            int u = d;
-            if (__shfl(rcnt - taken, d, 64) <= 0) {
-                // the residue with the most entries left: key = remaining * 16 + (15 - residue)
-                int key = lane < 16 ? ((rcnt - taken) << 4) | (15 - lane) : -1;
+            const uint32_t word = w < nw ? row[w] : 0x55555555u;
+            uint32_t um = 0;
 #pragma unroll
-                for (int o = 8; o > 0; o >>= 1) key = max(key, __shfl_xor(key, o, 64));
-                u = 15 - (__shfl(key, 0, 64) & 15);
+            for (int u = 0; u < 16; ++u) um |= (uint32_t)(sg_field(word, u) != 1u) << u;
+            const int c = __builtin_popcount(um);
+            int pre = 0, tot = 0;
+#pragma unroll
+            for (int bt = 0; bt < 5; ++bt) {
+                const uint64_t mk = __ballot((c >> bt) & 1);
+                pre += __popcll(mk & lt) << bt;
+                tot += __popcll(mk) << bt;
             }
-            const int at = __shfl(rstart + taken, u, 64);
-            if (lane == 0) out[t * SG_SLICE] = wb[at];
-            if (lane == u) ++taken;
+            int pos = cnt + pre;
+            while (um) {
+                const int u = __builtin_ctz(um);
+                um &= um - 1u;
+                nat[wv][pos++] = (uint32_t)((16 * w + u) << 2) | sg_field(word, u);
+            }
+            cnt += tot;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // stable counting sort by residue (l mod 16): counts, starts, ranks (16 ballots a batch)
+        int cntu = 0;   // lane u < 16: entries of residue u
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            const int res = i < cnt ? (int)((nat[wv][i] >> 2) & 15u) : 16;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int m = __popcll(__ballot(res == u));
+                if (lane == u) cntu += m;
+            }
+        }
+        int start = cntu;   // exclusive prefix over lanes 0..15
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int v = __shfl_up(start, o, 64);
+            if ((lane & 15) >= o) start += v;
+        }
+        start -= cntu;
+        if (lane < 16) {
+            rsb[wv][r][lane] = start;
+            rcb[wv][r][lane] = cntu;
+        }
+        int seen = 0;   // lane u < 16: entries of residue u already placed
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            const uint32_t e = i < cnt ? nat[wv][i] : 0u;
+            const int res = i < cnt ? (int)((e >> 2) & 15u) : 16;
+            int dst = 0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const uint64_t mk = __ballot(res == u);
+                const int su = __shfl(start + seen, u, 64);
+                if (res == u) dst = su + __popcll(mk & lt);
+                if (lane == u) seen += __popcll(mk);
+            }
+            if (i < cnt) grp[wv][r][dst] = e;
+        }
+        cntr[r] = cnt;
+        __builtin_amdgcn_wave_barrier();
+    }
+    // greedy order, the SG_FILL_RW rows at once: lane = 16 g + u (row g, residue u)
+    const int g = lane >> 4, u = lane & 15;
+    int myc = 0, mys = 0, mycnt = 0;
+    uint32_t* myout = nullptr;
+    int64_t mywid = 0;
+#pragma unroll
+    for (int r = 0; r < SG_FILL_RW; ++r)
+        if (g == r) { mycnt = cntr[r]; myout = outr[r]; mywid = widr[r]; }
+    if (mycnt > 0) {
+        myc = rcb[wv][g][u];
+        mys = rsb[wv][g][u];
+    }
+    int T = 0;
+#pragma unroll
+    for (int r = 0; r < SG_FILL_RW; ++r) T = cntr[r] > T ? cntr[r] : T;
+    const int q = (int)((p0 + g) & 15);
+    int taken = 0;
+    for (int t = 0; t < T; ++t) {
+        const int d = (q + t) & 15;
+        const int remd = __shfl(myc - taken, 16 * g + d, 64);
+        int key = ((myc - taken) << 4) | (15 - u);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) key = max(key, __shfl_xor(key, o, 64));
+        const int sel = remd > 0 ? d : 15 - (key & 15);
+        const int at = __shfl(mys + taken, 16 * g + sel, 64);
+        if (t < mycnt) {
+            if (u == 0) myout[(int64_t)t * SG_SLICE] = grp[wv][g][at];
+            if (u == sel) ++taken;
         }
     }
-    for (int64_t t = base + 0; t < width; ++t) out[t * SG_SLICE] = 1u;  // padding: l = 0, code 0
+    // padding: l = 0, code 0
+#pragma unroll
+    for (int r = 0; r < SG_FILL_RW; ++r) {
+        if (!outr[r]) continue;
+        const int64_t from = cntr[r] < 0 ? -cntr[r] : cntr[r];
+        for (int64_t t = from + lane; t < widr[r]; t += 64) outr[r][t * SG_SLICE] = 1u;
+    }
 }
 
 // one 64-row slice of the sorted ELL for the R staged rows: acc[r] = P[i0 + r, perm[64 s + lane]].
@@ -480,7 +578,7 @@ int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int
     CQ_REQUIRE(bits == 2, "cq_sgram_fill: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0 && L < (1ll << 29),
                "cq_sgram_fill: bad shape");
-    sgram_fill_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, as_stream(stream)>>>(
+    sgram_fill_kernel<<<dim3((unsigned)ceil_div(k, 4 * SG_FILL_RW), (unsigned)batch), 256, 0, as_stream(stream)>>>(
         packed, k, L, row_nnz, perm, slice_off, stride_ell, ell);
     return check_launch("cq_sgram_fill");
 }

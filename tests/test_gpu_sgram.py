@@ -5,6 +5,7 @@ of W) and P = (W - (s/2) c) diag(w) c^T over the sliced-ELL codes.  Checked: the
 nonzero counts (exact), the fp32 G and its K-blocked split halves (fp32-grade against fp64,
 and against the dense split-fp16 Gram of Y that it replaces), for every LDS slab height
 (R = 8 / 4 / 2 rows of E by contraction length) and with and without column weights."""
+import numpy as np
 import pytest
 import torch
 
@@ -90,3 +91,73 @@ def test_sparse_gram_matches_fp64(B, m, n, weighted):
           f"{errs:.2e}, dense split Gram {errd:.2e}")
     # fp32-grade: within 1.5x (+2e-7) of the dense split-fp16 Gram's own error, on every shape
     assert err32 < 1.5 * errd + 2e-7 and errs < 1.5 * errd + 2e-7
+
+
+def _expected_ell_rows(codes, perm, row_nnz):
+    """The sliced-ELL entry order (cq_sgram.hip, sgram_fill_kernel) restated on the host: per
+    sorted position p (row j = perm[p]) the nonzero codes (l << 2 | code + 1), grouped by
+    residue l mod 16 in increasing l; rows of at most 512 entries take residue (p + t) mod 16 at
+    step t while it has entries left, else the residue with the most left (ties: the smaller);
+    longer rows the residues in the order p, p + 1, ... (mod 16)."""
+    out = []
+    for p, j in enumerate(perm):
+        row = codes[j]
+        ls = np.nonzero(row != 0)[0]
+        ent = {u: [int((l << 2) | (row[l] + 1)) for l in ls if l % 16 == u] for u in range(16)}
+        q = p & 15
+        seq = []
+        if row_nnz[j] > 512:
+            for i in range(16):
+                seq += ent[(q + i) & 15]
+        else:
+            taken = [0] * 16
+            for t in range(len(ls)):
+                d = (q + t) & 15
+                if taken[d] < len(ent[d]):
+                    u = d
+                else:
+                    u = max(range(16), key=lambda v: (len(ent[v]) - taken[v], -v))
+                seq.append(ent[u][taken[u]])
+                taken[u] += 1
+        out.append(seq)
+    return out
+
+
+@pytest.mark.parametrize("k,L,dens", [(200, 1024, 0.03), (64, 4096, 0.004)])
+def test_sparse_gram_ell_order(k, L, dens):
+    """The ELL fill (sgram_count + sgram_fill) against the host restatement of its entry order:
+    counts, row sort, per-row entry sequence (bank-group rotation, greedy fallback, rows past
+    512 entries in residue-rotated order) and padding, entry for entry."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    rng = np.random.default_rng(k + L)
+    B = 2
+    codes = np.where(rng.random((B, k, L)) < dens, rng.choice([-1, 1], size=(B, k, L)), 0).astype(np.int8)
+    codes[0, 5, : L // 2] = 1          # a row past 512 entries when L >= 1026
+    codes[1, 7, :] = 0                 # an empty row
+    off = (codes + 1).astype(np.uint8).reshape(B, k, L // 4, 4)
+    packed = (off[..., 0] << 6) | (off[..., 1] << 4) | (off[..., 2] << 2) | off[..., 3]
+    dev = "cuda:0"
+    pk = torch.from_numpy(np.ascontiguousarray(packed).reshape(B, -1)).to(dev)
+    ns = -(-k // 64)
+    row_nnz = torch.empty(B * k, dtype=torch.int32, device=dev)
+    perm = torch.empty(B * k, dtype=torch.int32, device=dev)
+    slice_off = torch.empty(B * (ns + 1), dtype=torch.int64, device=dev)
+    total = torch.empty(B, dtype=torch.int64, device=dev)
+    K.sgram_count(pk, k, L, row_nnz, perm, slice_off, total)
+    stride = int(total.max().item()) + 64
+    ell = torch.full((B * stride,), -7, dtype=torch.int32, device=dev)
+    K.sgram_fill(pk, k, L, row_nnz, perm, slice_off, ell, stride)
+    torch.cuda.synchronize()
+    nz, pm, so = row_nnz.cpu().numpy().reshape(B, k), perm.cpu().numpy().reshape(B, k), slice_off.cpu().numpy()
+    el = ell.cpu().numpy().view(np.uint32).reshape(B, stride)
+    for b in range(B):
+        assert (nz[b] == (codes[b] != 0).sum(1)).all()
+        assert sorted(pm[b].tolist()) == list(range(k))
+        exp = _expected_ell_rows(codes[b], pm[b], nz[b])
+        sob = so[b * (ns + 1):(b + 1) * (ns + 1)]
+        for p in range(k):
+            s = p // 64
+            width = int(sob[s + 1] - sob[s])
+            got = [int(el[b, (sob[s] + t) * 64 + p % 64]) for t in range(width)]
+            want = exp[p] + [1] * (width - len(exp[p]))
+            assert got == want, (b, p, got[:8], want[:8])
