@@ -35,7 +35,8 @@ constexpr size_t QP_LDS_MAX = 156 * 1024;
 __host__ __device__ constexpr int qp_rstage(int ksmax) { return 2 * QP_BN * 32 * ksmax; }
 __host__ __device__ constexpr int qp_wslot(int nw, int rb) { return nw * rb * 512; }
 __host__ __device__ constexpr size_t qp_lds_bytes(int nw, int rb, int ksmax, bool wl) {
-    return (size_t)(2 * qp_rstage(ksmax) + (wl ? QP_WD * qp_wslot(nw, rb) : 0)) * 2;
+    // (W ring: + two 32-float slots of the error column weights of a chunk, pass 2)
+    return (size_t)(2 * qp_rstage(ksmax) + (wl ? QP_WD * qp_wslot(nw, rb) + 2 * 64 : 0)) * 2;
 }
 
 // 16-B chunk swizzle of an LDS row: the 16 rows one MFMA fragment read touches (rows
@@ -175,6 +176,17 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         }
     };
     _Float16* wring = smem + 2 * RSTAGE;
+    // pass 2 with error column weights: a chunk's 32 weights ride with its R^T stage (LDS-DMA
+    // by 8 lanes of wave 0, issued before the W loads, so the counted wait covers them), read
+    // from LDS in the epilogue -- a global load there would drain the W ring
+    float* ewslot = reinterpret_cast<float*>(wring + QP_WD * WSLOT);
+    const bool ewl = PASS == 2 && WL && q.ew != nullptr;
+    auto issue_ew = [&](int64_t chn) {
+        if (ewl && wid == 0 && lane < 8)
+            __builtin_amdgcn_global_load_lds((const void*)(q.ew + chn * QP_BN + 4 * lane),
+                                             (__attribute__((address_space(3))) void*)(ewslot + 32 * (chn & 1)), 16, 0,
+                                             0);
+    };
     // WL: this wave's RB pieces (16 rows x 64 B) of chunk chn into ring slot `slot` by LDS-DMA
     auto issue_w = [&](int64_t chn, int slot) {
 #pragma unroll
@@ -295,10 +307,19 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 // true), a wait that costs little next to a chunk's ~4 us of MFMA work.
                 uint32_t lm = 0u;
                 float e8 = 0.f;
+                if (ewl) {
+                    const float* wv = ewslot + 32 * (ch & 1) + 8 * lq;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    lm = max(lm, abs_bits(v[u]));
-                    e8 = __builtin_fmaf(v[u], v[u], e8);
+                    for (int u = 0; u < 8; ++u) {
+                        lm = max(lm, abs_bits(v[u]));
+                        e8 = __builtin_fmaf(v[u] * v[u], wv[u], e8);
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        lm = max(lm, abs_bits(v[u]));
+                        e8 = __builtin_fmaf(v[u], v[u], e8);
+                    }
                 }
                 mx = max(mx, lm);
                 err += (double)e8;
@@ -436,13 +457,16 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         // of ch + QP_WD - 1 (into the slot chunk ch - 1 has finished reading) are issued
         static_assert(QP_WD >= 3, "W(ch + 1) must be older than R(ch + 1) at the counted wait");
         qp_issue_r<NW, RROW>(Rhb, Rlb, 0, K, smem, wid, lane);
+        issue_ew(0);
         for (int c = 0; c < QP_WD - 1 && c < nchunks; ++c) issue_w(c, c);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int sw = 0;   // slot of chunk ch
         for (int64_t ch = 0; ch < nchunks; ++ch) {
-            if (ch + 1 < nchunks)
+            if (ch + 1 < nchunks) {
                 qp_issue_r<NW, RROW>(Rhb, Rlb, (ch + 1) * QP_BN, K, smem + ((ch + 1) & 1) * RSTAGE, wid, lane);
+                issue_ew(ch + 1);
+            }
             const bool wlive = ch + QP_WD - 1 < nchunks;
             if (wlive) issue_w(ch + QP_WD - 1, sw == 0 ? QP_WD - 1 : sw - 1);
             uint4 wc[RB][WV];
@@ -587,7 +611,12 @@ __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw
                     const uint32_t sh = 8u * (uint32_t)((loc >> 2) & 3) + 6u - 2u * (uint32_t)(loc & 3);
                     atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
                     const float d = c * s - x;
-                    delta += (double)(d * d) - (double)(x * x);
+                    if (q.ew) {
+                        const float w = q.ew[(loc + base) % n];
+                        delta += (double)((d * d) * w) - (double)((x * x) * w);
+                    } else {
+                        delta += (double)(d * d) - (double)(x * x);
+                    }
                 }
             }
         }

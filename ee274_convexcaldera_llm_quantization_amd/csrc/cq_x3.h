@@ -78,7 +78,7 @@ constexpr int QP_KMAX = 256;              // row-panel Q update: largest r
 int64_t qp_launch(QUK& q, int dtype, int bits, const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth,
                   const uint16_t* Rtl, int K, int64_t batch, hipStream_t s);
 // The single-recompute 2-bit path's geometry (rows per wave) and whether it applies: fp16 W,
-// K <= 256, no error weights, a wave region's packed codes fit the code kernel's LDS.
+// K <= 256, a wave region's packed codes fit the code kernel's LDS.
 int qp_cand_rows(int K);
 bool qp_cand_ok(int64_t m, int64_t n, int K);
 // Launches pass 2, the code kernel, the fallback pass 1 and the finalize (scale, error,

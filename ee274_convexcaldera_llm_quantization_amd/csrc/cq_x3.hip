@@ -1399,9 +1399,9 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     // row-panel kernel (q_update_p_kernel): K <= 256, m % 16 == 0, n % 32 == 0, 16-B aligned
     const bool pk = r > 0 && r <= QP_KMAX && m % 16 == 0 && n % QP_BN == 0 && vk && al16(Lh) && al16(Ll) &&
                     al16(Rth) && al16(Rtl);
-    // single recompute (2-bit packed codes, fp16 W, unit error weights, previous scale given):
+    // single recompute (2-bit packed codes, fp16 W, previous scale given):
     // pass 2 + candidate lists + code kernel, pass 1 only where a list cannot be complete
-    if (pk && !known && scale_hint && bits == 2 && packed && !codes && !err_w && dtype == CQ_F16 &&
+    if (pk && !known && scale_hint && bits == 2 && packed && !codes && dtype == CQ_F16 &&
         qp_cand_ok(m, n, (int)r)) {
         int64_t regions = 0, cap = 0;
         qu_cand_geom(m, n, batch, qp_cand_rows((int)r), &regions, &cap);

@@ -28,6 +28,7 @@ the only host synchronisation is the convergence test once per outer iteration.
 from __future__ import annotations
 
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -637,6 +638,13 @@ class RankRSolver:
                 recent = np.min(Hh[-2:], axis=0)
                 new_stall = (~stalled) & (resid > self.tol) & np.isfinite(before) & (recent > STALL_RATIO * before)
                 self.stats.stalls += int(new_stall.sum())
+                if new_stall.any():
+                    # the split-fp16 products' precision floor sits above the tolerance for these
+                    # matrices (an input whose dynamic range erodes the fp32-grade margin): the
+                    # rank-r projection is then only as accurate as the residual reached
+                    warnings.warn(f"rank-r solver: {int(new_stall.sum())} matrices stopped at the product "
+                                  f"precision floor above tolerance {self.tol:g} (residual estimate "
+                                  f"{float(resid[new_stall].max()):.2e})", RuntimeWarning, stacklevel=2)
                 stalled |= new_stall
             # converged (or stalled) matrices sit out the remaining filter products (X passes through)
             live = (resid > self.tol) & ~stalled

@@ -373,7 +373,7 @@ int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_
  * absmax_in (r = 0 only, may be NULL): max|W[b]| already known (cq_absmax of the same W),
  * so the absmax pass is skipped and W is read once.
  * scale_hint (may be NULL; may alias scale_out): the previous Q update's scale per matrix.
- * With 2-bit packed codes, fp16 W and unit error weights, LR is then recomputed once: the
+ * With 2-bit packed codes and fp16 W, LR is then recomputed once: the
  * absmax pass also sums the all-zero-code error and lists every 8-element group holding a
  * |res| >= 0.45 scale_hint; the codes come from that list (a 2-bit code is nonzero only where
  * |res| > scale / 2).  A

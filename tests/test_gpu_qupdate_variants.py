@@ -33,8 +33,9 @@ def test_q_update_matches_round2_kernel(case):
 LIST_CASES = [c for c in C.CASES if c[5] == 2 and c[6] == torch.float16]
 
 
+@pytest.mark.parametrize("weighted", [False, True], ids=["unit", "err_w"])
 @pytest.mark.parametrize("case", LIST_CASES, ids=[c[0] for c in LIST_CASES])
-def test_q_update_single_recompute_matches_two_pass(case):
+def test_q_update_single_recompute_matches_two_pass(case, weighted):
     """The 2-bit single-recompute path (scale_hint given: one L R recompute, candidate lists
     |res| >= 0.45 hint, codes from the lists) gives the two-pass kernel's packed codes and
     scales bit for bit and its error sums to 1e-7 relative (the same fp32 terms, summed in
@@ -48,6 +49,8 @@ def test_q_update_single_recompute_matches_two_pass(case):
     dev = torch.device("cuda:0")
     W, L, R = C.make(B, m, n, r, dt, seed=sum(map(ord, tag)) + 7)
     W, L, R = W.to(dev), L.to(dev), R.to(dev)
+    # error column weights (the activation-aware error, alg.py:286-302): h spanning 1e-3..10
+    ew = (10.0 ** torch.empty(n).uniform_(-3, 1, generator=torch.Generator().manual_seed(n))).to(dev) if weighted else None
 
     def call(hint, alias=False):
         packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=dev)
@@ -55,10 +58,12 @@ def test_q_update_single_recompute_matches_two_pass(case):
         fb = torch.full((B,), -1, dtype=torch.int32, device=dev)
         if alias and hint is not None:
             scale = hint.clone()
-            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=scale, fallback_out=fb)
+            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, err_w=ew, scale_hint=scale,
+                          fallback_out=fb)
         else:
             scale = torch.empty(B, device=dev)
-            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=hint, fallback_out=fb)
+            K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, err_w=ew, scale_hint=hint,
+                          fallback_out=fb)
         torch.cuda.synchronize()
         return packed.cpu(), scale.cpu(), err.cpu(), fb.cpu()
 
