@@ -602,16 +602,18 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     const dim3 grid((unsigned)ceil_div(k, R), (unsigned)batch);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const int64_t nsw = ceil_div(ceil_div(k, SG_SLICE), SG_WAVES);  // slices per wave
-    // the register-held form needs k <= L (the output block reuses the slab's LDS)
-    const bool held = k <= L && nsw * R <= 32;
+    // the register-held form needs k <= L (the output block reuses the slab's LDS) and fits the
+    // 128-VGPR budget of 16 waves per CU only at R = 8 (4 slices per wave): at R = 4 / 2 its 8 /
+    // 16 inlined slice loops spilled to scratch (cfg3's R = 2 SpMM ran 587 ms instead of ~20)
+    const bool held = k <= L && nsw * R <= 32 && R == 8;
 #define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
                                                                              perm, slice_off, stride_ell, P)
     if (R == 8) {
         if (held) CQ_SP(8, 4); else CQ_SP(8, 0);
     } else if (R == 4) {
-        if (held) CQ_SP(4, 8); else CQ_SP(4, 0);
+        CQ_SP(4, 0);
     } else {
-        if (held) CQ_SP(2, 16); else CQ_SP(2, 0);
+        CQ_SP(2, 0);
     }
 #undef CQ_SP
     return check_launch("cq_sgram_spmm");
