@@ -429,6 +429,25 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
             for (int r = 0; r < R; ++r)
                 if (i0 + r < k) Pb[(i0 + r) * k + j] = v[r];
         }
+    } else if constexpr (NSW < 0) {
+        // output block of its own after the slab (k x R, j-major): each slice's results go to
+        // LDS as soon as they are done (nothing held in registers), then stored over j
+        float* outb = slab + (int64_t)R * L;
+        for (int64_t s = wv; s < ns; s += SG_WAVES) {
+            float acc[R];
+            sg_slice<R>(slab, L, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc);
+            const int64_t p = s * SG_SLICE + lane;
+            if (p < k) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) outb[(int64_t)pm[p] * R + r] = acc[r];
+            }
+        }
+        __syncthreads();
+        for (int64_t j = threadIdx.x; j < k; j += SG_THREADS) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (i0 + r < k) Pb[(i0 + r) * k + j] = outb[j * R + r];
+        }
     } else {
         for (int64_t s = wv; s < ns; s += SG_WAVES) {
             float acc[R];
@@ -597,7 +616,7 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L % 64 == 0, "cq_sgram_spmm: bad shape");
     const int R = cq_sgram_rows(L);
     CQ_REQUIRE(R > 0, "cq_sgram_spmm: rows of %lld values do not fit the LDS", (long long)L);
-    const size_t lds = (size_t)L * R * sizeof(float);
+    size_t lds = (size_t)L * R * sizeof(float);
     hipStream_t s = as_stream(stream);
     const dim3 grid((unsigned)ceil_div(k, R), (unsigned)batch);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
@@ -606,14 +625,17 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     // 128-VGPR budget of 16 waves per CU only at R = 8 (4 slices per wave): at R = 4 / 2 its 8 /
     // 16 inlined slice loops spilled to scratch (cfg3's R = 2 SpMM ran 587 ms instead of ~20)
     const bool held = k <= L && nsw * R <= 32 && R == 8;
+    // R = 4 / 2: results through an LDS output block of their own where slab + block fit
+    const bool ldsout = !held && R < 8 && lds + (size_t)k * R * sizeof(float) <= 150 * 1024;
+    if (ldsout) lds += (size_t)k * R * sizeof(float);
 #define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
                                                                              perm, slice_off, stride_ell, P)
     if (R == 8) {
         if (held) CQ_SP(8, 4); else CQ_SP(8, 0);
     } else if (R == 4) {
-        CQ_SP(4, 0);
+        if (ldsout) CQ_SP(4, -1); else CQ_SP(4, 0);
     } else {
-        CQ_SP(2, 0);
+        if (ldsout) CQ_SP(2, -1); else CQ_SP(2, 0);
     }
 #undef CQ_SP
     return check_launch("cq_sgram_spmm");
