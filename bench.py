@@ -449,9 +449,9 @@ def main():
                      "flops_per_launch_fp32_equiv": flops, "achieved_tflops_fp32_equiv": ach_tf,
                      "mfma_frac": ach_tf / mfma_peak, "solver_block_p": solver_p})
         result["roofline"] = roof
-    # the quantise kernel (fused Q update, both passes; SURVEY.md 8(d) bytes_Q per call):
+    # the quantise kernel (fused Q update, every pass of a call; SURVEY.md 8(d) bytes_Q per call):
     # "w" = first Q step (quantise W itself, pure HBM), "lr" = Q steps recomputing W - L R on
-    # split-fp16 MFMAs (3 fp16 products per fp32-equivalent flop, both passes)
+    # split-fp16 MFMAs (3 fp16 products per fp32-equivalent flop; one recompute on the 2-bit list path)
     qroof = {}
     for kind, g in qprobe.items():
         t = g["avg_ms"] * 1e-3
