@@ -85,12 +85,22 @@ def synth_W(wl, seed):
     return (torch.randn(wl["m"], wl["n"]) * 0.02).to(torch.float16)
 
 
-def synth_batch(wl, B, seed0, dev):
-    """B synthetic weights; each goes to `dev` as soon as it is made (one matrix of host
-    memory per rank)."""
+PINNED = 16  # batch positions whose matrices the golden runs pin (seeds 0-15, host RNG)
+
+
+def synth_batch(wl, B, seed0, dev, host=PINNED):
+    """B synthetic weights of the same recipe (randn * 0.02 -> fp16).  The first `host` come
+    from the host generator (the survey's recipe: seeds seed0 + i, the matrices the golden runs
+    pin), each moved to `dev` as soon as it is made; the rest from the device generator (seeded
+    by seed0), so start-up does not grow with B or with the number of ranks sharing the host."""
     out = torch.empty((B, wl["m"], wl["n"]), dtype=torch.float16, device=dev)
-    for i in range(B):
+    host = min(host, B)
+    for i in range(host):
         out[i].copy_(synth_W(wl, seed0 + i))
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed0 + 0x5EED)
+    for i in range(host, B):
+        out[i].copy_(torch.randn((wl["m"], wl["n"]), generator=g, device=dev) * 0.02)
     return out
 
 
@@ -332,7 +342,11 @@ def main():
     qp = make_params(wl)
     ep = EngineParams.from_caldera_params(qp)
     B = args.batch or wl["batch"]
-    Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev)
+    # rank 0 holds the pinned seeds (parity_timed_step); other ranks' batches come from the
+    # device generator only, and each rank's host threads are capped at its share of the cores
+    if world > 1:
+        torch.set_num_threads(max(1, torch.get_num_threads() // world))
+    Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev, host=PINNED if rank == 0 else 0)
     h = make_h(wl)
     h = None if h is None else h.to(dev)
     parts = max(1, args.streams or 1)

@@ -116,6 +116,7 @@ _SIGS = {
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64, c_int]),
+    "cq_q_update_list_geometry": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp]),
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
@@ -724,8 +725,13 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         inv = 1.0 / (sL * sR)
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
-    # the candidate lists make this workspace ~m n / 2 bytes per matrix: cached (scratch.py)
-    hint = scale_hint is not None and r > 0
+    # the hint only matters to the 2-bit packed path on fp16 W (the C side ignores it
+    # otherwise): only then is the list workspace (~1.1 B per element: a quarter of the
+    # 8-element groups x 36 B) sized and cached (scratch.py)
+    hint = (scale_hint is not None and r > 0 and bits == 2 and packed is not None and codes is None
+            and W.dtype == torch.float16)
+    if not hint:
+        scale_hint = None
     ws = scratch.get("q_update.ws_list" if hint else "q_update.ws",
                      (max(int(lib.cq_q_update_workspace(m, n, B, int(hint))), 16),), torch.uint8, dev)
     if events is not None:  # HIP events around the quantise kernels only (bench roofline)
@@ -736,6 +742,15 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
            "cq_q_update_x3")
     if events is not None:
         events[1].record()
+
+
+def q_update_list_geometry(m: int, n: int, r: int):
+    """(rows of W per list region, list capacity in 8-element groups per region) of the 2-bit
+    single-recompute Q update (cq_q_update_list_geometry), or None where it does not apply."""
+    rows, cap = ctypes.c_int64(0), ctypes.c_int64(0)
+    if load().cq_q_update_list_geometry(m, n, r, ctypes.byref(rows), ctypes.byref(cap)) != 0:
+        return None
+    return int(rows.value), int(cap.value)
 
 
 def absmax(X: torch.Tensor) -> torch.Tensor:

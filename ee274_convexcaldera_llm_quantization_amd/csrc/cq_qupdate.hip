@@ -523,7 +523,9 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
     if (PASS == 2) {
         if (lane == 0) {
-            q.cnt[region] = (uint32_t)(gcur < q.cap ? gcur : q.cap + 1);
+            // gcur == cap: every listed group got a slot (pos < cap) -- a full list, not an
+            // overflow; past cap the count is clamped and the matrix falls back to pass 1
+            q.cnt[region] = (uint32_t)(gcur <= q.cap ? gcur : q.cap);
             if (gcur > q.cap) q.ovf[b] = 1u;
         }
         __shared__ double red2[16];

@@ -67,7 +67,9 @@ struct QUK {
 };
 
 constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
-constexpr int QP_CAP_DIV = 2;             // list capacity: 1 / 2 of a wave region's 8-element groups
+// list capacity: 1 / 4 of a wave region's 8-element groups (~12 % are candidates at config 2:
+// 2x margin; a region past it overflows and its matrix takes the second recompute)
+constexpr int QP_CAP_DIV = 4;
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
 constexpr int QP_KMAX = 256;              // row-panel Q update: largest r

@@ -1337,6 +1337,16 @@ size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint)
            (with_hint ? qu_cand_bytes(m, n, batch) : 0);
 }
 
+int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out) {
+    CQ_REQUIRE(rows_out && cap_out, "cq_q_update_list_geometry: null argument");
+    if (!(r > 0 && r % XW_BK == 0 && qp_cand_ok(m, n, (int)r)))
+        return set_error(CQ_EINVAL, "cq_q_update_list_geometry: (m, n, r) do not take the list path");
+    const int rpw = qp_cand_rows((int)r);
+    qu_cand_geom(m, n, 1, rpw, nullptr, cap_out);
+    *rows_out = rpw;
+    return CQ_OK;
+}
+
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
                    const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl, const float* inv_scale, int bits,
                    float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w, double* err_out,

@@ -254,7 +254,9 @@ class BatchState:
                     continue
                 sel = [b for b in range(self.B) if picks[b] == v]
                 idx = torch.tensor(sel, dtype=torch.long, device=qc.device)
-                src = self._vers[v]
+                # version 0 (never picked: the initial zero state) takes the picked snapshots'
+                # shapes -- its own L / R have width rank, an LR update's min(rank, m, n)
+                src = self._vers[v] if v else (*[torch.zeros_like(t) for t in out], None)
                 for d, s in zip(out, src[:4]):
                     d.index_copy_(0, idx, s.index_select(0, idx))
                 if oidx is not None and src[4] is not None:
@@ -876,6 +878,10 @@ class CalderaEngine:
             W = W.unsqueeze(0)
         B, m, n = W.shape
         dev = W.device
+        # every run starts cold: a reused engine's results do not depend on its earlier runs
+        # (the solver's warm start, shape and buffers belong to one run)
+        self.solver = None
+        self._qfb = None
         if W.dtype not in (torch.float16, torch.float32):
             W = W.float()
         pad = (-n) % 4

@@ -234,6 +234,9 @@ class RankRSolver:
             # large work buffers: cached scratch (scratch.py), reused by later solves
             f32, f16 = torch.float32, torch.float16
             self._bufs = [scratch.get(f"solver.blk{i}", (B, k, p), f32, dev) for i in range(5)]
+            # the warm start of an earlier solve may be one of the cached blocks (the final
+            # swap below): it must not also serve as scratch
+            self._bufs = [torch.empty_like(t) if t is self.X else t for t in self._bufs]
             # fp32 G only for the fp32 products (the split-fp16 path keeps G as its halves and
             # allocates it on an fp16 overflow fallback)
             self._G = None if self.x3 else torch.empty((B, k, k), dtype=f32, device=dev)
@@ -660,7 +663,9 @@ class RankRSolver:
         # the final block becomes the warm start by a swap with the pool (no copy): X's pool
         # slot takes the previous warm-start buffer (a fresh one on the first call)
         i = next(j for j, t in enumerate(self._bufs) if t is X)
-        old = self.X if self.X is not None else torch.empty((B, k, p), dtype=torch.float32, device=dev)
+        old = self.X
+        if old is None or any(t is old for t in self._bufs):  # never two pool slots on one tensor
+            old = torch.empty((B, k, p), dtype=torch.float32, device=dev)
         self._bufs[i], self.X = old, X
         self.theta = theta.clone()
         self._ends = ends

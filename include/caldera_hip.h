@@ -383,6 +383,11 @@ int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_
  * scales are those of the two-pass form bit for bit; err_out sums the same fp32 terms in
  * another order (~1e-8 relative). */
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint);
+/* Geometry of the single-recompute list path for rank r: rows of W per list region
+ * (*rows_out) and list capacity in 8-element groups per region (*cap_out); a region with
+ * more candidate groups than that overflows and its matrix takes the second recompute.
+ * Returns 0, or CQ_EINVAL when (m, n, r) do not take the list path. */
+int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out);
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
                    const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
                    const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,

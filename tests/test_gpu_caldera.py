@@ -172,6 +172,28 @@ def test_stream_split_matches_single_stream():
         assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qa)) < 1e-4
 
 
+def test_engine_reuse_is_stateless():
+    """One CalderaEngine run twice on the same batch, then on another shape, then a third time
+    on the first: every run starts cold (its own solver and warm start), so the repeated runs
+    give the first run's results bit for bit (the solver's block pool survives the reuse)."""
+    from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
+    ep = EngineParams(Q_bits=2, L_bits=16, R_bits=16, rank=32, iters=3, update_order=["Q", "LR"], sigma_reg=1e-8)
+    g = torch.Generator().manual_seed(17)
+    W1 = (torch.randn(2, 512, 1024, generator=g) * 0.02).half().to(DEV)
+    W2 = (torch.randn(3, 384, 512, generator=g) * 0.02).half().to(DEV)
+    eng = CalderaEngine(ep)
+    a = eng.run(W1)
+    a = [(d["Q_idxs"].clone(), d["L"].clone(), d["R"].clone(), d["errors"]) for d in a]
+    b = eng.run(W1)
+    c = eng.run(W2)
+    assert len(c) == 3 and c[0]["L"].shape == (384, 32)
+    d3 = eng.run(W1)
+    for out in (b, d3):
+        for (qa, la, ra, ea), d in zip(a, out):
+            assert torch.equal(qa, d["Q_idxs"]) and torch.equal(la, d["L"]) and torch.equal(ra, d["R"])
+            assert ea == d["errors"]
+
+
 @pytest.mark.parametrize("prec", ["f16x3", "f32", "overflow"])
 def test_solver_filter_precisions(prec, monkeypatch):
     """Top-r eigenpairs of Y Y^T from the split-fp16 filter, the fp32 filter, and the fp32

@@ -33,6 +33,49 @@ def test_q_update_matches_round2_kernel(case):
 LIST_CASES = [c for c in C.CASES if c[5] == 2 and c[6] == torch.float16]
 
 
+@pytest.mark.parametrize("extra", [-1, 0, 1], ids=["cap-1", "cap", "cap+1"])
+def test_q_update_list_at_capacity(extra):
+    """A list region holding exactly its capacity of candidate groups is complete (no
+    fallback) and one more overflows (fallback to the second recompute); both give the
+    two-pass codes bit for bit.  Region 0 of matrix 0 gets cap + extra planted groups, region 1
+    a few, so a count one past the filled slots would read region 1's first entry."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    dev = torch.device("cuda:0")
+    B, n, r = 2, 64, 32
+    rows, cap = K.q_update_list_geometry(8 * 48, n, r)
+    m = 8 * rows                          # one panel of 8 wave regions
+    g = torch.Generator().manual_seed(4242)
+    W = torch.randn(B, m, n, generator=g) * 0.01
+    groups = [(i, 8 * c) for i in range(rows) for c in range(n // 8)]   # (row, first column) of region 0
+    assert len(groups) >= cap + 1
+    pick = torch.randperm(len(groups), generator=g)[: cap + extra].tolist()
+    for t, j in enumerate(pick):          # one element >= 0.5 per planted group; the first is the absmax
+        i, c0 = groups[j]
+        W[0, i, c0 + t % 8] = 1.0 if t == 0 else (0.5 + 0.4 * torch.rand((), generator=g)) * (1 if t % 3 else -1)
+    for t in range(5):                    # region 1
+        W[0, rows + 3 * t, 8 * t % n] = 0.7
+    W[1, 5, 9] = 1.0
+    W = W.half().to(dev)
+    L = (torch.randn(B, m, r, generator=g) * 1e-3).to(dev)
+    R = (torch.randn(B, r, n, generator=g) * 1e-3).to(dev)
+
+    def call(hint):
+        packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=dev)
+        scale = torch.empty(B, device=dev)
+        err = torch.empty(B, dtype=torch.float64, device=dev)
+        fb = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=hint, fallback_out=fb)
+        torch.cuda.synchronize()
+        return packed.cpu(), scale.cpu(), err.cpu(), fb.cpu()
+
+    p0, s0, e0, _ = call(None)
+    p, s, e, fb = call(s0.to(dev))
+    assert fb.tolist() == [int(cap + extra > cap), 0], (cap, extra, fb.tolist())
+    assert torch.equal(p, p0) and torch.equal(s, s0)
+    for i in range(B):
+        assert abs(e[i].item() - e0[i].item()) <= 1e-7 * e0[i].item()
+
+
 @pytest.mark.parametrize("weighted", [False, True], ids=["unit", "err_w"])
 @pytest.mark.parametrize("case", LIST_CASES, ids=[c[0] for c in LIST_CASES])
 def test_q_update_single_recompute_matches_two_pass(case, weighted):
