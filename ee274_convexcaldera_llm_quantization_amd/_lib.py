@@ -128,6 +128,11 @@ _SIGS = {
                               c_vp]),
     "cq_sgram_combine": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp]),
+    "cq_codes_transpose": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "cq_codes_matmul": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                c_i64, c_int, c_vp]),
+    "cq_codes_ysq_corr": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "cq_transpose_f16": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_product_error": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
@@ -779,6 +784,60 @@ def sgram_fill(packed, k, L, row_nnz, perm, slice_off, ell, stride):
     assert ell.numel() >= B * stride
     _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), stride, _p(ell),
                                 _stream(packed.device)), "cq_sgram_fill")
+
+
+def codes_transpose(packed, rows, cols, out=None):
+    """2-bit packed codes (B, rows*cols/4) -> the packed codes of the transposes (B, cols*rows/4)."""
+    _require_hip(packed, out)
+    B = packed.shape[0]
+    assert packed.dtype == torch.uint8 and packed.is_contiguous() and packed.numel() == B * rows * cols // 4
+    if out is None:
+        out = torch.empty_like(packed)
+    assert out.shape == packed.shape and out.is_contiguous() and out.data_ptr() != packed.data_ptr()
+    _check(load().cq_codes_transpose(_p(packed), 2, B, rows, cols, _p(out), _stream(packed.device)),
+           "cq_codes_transpose")
+    return out
+
+
+def codes_matmul(packed, rows, cols, X, r, out, *, colw=None, roww=None, trans=False):
+    """out[b] = diag(roww) c[b] diag(colw) X[b][:, :r] (rows x r; trans: its transpose, r x rows) for
+    2-bit packed codes c (B, rows, cols) and X (B, cols, ldx) fp32 (cq_codes_matmul)."""
+    _require_hip(packed, X, colw, roww, out)
+    assert roww is None or (roww.numel() == rows and roww.dtype == torch.float32 and roww.is_contiguous())
+    B = packed.shape[0]
+    assert packed.numel() == B * rows * cols // 4 and X.shape[:2] == (B, cols) and X.stride(2) == 1
+    assert X.dtype == torch.float32 and out.dtype == torch.float32 and out.is_contiguous()
+    assert out.shape == ((B, r, rows) if trans else (B, rows, r))
+    assert colw is None or (colw.numel() == cols and colw.dtype == torch.float32 and colw.is_contiguous())
+    _check(load().cq_codes_matmul(_p(packed), 2, B, rows, cols, _p(X), X.stride(1), X.stride(0), _p(colw), _p(roww), r, _p(out),
+                                  out.shape[2], out.stride(0), int(bool(trans)), _stream(packed.device)),
+           "cq_codes_matmul")
+    return out
+
+
+def codes_ysq_corr(packed, W, qscale, colw=None, out=None):
+    """(B,) fp64: ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2 (colw = ycol^2) over the nonzero
+    2-bit codes c of W (B, m, n) fp16 (cq_codes_ysq_corr)."""
+    _require_hip(packed, W, qscale, colw, out)
+    B, m, n = W.shape
+    assert W.dtype == torch.float16 and W.is_contiguous() and packed.numel() == B * m * n // 4
+    if out is None:
+        out = torch.empty(B, dtype=torch.float64, device=W.device)
+    _check(load().cq_codes_ysq_corr(_p(packed), 2, _p(W), CQ_F16, _p(qscale), _p(colw), B, m, n, _p(out),
+                                    _stream(W.device)), "cq_codes_ysq_corr")
+    return out
+
+
+def transpose_f16(X, out=None):
+    """(B, rows, cols) fp16 -> (B, cols, rows) (cq_transpose_f16)."""
+    _require_hip(X, out)
+    B, rows, cols = X.shape
+    assert X.dtype == torch.float16 and X.is_contiguous()
+    if out is None:
+        out = torch.empty((B, cols, rows), dtype=torch.float16, device=X.device)
+    assert out.shape == (B, cols, rows) and out.is_contiguous()
+    _check(load().cq_transpose_f16(_p(X), B, rows, cols, _p(out), _stream(X.device)), "cq_transpose_f16")
+    return out
 
 
 def sgram_rows(L: int) -> int:

@@ -574,11 +574,270 @@ __global__ __launch_bounds__(256) void sgram_combine_kernel(const float* __restr
     }
 }
 
+// ------------------------------------------------------------------ packed-code helpers
+// Packed 2-bit code matrices: offset binary (field = c + 1), 16 codes per little-endian 32-bit
+// word, code u of a word at bits 8 (u / 4) + 6 - 2 (u % 4) (bytes MSB-first).
+
+__device__ __forceinline__ uint32_t sg_put(uint32_t f, int u) { return f << (8 * (u >> 2) + 6 - 2 * (u & 3)); }
+// code index u of the field whose low bit is at bit position p (p even)
+__device__ __forceinline__ int sg_u_of_bit(int p) { return 4 * (p >> 3) + ((6 - (p & 7)) >> 1); }
+
+// Transpose of packed 2-bit codes (rows x cols -> cols x rows), a tile of 256 x 256 codes per
+// workgroup: thread (i, j) loads the 16 x 16 block of input rows 16 i.., word j (16 lanes read a
+// row's 64 contiguous bytes), transposes it in registers and parks the 16 output words in LDS;
+// then thread q writes output row q's 16 words of the tile (64 contiguous bytes).
+__global__ __launch_bounds__(256) void codes_transpose_kernel(const uint32_t* __restrict__ in, int64_t rows,
+                                                              int64_t cols, uint32_t* __restrict__ out) {
+    __shared__ uint32_t t[256][17];
+    const int64_t b = blockIdx.z;
+    const int64_t wr = cols / 16, wc = rows / 16;   // words per input / output row
+    const int64_t r0 = (int64_t)blockIdx.y * 256, c0 = (int64_t)blockIdx.x * 256;
+    const int tid = threadIdx.x, i = tid >> 4, j = tid & 15;
+    const int64_t ir = r0 + 16 * i, iw = c0 / 16 + j;
+    if (ir < rows && iw < wr) {
+        const uint32_t* src = in + b * rows * wr + ir * wr + iw;
+        uint32_t w[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[r] = src[r * wr];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o |= sg_put(sg_field(w[r], u), r);
+            t[16 * j + u][i] = o;   // output row c0 + 16 j + u, word r0 / 16 + i
+        }
+    }
+    __syncthreads();
+    const int64_t orow = c0 + tid;
+    if (orow < cols) {
+        uint32_t* dst = out + b * cols * wc + orow * wc + r0 / 16;
+        const int64_t nwv = wc - r0 / 16 < 16 ? wc - r0 / 16 : 16;
+        if (nwv == 16 && (wc & 3) == 0) {   // 16-byte aligned rows
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<uint4*>(dst + 4 * q) = make_uint4(t[tid][4 * q], t[tid][4 * q + 1], t[tid][4 * q + 2],
+                                                                    t[tid][4 * q + 3]);
+        } else {
+            for (int q = 0; q < nwv; ++q) dst[q] = t[tid][q];
+        }
+    }
+}
+
+// out[row, :] = sum over the nonzero codes c (col) of row `row` of c w[col] X[col, :] (X: cols x r,
+// row stride ldx; w NULL = 1), times roww[row] if given: the sparse-code product of the LR step
+// (U^T c, c V).  One wave per
+// row: the row's nonzero codes are compacted into a per-wave LDS list (one pass over its words,
+// in increasing word order), then consumed 8 at a time with the X-row loads of all 8 in flight;
+// lane l owns r-values l, l + 64, ...  TRANS: out is r x rows (ld ldo), written through an LDS
+// tile of the workgroup's 64 rows (coalesced over rows); else rows x r.
+constexpr int CM_LIST = 1024;
+template <int RV, bool TRANS>
+__global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __restrict__ packed, int64_t rows,
+                                                           int64_t cols, const float* __restrict__ X, int64_t ldx,
+                                                           int64_t sx, const float* __restrict__ w,
+                                                           const float* __restrict__ roww, int r,
+                                                           float* __restrict__ out, int64_t ldo, int64_t so) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cm_lds[];
+    uint32_t* list = cm_lds + (threadIdx.x >> 6) * CM_LIST;
+    float* tile = reinterpret_cast<float*>(cm_lds + 4 * CM_LIST);   // TRANS: [r][65]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t b = blockIdx.y, row0 = (int64_t)blockIdx.x * 64;
+    const int64_t nw = cols / 16;
+    const uint32_t* pb = packed + b * rows * nw;
+    const float* Xb = X + b * sx;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int q = 0; q < 16; ++q) {
+        const int lr = wv * 16 + q;
+        const int64_t row = row0 + lr;
+        float acc[RV];
+#pragma unroll
+        for (int k = 0; k < RV; ++k) acc[k] = 0.f;
+        auto consume = [&](int cnt) {
+            for (int t0 = 0; t0 < cnt; t0 += 8) {
+                float cv[8], xv[8][RV];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t en = t0 + e < cnt ? list[t0 + e] : 1u;   // padding: code 0
+                    const int64_t col = en >> 2;
+                    cv[e] = (float)((int)(en & 3u) - 1);
+                    if (w && t0 + e < cnt) cv[e] *= w[col];
+                    const float* xr = Xb + col * ldx;
+#pragma unroll
+                    for (int k = 0; k < RV; ++k) xv[e][k] = (lane + 64 * k < r) ? xr[lane + 64 * k] : 0.f;
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+#pragma unroll
+                    for (int k = 0; k < RV; ++k) acc[k] = __builtin_fmaf(cv[e], xv[e][k], acc[k]);
+            }
+        };
+        if (row < rows) {
+            const uint32_t* pr = pb + row * nw;
+            int cnt = 0;
+            for (int64_t w0 = 0; w0 < nw; w0 += 64) {
+                const int64_t wi = w0 + lane;
+                const uint32_t word = wi < nw ? pr[wi] : 0x55555555u;
+                uint32_t nz = sg_nz_mask(word);
+                const int c = __builtin_popcount(nz);
+                int pre = 0, tot = 0;
+#pragma unroll
+                for (int bt = 0; bt < 5; ++bt) {
+                    const uint64_t mk = __ballot((c >> bt) & 1);
+                    pre += __popcll(mk & lt) << bt;
+                    tot += __popcll(mk) << bt;
+                }
+                if (cnt + tot > CM_LIST) {   // list full: consume it first (tot <= 1024 = CM_LIST)
+                    __builtin_amdgcn_wave_barrier();
+                    consume(cnt);
+                    __builtin_amdgcn_wave_barrier();
+                    cnt = 0;
+                }
+                int pos = cnt + pre;
+                while (nz) {
+                    const int p = __builtin_ctz(nz);
+                    nz &= nz - 1u;
+                    list[pos++] = (uint32_t)((16 * wi + sg_u_of_bit(p)) << 2) | ((word >> p) & 3u);
+                }
+                cnt += tot;
+            }
+            __builtin_amdgcn_wave_barrier();
+            consume(cnt);
+            __builtin_amdgcn_wave_barrier();
+            if (roww) {
+                const float rw = roww[row];
+#pragma unroll
+                for (int k = 0; k < RV; ++k) acc[k] *= rw;
+            }
+        }
+        if constexpr (TRANS) {
+#pragma unroll
+            for (int k = 0; k < RV; ++k)
+                if (lane + 64 * k < r) tile[(lane + 64 * k) * 65 + lr] = acc[k];
+        } else if (row < rows) {
+            float* o = out + b * so + row * ldo;
+#pragma unroll
+            for (int k = 0; k < RV; ++k)
+                if (lane + 64 * k < r) o[lane + 64 * k] = acc[k];
+        }
+    }
+    if constexpr (TRANS) {
+        __syncthreads();
+        for (int64_t e = threadIdx.x; e < (int64_t)r * 64; e += 256) {
+            const int64_t idx = e / 64, lr = e % 64;
+            if (row0 + lr < rows) out[b * so + idx * ldo + row0 + lr] = tile[idx * 65 + lr];
+        }
+    }
+}
+
+// per matrix: the part of ||(W - s c) diag(ycol)||_F^2 that the nonzero codes add to
+// ||W diag(ycol)||_F^2, sum over them of w[col] (s^2 - 2 s c W[row, col]) (w = ycol^2, NULL = 1),
+// in fp64 in a fixed order (wave wv: rows wv, wv + 16, ...; fixed reduction): deterministic
+__global__ __launch_bounds__(1024) void codes_ysq_corr_kernel(const uint32_t* __restrict__ packed,
+                                                              const _Float16* __restrict__ W,
+                                                              const float* __restrict__ qscale,
+                                                              const float* __restrict__ w, int64_t rows,
+                                                              int64_t cols, double* __restrict__ out) {
+    __shared__ double red[16];
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double s = (double)qscale[b];
+    const int64_t nw = cols / 16;
+    const uint32_t* pb = packed + b * rows * nw;
+    const _Float16* Wb = W + b * rows * cols;
+    double acc = 0.0;
+    for (int64_t row = wv; row < rows; row += 16) {
+        for (int64_t wi = lane; wi < nw; wi += 64) {
+            const uint32_t word = pb[row * nw + wi];
+            uint32_t nz = sg_nz_mask(word);
+            while (nz) {
+                const int p = __builtin_ctz(nz);
+                nz &= nz - 1u;
+                const int64_t col = 16 * wi + sg_u_of_bit(p);
+                const double c = (double)((int)((word >> p) & 3u) - 1);
+                const double x = (double)(float)Wb[row * cols + col];
+                const double t = s * s - 2.0 * s * c * x;
+                acc += w ? (double)w[col] * t : t;
+            }
+        }
+    }
+    const double tot = block_sum_f64(acc, red);
+    if (threadIdx.x == 0) out[b] = tot;
+}
+
+// Y = X^T for fp16 (batch x rows x cols -> batch x cols x rows), 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void transpose_f16_kernel(const uint16_t* __restrict__ in, int64_t rows, int64_t cols,
+                                                            uint16_t* __restrict__ out) {
+    __shared__ uint16_t t[64][66];
+    const int64_t b = blockIdx.z, r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const uint16_t* src = in + b * rows * cols;
+    for (int i = ty; i < 64; i += 4)
+        if (r0 + i < rows && c0 + tx < cols) t[i][tx] = src[(r0 + i) * cols + c0 + tx];
+    __syncthreads();
+    uint16_t* dst = out + b * rows * cols;
+    for (int i = ty; i < 64; i += 4)
+        if (c0 + i < cols && r0 + tx < rows) dst[(c0 + i) * rows + r0 + tx] = t[tx][i];
+}
+
 }  // namespace cq
 
 using namespace cq;
 
 extern "C" {
+
+int cq_codes_transpose(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, uint8_t* out,
+                       void* stream) {
+    CQ_REQUIRE(packed && out, "cq_codes_transpose: null argument");
+    CQ_REQUIRE(bits == 2, "cq_codes_transpose: 2-bit codes only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0 && rows % 16 == 0 && cols % 16 == 0,
+               "cq_codes_transpose: bad shape (rows, cols multiples of 16)");
+    const dim3 grid((unsigned)ceil_div(cols, 256), (unsigned)ceil_div(rows, 256), (unsigned)batch);
+    codes_transpose_kernel<<<grid, 256, 0, as_stream(stream)>>>(reinterpret_cast<const uint32_t*>(packed), rows,
+                                                                cols, reinterpret_cast<uint32_t*>(out));
+    return check_launch("cq_codes_transpose");
+}
+
+int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, const float* X,
+                    int64_t ldx, int64_t stride_x, const float* colw, const float* roww, int64_t r, float* out,
+                    int64_t ldo, int64_t stride_out, int trans, void* stream) {
+    CQ_REQUIRE(packed && X && out, "cq_codes_matmul: null argument");
+    CQ_REQUIRE(bits == 2, "cq_codes_matmul: 2-bit codes only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0 && cols % 16 == 0 && cols < (1ll << 29),
+               "cq_codes_matmul: bad shape");
+    CQ_REQUIRE(r > 0 && r <= 256 && ldx >= r, "cq_codes_matmul: r must be in 1..256 and <= ldx");
+    const dim3 grid((unsigned)ceil_div(rows, 64), (unsigned)batch);
+    const size_t lds = 4 * CM_LIST * sizeof(uint32_t) + (trans ? (size_t)r * 65 * sizeof(float) : 0);
+    hipStream_t s = as_stream(stream);
+    const uint32_t* pk = reinterpret_cast<const uint32_t*>(packed);
+#define CQ_CM(RV, T) codes_matmul_kernel<RV, T><<<grid, 256, lds, s>>>(pk, rows, cols, X, ldx, stride_x, colw, roww, (int)r, \
+                                                                       out, ldo, stride_out)
+    const int rv = (int)ceil_div(r, 64);
+    if (trans) {
+        if (rv == 1) CQ_CM(1, true); else if (rv == 2) CQ_CM(2, true); else if (rv == 3) CQ_CM(3, true); else CQ_CM(4, true);
+    } else {
+        if (rv == 1) CQ_CM(1, false); else if (rv == 2) CQ_CM(2, false); else if (rv == 3) CQ_CM(3, false); else CQ_CM(4, false);
+    }
+#undef CQ_CM
+    return check_launch("cq_codes_matmul");
+}
+
+int cq_codes_ysq_corr(const uint8_t* packed, int bits, const void* W, int dtype, const float* qscale, const float* colw,
+                      int64_t batch, int64_t rows, int64_t cols, double* out, void* stream) {
+    CQ_REQUIRE(packed && W && qscale && out, "cq_codes_ysq_corr: null argument");
+    CQ_REQUIRE(bits == 2 && dtype == CQ_F16, "cq_codes_ysq_corr: 2-bit codes, fp16 W only");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0 && cols % 16 == 0, "cq_codes_ysq_corr: bad shape");
+    codes_ysq_corr_kernel<<<(unsigned)batch, 1024, 0, as_stream(stream)>>>(
+        reinterpret_cast<const uint32_t*>(packed), reinterpret_cast<const _Float16*>(W), qscale, colw, rows, cols, out);
+    return check_launch("cq_codes_ysq_corr");
+}
+
+int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t cols, uint16_t* Y, void* stream) {
+    CQ_REQUIRE(X && Y && X != Y, "cq_transpose_f16: null or aliased argument");
+    CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0, "cq_transpose_f16: bad shape");
+    const dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64), (unsigned)batch);
+    transpose_f16_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, rows, cols, Y);
+    return check_launch("cq_transpose_f16");
+}
 
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
                    int32_t* perm, int64_t* slice_off, int64_t* total, void* stream) {

@@ -276,6 +276,10 @@ class CalderaEngine:
         self.p = params
         self.solver_kwargs = dict(solver_kwargs or {})
         self.solver_tol = solver_tol
+        # tolerances of the first LR updates (then solver_tol): the codes of the next Q update
+        # are decided on the L R of the one before it (alg.py:262), see DESIGN.md §6
+        self.solver_tol_steps = None
+        self._lr_step = 0
         self.solver_p = solver_p
         self.filter_precision = filter_precision
         self.profile = profile
@@ -286,6 +290,7 @@ class CalderaEngine:
         self.lplr_fused_err = True   # LPLR error from the normal-equation pieces (False: error GEMM)
         self.lplr_x3 = True          # LPLR m x n x r products on split-fp16 MFMAs where the halves exist
         self.sparse_gram = True      # G from the sparse 2-bit codes where it applies (sgram.py)
+        self.r_from_codes = True     # with it, R = U^T W - s U^T c and ||Y||^2 without a residual pass
         self.lplr_trace = None       # list -> per-LPLR-iteration errors are appended (diagnostics)
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
@@ -419,16 +424,23 @@ class CalderaEngine:
             # weighted space; the caller compares Q + L R unweighted, where the columns with
             # small h_j amplify it (2.4-4.5x at main.py's real Hessians, tools/crit_probe.py):
             # weighted problems run to a 4x tighter test
-            tol = self.solver_tol if (weighted is False) else self.solver_tol * WEIGHTED_TOL_FACTOR
-            self.solver = RankRSolver(B, m, n, p.rank, dev, tol=tol, p=self.solver_p,
+            self.solver = RankRSolver(B, m, n, p.rank, dev, tol=self.solver_tol, p=self.solver_p,
                                       filter_precision=self.filter_precision, **self.solver_kwargs)
             if not self.solver.left and self._n_true < n:
                 self.solver.valid_k = self._n_true
         sv = self.solver
+        if isinstance(sv, RankRSolver):
+            # per-LR-step tolerance (solver_tol_steps[i] for the i-th LR update, then
+            # solver_tol); weighted problems run to a tighter test (WEIGHTED_TOL_FACTOR)
+            steps = self.solver_tol_steps or ()
+            tol = steps[self._lr_step] if self._lr_step < len(steps) else self.solver_tol
+            sv.tol = tol if weighted is False else tol * WEIGHTED_TOL_FACTOR
+        self._lr_step += 1
         y_split = None
         gram = None
         ysq = None
         lplr_halves = None
+        self._r_lite = False
         if st.dense_q and st.has_Q:
             qsrc, qsc, qbits = st.Qd, st.Qbound, 32
         else:
@@ -458,11 +470,20 @@ class CalderaEngine:
             # Y's halves, which are then only written where another product reads them
             sparse_g = (self.sparse_gram and sv.left and st.has_Q and st.q_packed and not st.dense_q
                         and sgram.applicable(m, n, Ws, p.Q_bits, True, wts.dense))
+            # R = U^T Y without a residual pass (2-bit codes, unquantised factors): U^T (W diag(ycol))
+            # from W's transposed halves written once per run, minus s (U^T c) diag(ycol) from the
+            # sparse codes (cq_codes_matmul); ||Y||^2 = ||W diag(ycol)||^2 + the codes' correction
+            lite = sparse_g and x3_r and not x3_lplr and p.Q_bits == 2 and self.r_from_codes
             if sparse_g and self._sg_A is None:  # once per run: A = W diag(w) W^T
                 self._sg_A = scratch.get("sgram.A", (B, m, m), torch.float32, dev)
                 self._sg = sgram.SparseGram(B, m, n, dev)
                 self._sg_w = (wts.ycol * wts.ycol).contiguous() if weighted else None
                 sv._alloc(dev)
+                if lite:
+                    self._wth = scratch.get("lr.wth", (B, n, m), torch.float16, dev)
+                    self._wtl = scratch.get("lr.wtl", (B, n, m), torch.float16, dev)
+                    self._ysw = torch.empty(B, dtype=torch.float32, device=dev)
+                    self._wsq = torch.empty(B, dtype=torch.float64, device=dev)
                 # fp16 MFMA work: one product over the upper half (H = I: W's halves are W and 0),
                 # else the three split products; bytes: the operand halves read once, A written
                 nprod = 3.0 if weighted else 1.0
@@ -471,29 +492,36 @@ class CalderaEngine:
                 if gev is not None:
                     gev[0].record()
                 sgram.gram_A(Ws, wts.ycol if weighted else None, wts.ycol_max if weighted else 1.0, self._wmax,
-                             self._sg_A, sv._Gh, sv._Gl, X3_SCALE, self._yh, self._yl)
+                             self._sg_A, sv._Gh, sv._Gl, X3_SCALE, self._yh, self._yl,
+                             **(dict(ys=self._ysw, wth=self._wth, wtl=self._wtl, wsq=self._wsq) if lite else {}))
                 if gev is not None:
                     gev[1].record()
             if sparse_g and self._sg.count(st.Qc) > sgram.MAX_DENSITY * m * n:
                 sparse_g = False  # too many nonzero codes this step: dense Gram
-            halves = ({} if sparse_g and not x3_lplr else dict(hi=self._yh, lo=self._yl)) if sv.left else \
-                dict(thi=self._yh, tlo=self._yl)
-            if x3_r or x3_lplr:
-                if self._yth is None:
-                    self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
-                    self._ytl = scratch.get("lr.ytl", (B, n, m), torch.float16, dev)
-                halves.update(thi=self._yth, tlo=self._ytl)
-            # m > n: Y's own halves (K-blocked over n) for L = Y V on split-fp16 products
-            x3_yv = not sv.left and self.lplr_x3
-            if x3_yv:
-                if self._yrh is None:
-                    self._yrh = scratch.get("lr.yrh", (B, m, n), torch.float16, dev)
-                    self._yrl = scratch.get("lr.yrl", (B, m, n), torch.float16, dev)
-                halves.update(hi=self._yrh, lo=self._yrl)
-            K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
-                             ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
-                             res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
-                             scale=self._ys, sq=ysq, **halves)
+            lite = lite and sparse_g and self._wth is not None
+            self._r_lite = lite
+            if lite:
+                # no pass over Y at all: ||Y||^2 from ||W diag(ycol)||^2 and the nonzero codes
+                ysq = self._wsq + K.codes_ysq_corr(st.Qc, Ws, st.Qs, self._sg_w)
+            else:
+                halves = ({} if sparse_g and not x3_lplr else dict(hi=self._yh, lo=self._yl)) if sv.left else \
+                    dict(thi=self._yh, tlo=self._yl)
+                if x3_r or x3_lplr:
+                    if self._yth is None:
+                        self._yth = scratch.get("lr.yth", (B, n, m), torch.float16, dev)
+                        self._ytl = scratch.get("lr.ytl", (B, n, m), torch.float16, dev)
+                    halves.update(thi=self._yth, tlo=self._ytl)
+                # m > n: Y's own halves (K-blocked over n) for L = Y V on split-fp16 products
+                x3_yv = not sv.left and self.lplr_x3
+                if x3_yv:
+                    if self._yrh is None:
+                        self._yrh = scratch.get("lr.yrh", (B, m, n), torch.float16, dev)
+                        self._yrl = scratch.get("lr.yrl", (B, m, n), torch.float16, dev)
+                    halves.update(hi=self._yrh, lo=self._yrl)
+                K.residual_split(Ws, qsrc, qsc, qbits, self._wmax,
+                                 ycol=wts.ycol if weighted else None, ycol_max=wts.ycol_max if weighted else 1.0,
+                                 res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
+                                 scale=self._ys, sq=ysq, **halves)
             if sparse_g:
                 qc, qs, A, SG, w = st.Qc, st.Qs, self._sg_A, self._sg, self._sg_w
 
@@ -528,6 +556,8 @@ class CalderaEngine:
                 # R = (U^T Y) diag(1/sqrt(lam))   (alg.py:219-225); randomized: S Vh as returned
                 if rand:
                     R.copy_(sv.SVh)
+                elif self._r_lite:
+                    self._ut_w(sv, R, st, wts.ycol if weighted else None)
                 elif (y_split is not None or gram is not None) and self._yth is not None:
                     self._ut_y(sv, R)
                 else:
@@ -618,6 +648,24 @@ class CalderaEngine:
         K.gemm_x3(xh, xl, self._yrh, self._yrl, 1.0 / (self._ys * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
                   lda=p, M=r)
         K.transpose_split(Lt, out=L)
+
+    def _ut_w(self, sv, R, st, ycol):
+        """R~ = U^T Y = U^T (W diag(ycol)) - s (U^T c) diag(ycol) (m <= n, 2-bit Q = s c): the first
+        term a split-fp16 product of the block's transposed halves with (W diag(ycol))^T's halves
+        (written once per run by sgram.gram_A), the second from the codes' transpose by the sparse
+        product cq_codes_matmul, subtracted in the product's epilogue (gamma = -s)."""
+        X = sv.X  # (B, m, p), orthonormal columns
+        B, m, p = X.shape
+        r, n = R.shape[1], R.shape[2]
+        dev = X.device
+        xh, xl = sv.split_block_t(X)
+        ct = scratch.get("lr.codes_t", st.Qc.shape, torch.uint8, dev)
+        K.codes_transpose(st.Qc, m, n, out=ct)
+        utc = scratch.get("lr.utc", (B, r, n), torch.float32, dev)
+        K.codes_matmul(ct, n, m, X, r, utc, roww=ycol, trans=True)
+        inv = 1.0 / (self._ysw * X3_SCALE)
+        K.gemm_x3(xh, xl, self._wth, self._wtl, inv, R, a_blocked=True, b_blocked=True, lda=p, M=r, D=utc,
+                  gamma_v=-st.Qs)
 
     def _ut_y(self, sv, R):
         """R = U^T Y (U = the solver's Ritz block, first r columns; m <= n) as a split-fp16
@@ -882,6 +930,7 @@ class CalderaEngine:
         # (the solver's warm start, shape and buffers belong to one run)
         self.solver = None
         self._qfb = None
+        self._lr_step = 0
         if W.dtype not in (torch.float16, torch.float32):
             W = W.float()
         pad = (-n) % 4
@@ -916,6 +965,8 @@ class CalderaEngine:
         self._yh = self._yl = self._ys = None
         self._yth = self._ytl = None
         self._yrh = self._yrl = None
+        self._wth = self._wtl = self._ysw = self._wsq = None
+        self._r_lite = False
         if wts.dense:  # den = tr(W H W^T) (alg.py:298)
             self._etmp = torch.empty((B, m, n), dtype=torch.float32, device=dev)
             wf = torch.empty((B, m, n), dtype=torch.float32, device=dev)

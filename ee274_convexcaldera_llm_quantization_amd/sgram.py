@@ -29,14 +29,18 @@ def applicable(m: int, n: int, W: torch.Tensor, q_bits: int, packed: bool, dense
 
 
 def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch.Tensor, Gh, Gl, out_scale: float,
-           yh: torch.Tensor, yl: torch.Tensor):
+           yh: torch.Tensor, yl: torch.Tensor, ys=None, wth=None, wtl=None, wsq=None):
     """A (B, m, m) fp32 upper triangle = (W diag(ycol)) (W diag(ycol))^T on split-fp16 products
     (cq_gemm_x3 Gram of W's K-blocked halves, written into yh/yl (B, m, n); H = I makes them
-    exact, lo = 0).  Gh/Gl receive a split of A that the caller overwrites later."""
+    exact, lo = 0).  Gh/Gl receive a split of A that the caller overwrites later.  The same pass
+    can also write the halves of (W diag(ycol))^T (wth/wtl (B, n, m), K-blocked over m: the B
+    operand of R = U^T Y) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,)."""
     B, m, n = Ws.shape
     dev = Ws.device
-    ys = torch.empty(B, dtype=torch.float32, device=dev)
-    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=yl, scale=ys)
+    if ys is None:
+        ys = torch.empty(B, dtype=torch.float32, device=dev)
+    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=yl, thi=wth, tlo=wtl, scale=ys,
+                     sq=wsq)
     bound = torch.full((B,), 2.0 ** 60, dtype=torch.float64, device=dev)  # any bound >= max|A|: halves unused
     so = torch.empty(B, dtype=torch.float32, device=dev)
     io = torch.empty(B, dtype=torch.float32, device=dev)

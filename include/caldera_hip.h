@@ -363,6 +363,28 @@ int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_
                      const double* bound, float out_scale, uint16_t* Gh, uint16_t* Gl, float* scale_out,
                      float* inv_out, float* G32, void* stream);
 
+/* Sparse-code helpers of the LR step (cq_sgram.hip), for 2-bit packed codes c (batch x rows x
+ * cols, the layout above):
+ *   cq_codes_transpose: c^T (batch x cols x rows, same packing); rows, cols multiples of 16.
+ *     Lets the sparse-code Gram run on m > n shapes (G = Y^T Y from W^T and c^T) and the R step
+ *     read the codes by column.
+ *   cq_codes_matmul: out[b, i, :] = roww[i] sum_{j: c[b,i,j] != 0} c[b,i,j] colw[j] X[b, j, 0:r] (X
+ *     row stride ldx, matrix stride stride_x; colw, roww NULL = 1; r <= 256), row-major (ld ldo) or, with
+ *     trans, out[b] is r x rows (ld ldo).  Replaces the code part of R = U^T (W - Q) (alg.py:
+ *     219-225, via c^T: U^T c) and of L = Y V for m > n; fixed summation order (deterministic).
+ *   cq_codes_ysq_corr: out[b] = sum over the nonzero codes of colw[j] (s^2 - 2 s c W[b,i,j])
+ *     (fp64, s = qscale[b]): ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2 with colw = ycol^2,
+ *     the ||Y||_F^2 of alg.py:211 without a pass over Y.
+ *   cq_transpose_f16: Y[b] = X[b]^T for fp16 X (batch x rows x cols). */
+int cq_codes_transpose(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, uint8_t* out,
+                       void* stream);
+int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, const float* X,
+                    int64_t ldx, int64_t stride_x, const float* colw, const float* roww, int64_t r, float* out,
+                    int64_t ldo, int64_t stride_out, int trans, void* stream);
+int cq_codes_ysq_corr(const uint8_t* packed, int bits, const void* W, int dtype, const float* qscale,
+                      const float* colw, int64_t batch, int64_t rows, int64_t cols, double* out, void* stream);
+int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t cols, uint16_t* Y, void* stream);
+
 /* Fused Q update.  Replaces alg.py:253-283 (maybe_update_Q / update_Q_non_data_aware:
  * res = W - L@R, quantize_matrix) + quantization.py:244-269 (whole-matrix uniform quantise):
  * res is recomputed per tile from the split-fp16 halves of L (m x r) and R^T (n x r,

@@ -15,6 +15,7 @@ import numpy as np
 from conftest import GOLDEN
 
 _FX = None
+_EX = None
 
 
 def fixture():
@@ -24,18 +25,29 @@ def fixture():
     return _FX
 
 
+def exact_fixture():
+    """Final codes of config-2 seeds 0-15 with an exact (fp64) rank-r step and the reference's
+    fp32 Q step (tests/golden/gen_exact_codes.py): keys s<seed>_sha256 / _rowhash / _ties_*."""
+    global _EX
+    if _EX is None:
+        _EX = np.load(os.path.join(GOLDEN, "exact_codes_cfg2.npz"), allow_pickle=False)
+    return _EX
+
+
 def _rowhash(row):
     return int.from_bytes(hashlib.blake2b(row.tobytes(), digest_size=8).digest(), "little")
 
 
-def compare(tag, codes, m, n):
+def compare(tag, codes, m, n, fx=None):
     """codes: our final int8 codes (m*n, any array-like/tensor).  Returns a dict:
     sha_equal, rows_differing, rows_unexplained, flips (at near-ties, exact count),
-    max_flip_tie_dist (code units; 0 when no flip)."""
-    fx = fixture()
+    max_flip_tie_dist (code units; 0 when no flip).  fx: another fixture with the same keys
+    (exact_fixture(), tags s<seed>), default the reference's final codes."""
+    fx = fixture() if fx is None else fx
+    sha_key = tag + "_Q_idxs_sha256" if tag + "_Q_idxs_sha256" in fx.files else tag + "_sha256"
     c = np.ascontiguousarray(np.asarray(codes.cpu() if hasattr(codes, "cpu") else codes, dtype=np.int8)
                              .reshape(m, n))
-    out = {"sha_equal": hashlib.sha256(c.tobytes()).hexdigest() == str(fx[tag + "_Q_idxs_sha256"]),
+    out = {"sha_equal": hashlib.sha256(c.tobytes()).hexdigest() == str(fx[sha_key]),
            "rows_differing": 0, "rows_unexplained": 0, "flips": 0, "max_flip_tie_dist": 0.0}
     if out["sha_equal"]:
         return out
