@@ -731,8 +731,8 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
     # the hint only matters to the 2-bit packed path on fp16 W (the C side ignores it
-    # otherwise): only then is the list workspace (~1.1 B per element: a quarter of the
-    # 8-element groups x 36 B) sized and cached (scratch.py)
+    # otherwise): only then is the list workspace (~2.25 B per element: half of the 8-element
+    # groups x 36 B) sized and cached (scratch.py)
     hint = (scale_hint is not None and r > 0 and bits == 2 and packed is not None and codes is None
             and W.dtype == torch.float16)
     if not hint:

@@ -67,9 +67,11 @@ struct QUK {
 };
 
 constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
-// list capacity: 1 / 4 of a wave region's 8-element groups (~12 % are candidates at config 2:
-// 2x margin; a region past it overflows and its matrix takes the second recompute)
-constexpr int QP_CAP_DIV = 4;
+// list capacity: 1 / 2 of a wave region's 8-element groups.  Candidates (|res| >= 0.45 of the
+// absmax) are ~12 % of the groups at 4096^2 but ~31 % on a 320 x 544 matrix (the absmax of
+// fewer Gaussians sits lower); a region past it overflows and its matrix takes the second
+// recompute, so the margin is kept for small shapes (2.25 B of list per element)
+constexpr int QP_CAP_DIV = 2;
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
 constexpr int QP_KMAX = 256;              // row-panel Q update: largest r

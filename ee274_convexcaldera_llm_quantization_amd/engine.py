@@ -474,7 +474,37 @@ class CalderaEngine:
             # from W's transposed halves written once per run, minus s (U^T c) diag(ycol) from the
             # sparse codes (cq_codes_matmul); ||Y||^2 = ||W diag(ycol)||^2 + the codes' correction
             lite = sparse_g and x3_r and not x3_lplr and p.Q_bits == 2 and self.r_from_codes
-            if sparse_g and self._sg_A is None:  # once per run: A = W diag(w) W^T
+            # m > n (gate/up projections): the same sparse-code Gram on the transposed problem,
+            # G = Y^T Y = (W^T - s c^T)(W^T - s c^T)^T from W^T (once per run) and c^T (per step);
+            # unweighted Y and unquantised factors (L = W V - s c V from W's halves and the codes)
+            tall = (self.sparse_gram and not sv.left and st.has_Q and st.q_packed and not st.dense_q and not weighted
+                    and not quantized and p.Q_bits == 2 and self.r_from_codes
+                    and sgram.applicable(n, m, Ws, p.Q_bits, True, wts.dense))
+            if tall and self._sg_A is None:  # once per run: W^T, A = W^T W, W's halves, ||W||^2
+                self._wt16 = K.transpose_f16(Ws, out=scratch.get("sgram.wt", (B, n, m), torch.float16, dev))
+                self._sg_A = scratch.get("sgram.A", (B, n, n), torch.float32, dev)
+                self._sg = sgram.SparseGram(B, n, m, dev)
+                self._sg_w = None
+                sv._alloc(dev)
+                self._wth = scratch.get("lr.wth", (B, m, n), torch.float16, dev)
+                self._wtl = scratch.get("lr.wtl", (B, m, n), torch.float16, dev)
+                self._ysw = torch.empty(B, dtype=torch.float32, device=dev)
+                self._wsq = torch.empty(B, dtype=torch.float64, device=dev)
+                gev = GRAM_PROBE.start("gram_A", 1.0 * n * n * m * B, 2.0 * m * n * B + 4.0 * n * n * B)
+                if gev is not None:
+                    gev[0].record()
+                sgram.gram_A(self._wt16, None, 1.0, self._wmax, self._sg_A, sv._Gh, sv._Gl, X3_SCALE, self._yh,
+                             self._yl, ys=self._ysw, wth=self._wth, wtl=self._wtl, wsq=self._wsq)
+                if gev is not None:
+                    gev[1].record()
+            if tall:
+                ct = scratch.get("sgram.codes_t", st.Qc.shape, torch.uint8, dev)
+                K.codes_transpose(st.Qc, m, n, out=ct)
+                if self._sg.count(ct) > sgram.MAX_DENSITY * m * n:
+                    tall = False  # too many nonzero codes this step: dense Gram
+                else:
+                    sparse_g = lite = True
+            if sparse_g and not tall and self._sg_A is None:  # once per run: A = W diag(w) W^T
                 self._sg_A = scratch.get("sgram.A", (B, m, m), torch.float32, dev)
                 self._sg = sgram.SparseGram(B, m, n, dev)
                 self._sg_w = (wts.ycol * wts.ycol).contiguous() if weighted else None
@@ -496,11 +526,12 @@ class CalderaEngine:
                              **(dict(ys=self._ysw, wth=self._wth, wtl=self._wtl, wsq=self._wsq) if lite else {}))
                 if gev is not None:
                     gev[1].record()
-            if sparse_g and self._sg.count(st.Qc) > sgram.MAX_DENSITY * m * n:
+            if sparse_g and not tall and self._sg.count(st.Qc) > sgram.MAX_DENSITY * m * n:
                 sparse_g = False  # too many nonzero codes this step: dense Gram
             lite = lite and sparse_g and self._wth is not None
             self._r_lite = lite
             if lite:
+                self.lr_steps_from_codes += 1
                 # no pass over Y at all: ||Y||^2 from ||W diag(ycol)||^2 and the nonzero codes
                 ysq = self._wsq + K.codes_ysq_corr(st.Qc, Ws, st.Qs, self._sg_w)
             else:
@@ -523,10 +554,12 @@ class CalderaEngine:
                                  res=None if x3_r else res, Y=Y if (weighted and not x3_r) else None,
                                  scale=self._ys, sq=ysq, **halves)
             if sparse_g:
-                qc, qs, A, SG, w = st.Qc, st.Qs, self._sg_A, self._sg, self._sg_w
+                # tall: the Gram of Y^T's rows from W^T and the transposed codes
+                gw, qc = (self._wt16, ct) if tall else (Ws, st.Qc)
+                qs, A, SG, w = st.Qs, self._sg_A, self._sg, self._sg_w
 
                 def fill(Gh, Gl, gscale, ginv, G32=None):
-                    SG.gram(Ws, qc, qs, w, A, ysq, Gh, Gl, gscale, ginv, X3_SCALE, G32=G32, counted=True)
+                    SG.gram(gw, qc, qs, w, A, ysq, Gh, Gl, gscale, ginv, X3_SCALE, G32=G32, counted=True)
 
                 gram = dict(fill=fill, ysq=ysq)
             else:
@@ -585,7 +618,7 @@ class CalderaEngine:
             # (Pythagoras, V orthonormal) from the Y V product the factors need anyway
             pyth_right = (not quantized and not rand and not wts.dense and wts.ycol is None and wts.err_unit)
             if p.activation_aware_LR:
-                self._y_times_v(sv, Ysrc, V, L)      # Y V
+                self._y_times_v(sv, Ysrc, V, L, st)  # Y V
                 if pyth_right:
                     yv2 = K.weighted_sqsum(L, None, r)
                 K.scale_rc(L, colscale=inv, out=L)   # U = Y V / S
@@ -594,7 +627,7 @@ class CalderaEngine:
                     R = K.gemm(R.clone(), wts.Vinv, tb=True, C=R)
             else:
                 sq = torch.sqrt(S32)
-                self._y_times_v(sv, Ysrc, V, L)
+                self._y_times_v(sv, Ysrc, V, L, st)
                 if pyth_right:
                     yv2 = K.weighted_sqsum(L, None, r)
                 K.scale_rc(L, colscale=torch.where(tiny, torch.zeros_like(sq), 1.0 / sq.clamp_min(1e-30)), out=L)
@@ -632,11 +665,24 @@ class CalderaEngine:
         K.gemm(L, R, D=res, epi=K.EPI_WERR, w=wts.err, err_out=err)
         return err
 
-    def _y_times_v(self, sv, Ysrc, V, L):
+    def _y_times_v(self, sv, Ysrc, V, L, st=None):
         """L = Y V (m > n; V = the first r columns of the solver's Ritz block, n x r): from Y's
         K-blocked halves (written by cq_residual_split) as the split-fp16 product L^T = V^T Y^T
         (A = the block's transposed split, rows r of p), transposed into L; the fp32 MFMA GEMM
-        when the halves are not there."""
+        when the halves are not there.  Sparse-code step (self._r_lite): Y = W - s c, so
+        L^T = V^T W^T (W's halves, once per run) - s (c V)^T (cq_codes_matmul, in the epilogue)."""
+        if self._r_lite:
+            X = sv.X
+            B, n, p = X.shape
+            r, m = L.shape[2], L.shape[1]
+            xh, xl = sv.split_block_t(X)
+            cv = scratch.get("lr.utc", (B, r, m), torch.float32, L.device)
+            K.codes_matmul(st.Qc, m, n, X, r, cv, trans=True)
+            Lt = torch.empty((B, r, m), dtype=torch.float32, device=L.device)
+            K.gemm_x3(xh, xl, self._wth, self._wtl, 1.0 / (self._ysw * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
+                      lda=p, M=r, D=cv, gamma_v=-st.Qs)
+            K.transpose_split(Lt, out=L)
+            return
         if self._yrh is None or isinstance(sv, RandSVD) or sv.direct:
             K.gemm(Ysrc, V, C=L)
             return
@@ -931,6 +977,7 @@ class CalderaEngine:
         self.solver = None
         self._qfb = None
         self._lr_step = 0
+        self.lr_steps_from_codes = 0  # LR updates that took the sparse-code path (no residual pass)
         if W.dtype not in (torch.float16, torch.float32):
             W = W.float()
         pad = (-n) % 4
@@ -965,7 +1012,7 @@ class CalderaEngine:
         self._yh = self._yl = self._ys = None
         self._yth = self._ytl = None
         self._yrh = self._yrl = None
-        self._wth = self._wtl = self._ysw = self._wsq = None
+        self._wth = self._wtl = self._ysw = self._wsq = self._wt16 = None
         self._r_lite = False
         if wts.dense:  # den = tr(W H W^T) (alg.py:298)
             self._etmp = torch.empty((B, m, n), dtype=torch.float32, device=dev)

@@ -161,3 +161,31 @@ def test_sparse_gram_ell_order(k, L, dens):
             got = [int(el[b, (sob[s] + t) * 64 + p % 64]) for t in range(width)]
             want = exp[p] + [1] * (width - len(exp[p]))
             assert got == want, (b, p, got[:8], want[:8])
+
+
+@pytest.mark.parametrize("m,n,weighted", [(1024, 2048, False), (1024, 2048, True), (2048, 1024, False),
+                                          (1024, 1024, False)])
+def test_lr_step_from_codes_matches_residual_pass(m, n, weighted):
+    """The LR step without a pass over Y (R = U^T W - s U^T c, L = W V - s c V for m > n, and
+    ||Y||^2 from ||W||^2 plus the codes' correction; tall shapes through the sparse-code Gram of
+    W^T and c^T) against the same engine with the residual pass (r_from_codes off; for m > n
+    also the dense Gram): same first-Q codes, errors and Q + L R to the solver tolerance."""
+    from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
+    ep = EngineParams(Q_bits=2, L_bits=16, R_bits=16, rank=64, iters=3, update_order=["Q", "LR"], sigma_reg=1e-8)
+    g = torch.Generator().manual_seed(m + 3 * n + weighted)
+    W = (torch.randn(2, m, n, generator=g) * 0.02).half().to(DEV)
+    h = (torch.rand(n, generator=g) + 0.05).to(DEV) if weighted else None
+    outs, engs = [], []
+    for codes in (True, False):
+        e = CalderaEngine(ep)
+        e.r_from_codes = codes
+        outs.append(e.run(W, h))
+        engs.append(e)
+    assert engs[0].lr_steps_from_codes == 3 and engs[1].lr_steps_from_codes == 0
+    for a, b in zip(*outs):
+        assert torch.equal(a["Q_idxs"], b["Q_idxs"]) or (a["Q_idxs"] != b["Q_idxs"]).sum() <= 2
+        for k in ("Q", "LR"):
+            assert max(abs(x - y) for x, y in zip(a["errors"][k], b["errors"][k])) < 2e-6, (k, a["errors"], b["errors"])
+        qa = a["Q"].double() + a["L"].double() @ a["R"].double()
+        qb = b["Q"].double() + b["L"].double() @ b["R"].double()
+        assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qb)) < 2e-5
