@@ -8,6 +8,8 @@ timeout -k 10 300 python3 -u -m pytest tests/test_gpu_sgram.py tests/test_gpu_co
 rc=$?; echo "new tests rc=$rc"; tail -4 $O/new_tests.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -12 $O/gpu_tests.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 200 python3 -u tools/bench_qupdate_list.py 256 10 > $O/qupdate_list.log 2>&1 || exit $?
+tail -4 $O/qupdate_list.log
 timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
 tail -1 $O/bench.log | cut -c1-300
 for w in ${WORKLOADS:-cfg4t cfg3}; do
