@@ -102,6 +102,7 @@ _SIGS = {
     "cq_jacobi_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh": (c_int, [c_vp, c_i64, c_i64, c_int, c_double, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_size, c_vp]),
+    "cq_jacobi_staged_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh_staged": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_double, c_int, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
@@ -121,7 +122,8 @@ _SIGS = {
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
-    "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp]),
     "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cq_sgram_rows": (c_int, [c_i64]),
     "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
@@ -513,7 +515,7 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
 
 
 class BlockJacobi:
-    """cq_jacobi_eigh_staged for p > 192: begin + a first batch of sweeps, then further sweeps
+    """cq_jacobi_eigh_staged (block Jacobi): begin + a first batch of sweeps, then further sweeps
     only while the device count of unconverged matrices (read back by the caller) is nonzero."""
     BEGIN, SWEEPS, END = 1, 2, 4
 
@@ -521,7 +523,7 @@ class BlockJacobi:
         _require_hip(A)
         self.A, self.tol, self.want = A, tol, bool(want_vectors)
         self.B, self.p, _ = A.shape
-        self.ws = workspace(load().cq_jacobi_workspace(self.p, self.B), A.device)
+        self.ws = workspace(load().cq_jacobi_staged_workspace(self.p, self.B), A.device)
         self.pending = torch.zeros(1, dtype=torch.int32, device=A.device)
         self.swept = 0
 
@@ -769,13 +771,20 @@ def absmax(X: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def sgram_count(packed, k, L, row_nnz, perm, slice_off, total):
-    """Sliced-ELL layout of the nonzero 2-bit codes per row (cq_sgram_count): packed (B, k*L/4)."""
-    _require_hip(packed, row_nnz, perm, slice_off, total)
+def sgram_count(packed, k, L, row_nnz, perm, slice_off, total, W=None, qscale=None, wcol=None, corr_ws=None,
+                corr_out=None):
+    """Sliced-ELL layout of the nonzero 2-bit codes per row (cq_sgram_count): packed (B, k*L/4).
+    With W (B, k, L) fp16: corr_out (B,) fp64 = ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2
+    (wcol = ycol^2), corr_ws (B * k,) fp64 scratch."""
+    _require_hip(packed, row_nnz, perm, slice_off, total, W, qscale, wcol, corr_ws, corr_out)
     B = total.numel()
     assert row_nnz.numel() >= B * k and perm.numel() >= B * k and slice_off.numel() >= B * (-(-k // 64) + 1)
-    _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total),
-                                 _stream(packed.device)), "cq_sgram_count")
+    if W is not None:
+        assert W.dtype == torch.float16 and W.is_contiguous() and W.shape == (B, k, L)
+        assert corr_ws.numel() >= B * k and corr_ws.dtype == torch.float64 and corr_out.numel() == B
+    _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total), _p(W),
+                                 _p(qscale), _p(wcol), _p(corr_ws), _p(corr_out), _stream(packed.device)),
+           "cq_sgram_count")
 
 
 def sgram_fill(packed, k, L, row_nnz, perm, slice_off, ell, stride):

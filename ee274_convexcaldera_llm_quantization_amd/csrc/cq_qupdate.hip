@@ -246,40 +246,14 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         return cur;
     };
     uint2 seg[RB][E];   // pass 1, 2-bit packed: a row's code bytes of the current GRP-chunk group
-    // pass 2: this lane's listed groups of the current chunk (one per row block at most), stored
-    // at the start of the next chunk, BEFORE its prefetches are issued -- a store issued after a
-    // prefetch forces a full vmcnt drain at the chunk's end (stores and loads may complete out of
-    // order, so a counted wait would not prove the stage landed), which exposed the latency of
-    // the ring's newest W chunk on every chunk holding a candidate (nearly all of them)
-    float kv[PASS == 2 ? RB : 1][8];
-    int kpos[PASS == 2 ? RB : 1];   // list position of the kept group, -1: none
-#pragma unroll
-    for (int rb = 0; rb < (PASS == 2 ? RB : 1); ++rb) kpos[rb] = -1;
-    auto flush = [&](int64_t chk) {   // the kept groups of chunk chk
-        if constexpr (PASS == 2) {
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) {
-                if (kpos[rb] >= 0) {
-                    const int64_t slot = region * q.cap + kpos[rb];
-                    float4* dv = q.gval + 2 * slot;
-                    dv[0] = make_float4(kv[rb][0], kv[rb][1], kv[rb][2], kv[rb][3]);
-                    dv[1] = make_float4(kv[rb][4], kv[rb][5], kv[rb][6], kv[rb][7]);
-                    q.gid[slot] = (uint32_t)((row0 + 16 * rb + l16) * n + chk * QP_BN + 8 * lq);
-                    kpos[rb] = -1;
-                }
-            }
-        }
-    };
     // chunk ch's products and epilogue on W wc and R^T stage st; returns whether it issued
     // global stores (then only a full vmcnt drain is a safe wait)
-    // pass 0, K <= 128 (UPF): the chunk's R^T fragments (both halves, every K step: 64 VGPRs) are read
+    // passes 0 and 2, K <= 128 (UPF): the chunk's R^T fragments (both halves, every K step: 64 VGPRs) are read
     // from LDS once, behind one wait, and each row block's MFMAs are followed by its epilogue,
     // so the epilogue's VALU work of row block rb overlaps the MFMAs of rb + 1 (independent
     // registers) instead of waiting for all of them; the MFMA order per accumulator (K steps,
     // then al x lh, ah x ll, ah x lh) is the same as mma()'s, so the sums are bit-identical.
-    // (pass 2 holds its listed groups across the chunk's end instead, and with the up-front
-    // fragments as well it would spill: 256 VGPRs + 8 spilled vs 222 without them)
-    constexpr bool UPF = KSMAX <= 4 && PASS == 0;
+    constexpr bool UPF = KSMAX <= 4 && (PASS == 0 || PASS == 2);
     auto compute = [&](int64_t ch, const uint4 (&wc)[RB][WV], const _Float16* st) -> bool {
         const int64_t n0 = ch * QP_BN;
         bool stored = false;
@@ -329,7 +303,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 // lane's 8 elements, fp64 across); and, where any of the lane's 8 elements has
                 // |res| >= tau, the whole group of 8 residuals to this wave's list (slot from
                 // one ballot: the list order, hence every later sum, is deterministic).  The
-                // group is kept in registers and stored by flush() at the next chunk's start.
+                // stores are followed by a full drain at the chunk's end (compute() returns
+                // true), a wait that costs little next to a chunk's ~4 us of MFMA work.
                 uint32_t lm = 0u;
                 float e8 = 0.f;
                 if (ewl) {
@@ -351,13 +326,15 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 const bool cand = lm >= tb;
                 const uint64_t mk = __ballot(cand);
                 if (mk) {
+                    stored = true;
                     if (cand) {
                         const int64_t pos = gcur + (int64_t)__builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
                         if (pos < q.cap) {
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) kv[rb][u] = v[u];
-                            kpos[rb] = (int)pos;
+                            float4* dv = q.gval + 2 * (region * q.cap + pos);
+                            dv[0] = make_float4(v[0], v[1], v[2], v[3]);
+                            dv[1] = make_float4(v[4], v[5], v[6], v[7]);
+                            q.gid[region * q.cap + pos] = (uint32_t)e;
                         }
                     }
                     gcur += __builtin_popcountll(mk);
@@ -486,7 +463,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         __syncthreads();
         int sw = 0;   // slot of chunk ch
         for (int64_t ch = 0; ch < nchunks; ++ch) {
-            if (ch) flush(ch - 1);   // the previous chunk's list entries, ahead of this chunk's prefetches
             if (ch + 1 < nchunks) {
                 qp_issue_r<NW, RROW>(Rhb, Rlb, (ch + 1) * QP_BN, K, smem + ((ch + 1) & 1) * RSTAGE, wid, lane);
                 issue_ew(ch + 1);
@@ -505,7 +481,6 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             __syncthreads();  // next chunk's stage landed everywhere; this chunk's stage fully read
             sw = sw + 1 == QP_WD ? 0 : sw + 1;
         }
-        if (nchunks) flush(nchunks - 1);
     } else {
         // registers: pass 0 keeps W two chunks ahead (three buffers, loop unrolled by 3 so no
         // in-flight destination is copied), pass 1 one chunk ahead

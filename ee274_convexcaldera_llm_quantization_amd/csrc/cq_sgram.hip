@@ -37,8 +37,17 @@ __device__ __forceinline__ uint32_t sg_field(uint32_t word, int u) {
     return (word >> (8 * (u >> 2) + 6 - 2 * (u & 3))) & 3u;
 }
 
+// code u (0..15) of the field whose low bit is at bit position p (p even)
+__device__ __forceinline__ int sg_u_of_bit(int p) { return 4 * (p >> 3) + ((6 - (p & 7)) >> 1); }
+
+// Per row: the nonzero count and, with W (fp16, the codes' layout) given, the row's part of
+// ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2 = sum over its nonzero codes of
+// wcol[l] (s^2 - 2 s c W[j, l]) (fp64; wcol = ycol^2, NULL = 1): ||Y||_F^2 of the LR step
+// without a pass over Y (the per-matrix sum in row order in sgram_slices_kernel)
 __global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
-                                                          int32_t* __restrict__ row_nnz) {
+                                                          int32_t* __restrict__ row_nnz, const _Float16* __restrict__ W,
+                                                          const float* __restrict__ qscale,
+                                                          const float* __restrict__ wcol, double* __restrict__ row_corr) {
     const int lane = threadIdx.x & 63;
     const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t b = blockIdx.y;
@@ -46,9 +55,30 @@ __global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restr
     const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
     const int64_t nw = L / 16;
     uint32_t cnt = 0;
-    for (int64_t w = lane; w < nw; w += 64) cnt += __popc(sg_nz_mask(row[w]));
+    double corr = 0.0;
+    const double s = W ? (double)qscale[b] : 0.0;
+    const _Float16* Wr = W ? W + b * k * L + j * L : nullptr;
+    for (int64_t w = lane; w < nw; w += 64) {
+        const uint32_t word = row[w];
+        uint32_t nz = sg_nz_mask(word);
+        cnt += __popc(nz);
+        if (W) {
+            while (nz) {
+                const int p = __builtin_ctz(nz);
+                nz &= nz - 1u;
+                const int64_t l = 16 * w + sg_u_of_bit(p);
+                const double c = (double)((int)((word >> p) & 3u) - 1);
+                const double t = s * s - 2.0 * s * c * (double)(float)Wr[l];
+                corr += wcol ? (double)wcol[l] * t : t;
+            }
+        }
+    }
     cnt = wave_sum(cnt);
     if (lane == 0) row_nnz[b * k + j] = (int32_t)cnt;
+    if (W) {
+        corr = wave_sum(corr);
+        if (lane == 0) row_corr[b * k + j] = corr;
+    }
 }
 
 // one workgroup per matrix: the rows sorted by nonzero count (descending; ties in row order --
@@ -59,7 +89,8 @@ constexpr int SG_BINS = 1024;
 
 __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __restrict__ row_nnz, int64_t k,
                                                            int32_t* __restrict__ perm, int64_t* __restrict__ slice_off,
-                                                           int64_t* __restrict__ total) {
+                                                           int64_t* __restrict__ total, const double* __restrict__ row_corr,
+                                                           double* __restrict__ corr_out) {
     __shared__ int32_t hist[SG_BINS];
     const int64_t b = blockIdx.x;
     const int32_t* nz = row_nnz + b * k;
@@ -76,6 +107,11 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
             acc += c;
         }
         for (int64_t j = 0; j < k; ++j) pm[hist[min(nz[j], SG_BINS - 1)]++] = (int32_t)j;
+        if (row_corr) {   // the rows' norm corrections, summed in row order
+            double cs = 0.0;
+            for (int64_t j = 0; j < k; ++j) cs += row_corr[b * k + j];
+            corr_out[b] = cs;
+        }
     }
     __syncthreads();
     const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
@@ -579,8 +615,6 @@ __global__ __launch_bounds__(256) void sgram_combine_kernel(const float* __restr
 // word, code u of a word at bits 8 (u / 4) + 6 - 2 (u % 4) (bytes MSB-first).
 
 __device__ __forceinline__ uint32_t sg_put(uint32_t f, int u) { return f << (8 * (u >> 2) + 6 - 2 * (u & 3)); }
-// code index u of the field whose low bit is at bit position p (p even)
-__device__ __forceinline__ int sg_u_of_bit(int p) { return 4 * (p >> 3) + ((6 - (p & 7)) >> 1); }
 
 // Transpose of packed 2-bit codes (rows x cols -> cols x rows), a tile of 256 x 256 codes per
 // workgroup: thread (i, j) loads the 16 x 16 block of input rows 16 i.., word j (16 lanes read a
@@ -625,12 +659,15 @@ __global__ __launch_bounds__(256) void codes_transpose_kernel(const uint32_t* __
 
 // out[row, :] = sum over the nonzero codes c (col) of row `row` of c w[col] X[col, :] (X: cols x r,
 // row stride ldx; w NULL = 1), times roww[row] if given: the sparse-code product of the LR step
-// (U^T c, c V).  One wave per
-// row: the row's nonzero codes are compacted into a per-wave LDS list (one pass over its words,
-// in increasing word order), then consumed 8 at a time with the X-row loads of all 8 in flight;
-// lane l owns r-values l, l + 64, ...  TRANS: out is r x rows (ld ldo), written through an LDS
-// tile of the workgroup's 64 rows (coalesced over rows); else rows x r.
-constexpr int CM_LIST = 1024;
+// (U^T c, c V).  One wave per row: the row's nonzero codes are compacted into a per-wave LDS list
+// (in increasing word order; fixed order, deterministic), then consumed CM_G at a time with the
+// X-row loads of all CM_G in flight; lane l owns r-values l, l + 64, ...  The words of a row
+// (CM_WPL per lane and block of 64 CM_WPL words) are loaded in one batch, and the next row's
+// first block while the current row is consumed.  TRANS: out is r x rows (ld ldo), written
+// through an LDS tile of the workgroup's 64 rows (coalesced over rows); else rows x r.
+constexpr int CM_LIST = 1024;   // list entries per wave (one block of 4 x 64 words holds <= 4096)
+constexpr int CM_WPL = 4;       // words per lane per block
+constexpr int CM_G = 16;        // entries per gather batch
 template <int RV, bool TRANS>
 __global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __restrict__ packed, int64_t rows,
                                                            int64_t cols, const float* __restrict__ X, int64_t ldx,
@@ -646,38 +683,49 @@ __global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __res
     const uint32_t* pb = packed + b * rows * nw;
     const float* Xb = X + b * sx;
     const uint64_t lt = (1ull << lane) - 1ull;
+    constexpr int64_t BLK = 64 * CM_WPL;   // words per block
+    auto load_block = [&](int64_t row, int64_t w0, uint32_t (&wd)[CM_WPL]) {
+#pragma unroll
+        for (int t = 0; t < CM_WPL; ++t) {
+            const int64_t wi = w0 + 64 * t + lane;
+            wd[t] = (row < rows && wi < nw) ? pb[row * nw + wi] : 0x55555555u;
+        }
+    };
+    float acc[RV];
+    int cnt = 0;
+    auto consume = [&]() {
+        for (int t0 = 0; t0 < cnt; t0 += CM_G) {
+            float cv[CM_G], xv[CM_G][RV];
+#pragma unroll
+            for (int e = 0; e < CM_G; ++e) {
+                const bool live = t0 + e < cnt;
+                const uint32_t en = live ? list[t0 + e] : 1u;   // padding: code 0 at column 0
+                const int64_t col = en >> 2;
+                cv[e] = (float)((int)(en & 3u) - 1);
+                if (w && live) cv[e] *= w[col];
+                const float* xr = Xb + col * ldx;
+#pragma unroll
+                for (int k = 0; k < RV; ++k) xv[e][k] = (lane + 64 * k < r) ? xr[lane + 64 * k] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < CM_G; ++e)
+#pragma unroll
+                for (int k = 0; k < RV; ++k) acc[k] = __builtin_fmaf(cv[e], xv[e][k], acc[k]);
+        }
+        cnt = 0;
+    };
+    uint32_t cur[CM_WPL];
+    load_block(row0 + wv * 16, 0, cur);
     for (int q = 0; q < 16; ++q) {
         const int lr = wv * 16 + q;
         const int64_t row = row0 + lr;
-        float acc[RV];
 #pragma unroll
         for (int k = 0; k < RV; ++k) acc[k] = 0.f;
-        auto consume = [&](int cnt) {
-            for (int t0 = 0; t0 < cnt; t0 += 8) {
-                float cv[8], xv[8][RV];
+        for (int64_t w0 = 0; w0 < nw; w0 += BLK) {
+            // compact this block's nonzero codes into the list (ballot prefix of the counts)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const uint32_t en = t0 + e < cnt ? list[t0 + e] : 1u;   // padding: code 0
-                    const int64_t col = en >> 2;
-                    cv[e] = (float)((int)(en & 3u) - 1);
-                    if (w && t0 + e < cnt) cv[e] *= w[col];
-                    const float* xr = Xb + col * ldx;
-#pragma unroll
-                    for (int k = 0; k < RV; ++k) xv[e][k] = (lane + 64 * k < r) ? xr[lane + 64 * k] : 0.f;
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-#pragma unroll
-                    for (int k = 0; k < RV; ++k) acc[k] = __builtin_fmaf(cv[e], xv[e][k], acc[k]);
-            }
-        };
-        if (row < rows) {
-            const uint32_t* pr = pb + row * nw;
-            int cnt = 0;
-            for (int64_t w0 = 0; w0 < nw; w0 += 64) {
-                const int64_t wi = w0 + lane;
-                const uint32_t word = wi < nw ? pr[wi] : 0x55555555u;
-                uint32_t nz = sg_nz_mask(word);
+            for (int t = 0; t < CM_WPL; ++t) {
+                uint32_t nz = sg_nz_mask(cur[t]);
                 const int c = __builtin_popcount(nz);
                 int pre = 0, tot = 0;
 #pragma unroll
@@ -686,28 +734,32 @@ __global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __res
                     pre += __popcll(mk & lt) << bt;
                     tot += __popcll(mk) << bt;
                 }
-                if (cnt + tot > CM_LIST) {   // list full: consume it first (tot <= 1024 = CM_LIST)
+                if (cnt + tot > CM_LIST) {   // list full (tot <= 1024 = CM_LIST): consume it first
                     __builtin_amdgcn_wave_barrier();
-                    consume(cnt);
+                    consume();
                     __builtin_amdgcn_wave_barrier();
-                    cnt = 0;
                 }
                 int pos = cnt + pre;
+                const int64_t wi = w0 + 64 * t + lane;
                 while (nz) {
                     const int p = __builtin_ctz(nz);
                     nz &= nz - 1u;
-                    list[pos++] = (uint32_t)((16 * wi + sg_u_of_bit(p)) << 2) | ((word >> p) & 3u);
+                    list[pos++] = (uint32_t)((16 * wi + sg_u_of_bit(p)) << 2) | ((cur[t] >> p) & 3u);
                 }
                 cnt += tot;
             }
+            // the next block of this row, or the first block of the next row, in flight while
+            // this list is consumed
+            if (w0 + BLK < nw) load_block(row, w0 + BLK, cur);
+            else if (q + 1 < 16) load_block(row + 1, 0, cur);
             __builtin_amdgcn_wave_barrier();
-            consume(cnt);
+            consume();
             __builtin_amdgcn_wave_barrier();
-            if (roww) {
-                const float rw = roww[row];
+        }
+        if (roww && row < rows) {
+            const float rw = roww[row];
 #pragma unroll
-                for (int k = 0; k < RV; ++k) acc[k] *= rw;
-            }
+            for (int k = 0; k < RV; ++k) acc[k] *= rw;
         }
         if constexpr (TRANS) {
 #pragma unroll
@@ -840,13 +892,17 @@ int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t col
 }
 
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
-                   int32_t* perm, int64_t* slice_off, int64_t* total, void* stream) {
+                   int32_t* perm, int64_t* slice_off, int64_t* total, const void* W, const float* qscale,
+                   const float* wcol, double* corr_ws, double* corr_out, void* stream) {
     CQ_REQUIRE(packed && row_nnz && perm && slice_off && total, "cq_sgram_count: null argument");
     CQ_REQUIRE(bits == 2, "cq_sgram_count: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0, "cq_sgram_count: bad shape");
+    CQ_REQUIRE(!W || (qscale && corr_ws && corr_out), "cq_sgram_count: the norm correction needs qscale, corr_ws, corr_out");
     hipStream_t s = as_stream(stream);
-    sgram_count_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, s>>>(packed, k, L, row_nnz);
-    sgram_slices_kernel<<<(unsigned)batch, 256, 0, s>>>(row_nnz, k, perm, slice_off, total);
+    sgram_count_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, s>>>(
+        packed, k, L, row_nnz, reinterpret_cast<const _Float16*>(W), qscale, wcol, corr_ws);
+    sgram_slices_kernel<<<(unsigned)batch, 256, 0, s>>>(row_nnz, k, perm, slice_off, total, W ? corr_ws : nullptr,
+                                                        corr_out);
     return check_launch("cq_sgram_count");
 }
 

@@ -849,14 +849,16 @@ int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double t
     return check_launch("cq_jacobi_eigh");
 }
 
+size_t cq_jacobi_staged_workspace(int64_t p, int64_t batch) { return cq::bj_workspace(p, batch); }
+
 int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double tol, int want_vectors,
                           double* evals, float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws,
                           size_t ws_bytes, void* stream) {
-    CQ_REQUIRE(A && p > kBlockJacobiMinP && p <= 4096 && batch > 0, "cq_jacobi_eigh_staged: bad args (p > 192 only)");
+    CQ_REQUIRE(A && p >= 2 && p <= 4096 && batch > 0, "cq_jacobi_eigh_staged: bad args");
     CQ_REQUIRE(phase > 0 && phase <= (BJ_BEGIN | BJ_SWEEPS | BJ_END), "cq_jacobi_eigh_staged: bad phase");
     CQ_REQUIRE(!(phase & BJ_SWEEPS) || nsweeps > 0, "cq_jacobi_eigh_staged: nsweeps must be > 0");
     CQ_REQUIRE(!(phase & BJ_END) || (evals && (!want_vectors || V32 || V64)), "cq_jacobi_eigh_staged: outputs");
-    if (!ws || ws_bytes < cq_jacobi_workspace(p, batch))
+    if (!ws || ws_bytes < cq_jacobi_staged_workspace(p, batch))
         return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh_staged: workspace too small");
     return cq::bj_stage(A, p, batch, phase, nsweeps, tol, want_vectors != 0, evals, V32, V64, sweeps_out, pending_out,
                         ws, ws_bytes, as_stream(stream));

@@ -500,7 +500,7 @@ class CalderaEngine:
             if tall:
                 ct = scratch.get("sgram.codes_t", st.Qc.shape, torch.uint8, dev)
                 K.codes_transpose(st.Qc, m, n, out=ct)
-                if self._sg.count(ct) > sgram.MAX_DENSITY * m * n:
+                if self._sg.count(ct, self._wt16, st.Qs) > sgram.MAX_DENSITY * m * n:
                     tall = False  # too many nonzero codes this step: dense Gram
                 else:
                     sparse_g = lite = True
@@ -526,14 +526,17 @@ class CalderaEngine:
                              **(dict(ys=self._ysw, wth=self._wth, wtl=self._wtl, wsq=self._wsq) if lite else {}))
                 if gev is not None:
                     gev[1].record()
-            if sparse_g and not tall and self._sg.count(st.Qc) > sgram.MAX_DENSITY * m * n:
-                sparse_g = False  # too many nonzero codes this step: dense Gram
+            if sparse_g and not tall:
+                # (the codes' norm correction of ||Y||^2 comes with the count where it is used)
+                corr = dict(W=Ws, qscale=st.Qs, wcol=self._sg_w) if lite and self._wth is not None else {}
+                if self._sg.count(st.Qc, **corr) > sgram.MAX_DENSITY * m * n:
+                    sparse_g = False  # too many nonzero codes this step: dense Gram
             lite = lite and sparse_g and self._wth is not None
             self._r_lite = lite
             if lite:
                 self.lr_steps_from_codes += 1
                 # no pass over Y at all: ||Y||^2 from ||W diag(ycol)||^2 and the nonzero codes
-                ysq = self._wsq + K.codes_ysq_corr(st.Qc, Ws, st.Qs, self._sg_w)
+                ysq = self._wsq + self._sg.ysq_corr
             else:
                 halves = ({} if sparse_g and not x3_lplr else dict(hi=self._yh, lo=self._yl)) if sv.left else \
                     dict(thi=self._yh, tlo=self._yl)

@@ -61,10 +61,20 @@ class SparseGram:
         self.total = torch.empty(B, dtype=torch.int64, device=dev)
         self.density = None
         self.stats = {"sparse": 0, "dense": 0}
+        self._corr_ws = None
+        self.ysq_corr = None
 
-    def count(self, packed: torch.Tensor) -> int:
-        """ELL entries per matrix (max over the batch) -- one host read-back."""
-        K.sgram_count(packed, self.m, self.n, self.row_nnz, self.perm, self.slice_off, self.total)
+    def count(self, packed: torch.Tensor, W=None, qscale=None, wcol=None) -> int:
+        """ELL entries per matrix (max over the batch) -- one host read-back.  With W (the codes'
+        layout, fp16) also self.ysq_corr (B,) fp64 = ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2
+        (wcol = ycol^2)."""
+        corr = {}
+        if W is not None:
+            if self._corr_ws is None:
+                self._corr_ws = torch.empty(self.B * self.m, dtype=torch.float64, device=W.device)
+            self.ysq_corr = torch.empty(self.B, dtype=torch.float64, device=W.device)
+            corr = dict(W=W, qscale=qscale, wcol=wcol, corr_ws=self._corr_ws, corr_out=self.ysq_corr)
+        K.sgram_count(packed, self.m, self.n, self.row_nnz, self.perm, self.slice_off, self.total, **corr)
         mx = int(self.total.max().item())
         self.density = mx / float(self.m * self.n)
         return mx

@@ -135,6 +135,7 @@ JACOBI_MAX_SWEEPS = 30
 # stream-ordered): a first batch of sweeps sized from the previous call, then BJ_STEP more at a
 # time while the device count of unconverged matrices (one int read back) is nonzero
 BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
+BJ_SMALL_BATCH = 8  # batches this small take the block Jacobi at every p
 STALL_RATIO = 0.98
 
 
@@ -198,7 +199,10 @@ class RankRSolver:
         self.valid_k = self.k  # rows >= valid_k of the eigenproblem are zero padding (engine.py)
         # Rayleigh-Ritz sweep budget: fixed for the one-workgroup Jacobi (its sweep loop runs
         # inside one kernel), adaptive for the block Jacobi (each sweep is a set of launches)
-        self.block_jacobi = self.p > 192
+        # block Jacobi over many workgroups where one CU cannot hold the problem (p > 192), and
+        # for small batches, where the one-workgroup-per-matrix kernel leaves the chip idle (one
+        # caldera() call: ~4 ms per 192 x 192 eigensolve on one CU)
+        self.block_jacobi = self.p > 192 or B <= BJ_SMALL_BATCH
         self.bj_first = BJ_FIRST  # block Jacobi: sweeps launched before the first read-back
         self._bufs = None
         self._G = None

@@ -220,13 +220,16 @@ size_t cq_jacobi_workspace(int64_t p, int64_t batch);
 int cq_jacobi_eigh(double* A, int64_t p, int64_t batch, int max_sweeps, double tol,
                    double* evals, float* V32, double* V64, int* sweeps_out, void* ws,
                    size_t ws_bytes, void* stream);
-/* The same eigensolve for p > 192 (block Jacobi over many workgroups) in caller-driven
+/* The same eigensolve as a block Jacobi over many workgroups per matrix, in caller-driven
  * stages, each stream-ordered: phase bit 1 = begin (V = I), 2 = nsweeps sweeps (matrices that
  * converged skip the rest; pending_out, a device int, = matrices still unconverged), 4 = end
- * (evals, V32/V64, sweeps_out).  The state stays in ws (cq_jacobi_workspace) between calls,
- * so a caller reading pending_out launches further sweeps only while some are needed (the
- * Rayleigh-Ritz eigensolve of alg.py:217's replacement at rank > 136, e.g. main.py:176's
- * rank 200 and config 5's rank 256).  want_vectors must be the same in every stage. */
+ * (evals, V32/V64, sweeps_out).  The state stays in ws (cq_jacobi_staged_workspace) between
+ * calls, so a caller reading pending_out launches further sweeps only while some are needed.
+ * Used for p > 192 (the Rayleigh-Ritz eigensolve of alg.py:217's replacement at rank > 136,
+ * e.g. main.py:176's rank 200 and config 5's rank 256), and at any p for small batches (one
+ * caldera() call, main.py:189-196), where the one-CU kernel would leave the other CUs idle.
+ * want_vectors must be the same in every stage. */
+size_t cq_jacobi_staged_workspace(int64_t p, int64_t batch);
 int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double tol, int want_vectors,
                           double* evals, float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws,
                           size_t ws_bytes, void* stream);
@@ -341,6 +344,10 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  *                     (batch x k x L, offset-binary MSB-first), perm (batch x k, int32: rows
  *                     sorted by count, descending, ties in row order), slice_off (batch x (ceil(k/64)
  *                     + 1), int64: sliced-ELL offsets per 64-row slice, in 64-entry rows), total[b] entries;
+ *                     with W (fp16, batch x k x L; may be NULL) also corr_out[b] = sum over the
+ *                     nonzero codes of wcol[l] (s^2 - 2 s c W[j, l]) (fp64, s = qscale[b], wcol NULL
+ *                     = 1; corr_ws: batch x k doubles): ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2
+ *                     for wcol = ycol^2, the ||Y||_F^2 of alg.py:211 without a pass over Y;
  *   cq_sgram_fill:    the ELL entries (uint32: l << 2 | code + 1) of matrix b at ell + b stride_ell
  *                     (row_nnz, perm, slice_off from cq_sgram_count);
  *   cq_sgram_rows:    rows of E a workgroup stages for contraction length L (0: too long);
@@ -352,7 +359,8 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  *                     inv_out[b] = 1 / (scale_out[b] out_scale)); G32 (full fp32 G) optional.
  * k % 64 == 0, L % 64 == 0. */
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
-                   int32_t* perm, int64_t* slice_off, int64_t* total, void* stream);
+                   int32_t* perm, int64_t* slice_off, int64_t* total, const void* W, const float* qscale,
+                   const float* wcol, double* corr_ws, double* corr_out, void* stream);
 int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
                   const int32_t* perm, const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream);
 int cq_sgram_rows(int64_t L);
