@@ -66,6 +66,8 @@ class X3Args(ctypes.Structure):
         ("scale_out", c_vp),
         ("inv_out", c_vp),
         ("single", c_int),
+        ("ksplit", c_int),
+        ("split_ws", c_vp),
     ]
 
 
@@ -655,7 +657,7 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
-            single=False):
+            single=False, ksplit=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
@@ -696,6 +698,18 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.a_blocked = int(a_blocked)
     g.o_blocked = int(bool(o_blocked))
     g.single = int(bool(single))
+    # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
+    # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups
+    tiles = -(-N // 384) * -(-M // 192) * Bt
+    splittable = not tri and sym_bound is None and C is not None and N % 4 == 0
+    if ksplit is None:  # automatic
+        ks = min(Kd // 32 // 8, -(-512 // tiles)) if splittable and tiles < 256 and Kd >= 512 else 1
+    else:
+        ks = int(ksplit)
+        assert ks == 1 or (splittable and ks <= Kd // 32), "gemm_x3: split-K not possible here"
+    if ks > 1:
+        g.ksplit = ks
+        g.split_ws = scratch.get_flat("gemm_x3.split", ks * Bt * M * N, torch.float32, Ah.device).data_ptr()
     if sym_bound is not None:
         g.sym_out = 1
         g.out_bound, g.scale_out, g.inv_out = sym_bound.data_ptr(), scale_out.data_ptr(), inv_out.data_ptr()

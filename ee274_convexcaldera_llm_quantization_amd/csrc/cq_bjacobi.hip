@@ -430,8 +430,10 @@ int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double
             for (int st = 0; st < nblk - 1; ++st) {
                 bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
                                                                                        done, poff, pdg, nslots);
-                bj_update_kernel<<<dim3((unsigned)(noff + (want_v ? npair * nch : 0)), (unsigned)batch), BT, 0, s>>>(
-                    A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
+                const int nupd = noff + (want_v ? npair * nch : 0);   // 0: one pair, values only
+                if (nupd > 0)
+                    bj_update_kernel<<<dim3((unsigned)nupd, (unsigned)batch), BT, 0, s>>>(
+                        A, (int)p, nblk, st, Vs, rot, done, want_v ? Vt : nullptr, poff, nslots);
             }
             bj_check_kernel<<<(unsigned)batch, 64, 0, s>>>(poff, pdg, nslots, npair, tol, done, sweeps);
         }

@@ -33,6 +33,8 @@ struct X3K {
     const double* out_bound;   // [batch] bound on max|C|: split scale 2^(14 - e)
     float* scale_out;          // [batch] that scale
     float* inv_out;            // [batch] 1 / (scale * out_scale)
+    int ksplit;                // > 1: K cut into ksplit chunks, fp32 partials in part (split-K)
+    float* part;               // [ksplit][batch][M][N]
 };
 
 using f16x8g = __attribute__((ext_vector_type(8))) _Float16;

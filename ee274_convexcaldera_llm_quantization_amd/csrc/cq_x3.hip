@@ -173,7 +173,7 @@ __device__ __forceinline__ void xw_mainloop(const X3K& a, int64_t b, int64_t m0,
 template <bool PERMB = false>
 __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                             _Float16* smem, int wid, int lane, int wm, int wn,
-                                            f32x4v (&acc)[6][4]) {
+                                            f32x4v (&acc)[6][4], int64_t kb = 0) {
     const int l16 = lane & 15, lq = lane >> 4;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -181,7 +181,7 @@ __device__ __forceinline__ void xv_mainloop(const X3K& a, int64_t b, int64_t m0,
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
     wid = __builtin_amdgcn_readfirstlane(wid);
     uint32_t off[XW_PER_WAVE];
-    auto issue = [&](int64_t k0, _Float16* st) { xw_issue(a, b, k0, st, wid, off); };
+    auto issue = [&](int64_t k0, _Float16* st) { xw_issue(a, b, kb * XW_BK + k0, st, wid, off); };
     if (nt > 0) {
         xw_plan(a, m0, n0, wid, lane, off);
         issue(0, smem);
@@ -271,7 +271,7 @@ __device__ __forceinline__ void xv1_wait(int64_t after) {
 
 __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
                                              _Float16* smem, int wid, int lane, int wm, int wn,
-                                             f32x4v (&acc)[6][4]) {
+                                             f32x4v (&acc)[6][4], int64_t kb = 0) {
     static_assert(XV1_NS == 4 && XW1_PER_WAVE == 3, "xv1_wait's counts");
     const int l16 = lane & 15, lq = lane >> 4;
 #pragma unroll
@@ -282,7 +282,8 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
     uint32_t off[XW1_PER_WAVE];
     if (nt > 0) {
         xw1_plan(a, m0, n0, wid, lane, off);
-        for (int64_t s = 0; s < XV1_NS - 1 && s < nt; ++s) xv1_issue(a, b, s * XW_BK, smem + s * XV1_STAGE, wid, off);
+        for (int64_t s = 0; s < XV1_NS - 1 && s < nt; ++s)
+            xv1_issue(a, b, (kb + s) * XW_BK, smem + s * XV1_STAGE, wid, off);
     }
     const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
     uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
@@ -292,8 +293,8 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
             xv1_wait(nt - 1 - t);
             __builtin_amdgcn_s_barrier();
             if (t + XV1_NS - 1 < nt)
-                xv1_issue(a, b, (t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE, wid,
-                          off);
+                xv1_issue(a, b, (kb + t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE,
+                          wid, off);
         }
         return;
     }
@@ -302,7 +303,8 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
         __builtin_amdgcn_s_barrier();  // stage t landed everywhere; the slot of t - 1 fully read
         // slot (t + 3) % 4 last held step t - 1, whose reads every wave finished before this barrier
         if (t + XV1_NS - 1 < nt)
-            xv1_issue(a, b, (t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE, wid, off);
+            xv1_issue(a, b, (kb + t + XV1_NS - 1) * XW_BK, smem + ((t + XV1_NS - 1) & (XV1_NS - 1)) * XV1_STAGE, wid,
+                      off);
         const _Float16* sA = smem + (t & (XV1_NS - 1)) * XV1_STAGE;
         const _Float16* sB = sA + XW_APART;
         f16x8 bh[4];
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
         gram_tile(a, blockIdx.x, b, tm, tn);
     } else {
         const int64_t total = a.tiles_n * a.tiles_m * a.batch;
-        const int64_t orig = blockIdx.x;
+        const int64_t orig = a.ksplit > 1 ? blockIdx.x / a.ksplit : blockIdx.x;   // split-K: chunk fastest
         const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
         const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
         // row tiles fastest: when A has more than one 192-row tile (the filter at p > 192), the
@@ -390,13 +392,37 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
 
     f32x4v acc[6][4];
     const bool live = !a.active || a.active[b];
+    const int64_t nk = a.K / XW_BK;
+    int64_t kb = 0, kn = nk;
+    if (a.ksplit > 1) {   // this workgroup's K chunk
+        const int64_t ks = blockIdx.x % a.ksplit;
+        kb = ks * nk / a.ksplit;
+        kn = (ks + 1) * nk / a.ksplit - kb;
+    }
     if constexpr (X1) {
-        xv1_mainloop(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+        xv1_mainloop(a, b, m0, n0, live ? kn : 0, smem, wid, lane, wm, wn, acc, kb);
     } else {
-        xv_mainloop<false>(a, b, m0, n0, live ? a.K / XW_BK : 0, smem, wid, lane, wm, wn, acc);
+        xv_mainloop<false>(a, b, m0, n0, live ? kn : 0, smem, wid, lane, wm, wn, acc, kb);
     }
 
     const float sc = a.inv_scale[b];
+    if (a.ksplit > 1) {   // partial products (times the operand scale) for x3_splitk_epi_kernel
+        float* part = a.part + ((blockIdx.x % a.ksplit) * a.batch + b) * a.M * a.N;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int64_t row = m0 + 96 * wm + 16 * i + l16;
+            if (row >= a.M) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t col = n0 + 64 * wn + 16 * j + 4 * lq;
+                if (col >= a.N) continue;
+                // N % 4 == 0 (host check): 4 columns, 16-byte aligned
+                *reinterpret_cast<float4*>(part + row * a.N + col) =
+                    make_float4(acc[i][j][0] * sc, acc[i][j][1] * sc, acc[i][j][2] * sc, acc[i][j][3] * sc);
+            }
+        }
+        return;
+    }
     if (a.sym_out) {
         // symmetric Gram: entries on/above the diagonal are written at (row, col) and, mirrored,
         // at (col, row) of the K-blocked split (the lower triangle of a straddling tile is not
@@ -520,6 +546,44 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     if (ovf) atomicOr(a.overflow + b, 1);
 }
 
+
+// Split-K epilogue: C = alpha (sum of the ksplit partials, in chunk order) + beta P + gamma D,
+// and the split halves of C, as gemm_x3v_kernel's epilogue does (inactive matrices: C = D).
+// One thread per 4 consecutive columns (N % 4 == 0).
+__global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
+    const int64_t nq = a.N / 4;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t b = blockIdx.y;
+    if (t >= a.M * nq) return;
+    const int64_t row = t / nq, col = 4 * (t % nq);
+    const bool live = !a.active || a.active[b];
+    const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
+    const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
+    const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < a.ksplit; ++ks) {
+        const float4 pv = *reinterpret_cast<const float4*>(a.part + ((ks * a.batch + b) * a.M + row) * a.N + col);
+        s[0] += pv.x; s[1] += pv.y; s[2] += pv.z; s[3] += pv.w;
+    }
+    bool ovf = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float w = al_ * s[r];
+        if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + col + r];
+        if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + col + r];
+        a.C[b * a.sc + row * a.ldc + col + r] = w;
+        if (a.Oh) {
+            const float hs = w * a.out_scale;
+            const _Float16 h = (_Float16)hs;
+            const int64_t c = col + r;
+            const int64_t o = b * a.so + (a.o_blocked ? (c >> 5) * (a.M * 32) + row * 32 + (c & 31) : row * a.ldo + c);
+            a.Oh[o] = h;
+            a.Ol[o] = (_Float16)(hs - (float)h);
+            ovf |= !(fabsf(hs) < 65504.f);
+        }
+    }
+    if (ovf) atomicOr(a.overflow + b, 1);
+}
 
 // ------------------------------------------------------------------ fused Q update
 // maybe_update_Q (alg.py:253-283) + quantize_matrix (alg.py:245-250, quantization.py:244-269)
@@ -765,16 +829,14 @@ __global__ __launch_bounds__(XW_THREADS, 1) void q_update_v_kernel(QUK q) {
 // the fused kernels with res = W.  n % 16 == 0; per-block fp64 error partials in part.
 template <int DT, int BITS, bool FAST>
 __device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t MN, int64_t e, const uint4 (&wr)[4],
-                                              float s, float ys, float yk, double& err) {
+                                              const float4 (&ewv)[4], float s, float ys, float yk, double& err) {
     constexpr float kq = (float)((1 << (BITS - 1)) - 1);
-    const int64_t col = e % q.n;
     uint32_t pk[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         int cq[4];
         float e4[4];
-        float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
-        if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + col + 4 * j);
+        const float4 wv = ewv[j];   // error column weights (1 without), loaded with the group's W
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float v;
@@ -816,7 +878,18 @@ __device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t M
 }
 
 template <int DT>
-__device__ __forceinline__ void qstream_load(const QUK& q, int64_t b, int64_t MN, int64_t e, uint4 (&wr)[4]) {
+__device__ __forceinline__ void qstream_load(const QUK& q, int64_t b, int64_t MN, int64_t e, uint4 (&wr)[4],
+                                             float4 (&ewv)[4]) {
+    // the group's error column weights ride with its W (a load issued at use would expose an
+    // L2 round trip per group: config 3's diagonal-H first Q step ran at 0.42 of HBM)
+    if (q.ew) {
+        const float* ew = q.ew + e % q.n;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ewv[j] = *reinterpret_cast<const float4*>(ew + 4 * j);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ewv[j] = make_float4(1.f, 1.f, 1.f, 1.f);
+    }
     if (DT == CQ_F16) {
         const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN + e;
         wr[0] = *reinterpret_cast<const uint4*>(Wh);
@@ -845,20 +918,23 @@ __global__ __launch_bounds__(256) void quant_w_stream_kernel(QUK q) {
     const int64_t stride = (int64_t)gridDim.x * 256;
     int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (div_fast_ok(s)) {  // uniform: the common case, branch-free correctly rounded division
-        uint4 nx[4];  // the next group's W, loaded while this one is quantised
-        if (g < ng) qstream_load<DT>(q, b, MN, g * 16, nx);
+        uint4 nx[4];  // the next group's W (and weights), loaded while this one is quantised
+        float4 nw[4];
+        if (g < ng) qstream_load<DT>(q, b, MN, g * 16, nx, nw);
         for (; g < ng; g += stride) {
             uint4 cur[4];
+            float4 cw[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) cur[u] = nx[u];
-            if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx);
-            qstream_group<DT, BITS, true>(q, b, MN, g * 16, cur, s, ys, yk, err);
+            for (int u = 0; u < 4; ++u) { cur[u] = nx[u]; cw[u] = nw[u]; }
+            if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx, nw);
+            qstream_group<DT, BITS, true>(q, b, MN, g * 16, cur, cw, s, ys, yk, err);
         }
     } else {  // non-finite / subnormal scale: IEEE divisions
         for (; g < ng; g += stride) {
             uint4 w0[4];
-            qstream_load<DT>(q, b, MN, g * 16, w0);
-            qstream_group<DT, BITS, false>(q, b, MN, g * 16, w0, s, ys, yk, err);
+            float4 ew0[4];
+            qstream_load<DT>(q, b, MN, g * 16, w0, ew0);
+            qstream_group<DT, BITS, false>(q, b, MN, g * 16, w0, ew0, s, ys, yk, err);
         }
     }
     if (q.part) {
@@ -1582,9 +1658,19 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         for (int64_t tm = 0; tm < a.tiles_m; ++tm) a.tiles_live += std::max<int64_t>(0, a.tiles_n - (tm >> 1));
         total = a.tiles_live * a.batch;
     }
+    a.ksplit = g->ksplit > 1 ? g->ksplit : 1;
+    a.part = g->split_ws;
+    if (a.ksplit > 1) {
+        CQ_REQUIRE(!a.tri && !a.sym_out && a.part && a.C && g->N % 4 == 0 && a.ksplit <= g->K / XW_BK,
+                   "cq_gemm_x3: split-K needs a plain product with C, N % 4 == 0, split_ws, ksplit <= K / 32");
+        total *= a.ksplit;
+    }
     CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
     if (a.single) gemm_x3v_kernel<true><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     else gemm_x3v_kernel<false><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    if (a.ksplit > 1)
+        x3_splitk_epi_kernel<<<dim3((unsigned)ceil_div(g->M * (g->N / 4), 256), (unsigned)g->batch), 256, 0,
+                               as_stream(stream)>>>(a);
     return check_launch("cq_gemm_x3");
 }
 

@@ -30,6 +30,20 @@ def get(name: str, shape, dtype, device) -> torch.Tensor:
     return t
 
 
+def get_flat(name: str, numel: int, dtype, device) -> torch.Tensor:
+    """A cached uninitialised 1-D tensor of at least `numel` elements (grown, never shrunk, so
+    calls of varying sizes share one buffer); returns its first `numel` elements."""
+    dev = torch.device(device)
+    sid = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+    key = (sid, name, dev)
+    t = _CACHE.get(key)
+    if t is None or t.numel() < numel or t.dtype != dtype:
+        _CACHE.pop(key, None)
+        t = torch.empty(max(int(numel), 1), dtype=dtype, device=dev)
+        _CACHE[key] = t
+    return t[:numel]
+
+
 def release():
     """Free every cached scratch buffer (returned to PyTorch's caching allocator)."""
     _CACHE.clear()

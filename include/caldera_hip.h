@@ -314,6 +314,11 @@ typedef struct cq_x3_args {
     float* inv_out;                /* [batch] 1 / (s[b] * out_scale) */
     int single;                    /* one fp16 product hi x hi (Al, Bl not read): ~2^-11
                                       relative, for filter steps whose error later steps damp */
+    int ksplit;                    /* > 1 (not with tri/sym_out): the K loop is cut into ksplit
+                                      chunks run by separate workgroups (a small batch's few tiles
+                                      then fill the chip: one caldera() call), their fp32 partials
+                                      summed in chunk order by an epilogue kernel */
+    float* split_ws;               /* ksplit x batch x M x N fp32 partials (ksplit > 1) */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

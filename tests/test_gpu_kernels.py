@@ -900,3 +900,44 @@ def test_q_update_kernels_kat_bit_exact(K, kat, bits):
             assert float(sc[0]) == float(kat[key + "_scale"].reshape(-1)[0]), key
             # the kernels sum d^2 in fp32 within runs of 4 elements, in fp64 across runs
             assert float(err[0]) == pytest.approx(e_ref, rel=1e-6, abs=1e-30), key
+
+
+@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("Bt,M,N,Kd,ks", [(1, 192, 4096, 4096, 16), (3, 128, 1000, 1024, 5), (2, 200, 520, 2048, 64)])
+def test_gemm_x3_split_k_matches_one_pass(K, single, Bt, M, N, Kd, ks):
+    """Split-K (ksplit chunks of the K loop by separate workgroups, partials summed in chunk
+    order by the epilogue kernel: small batches, one caldera() call) against the one-pass
+    kernel: the full epilogue -- alpha/beta/gamma, P and D, the K-blocked split output and its
+    overflow flag, an inactive matrix passing D through -- within fp32 summation-order noise,
+    and bit-exact where the output is pass-through."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + ks)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g)
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g)
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 10, blocked=True)
+    Bh, Bl = K.split_f16(Bm.contiguous(), 2.0 ** 8, blocked=True)
+    inv = torch.full((Bt,), 2.0 ** -18, device=DEV)
+    P = torch.randn(Bt, M, N, device=DEV, generator=g)
+    D = torch.randn(Bt, M, N, device=DEV, generator=g)
+    al = torch.rand(Bt, device=DEV, generator=g) * 1e-2
+    be = torch.rand(Bt, device=DEV, generator=g)
+    ga = torch.rand(Bt, device=DEV, generator=g)
+    active = torch.ones(Bt, dtype=torch.int32, device=DEV)
+    active[-1] = 0 if Bt > 1 else 1
+    outs = []
+    for split in (1, ks):
+        C = torch.full((Bt, M, N), float("nan"), device=DEV)
+        oh = torch.empty((Bt, M, N), dtype=torch.float16, device=DEV)
+        ol = torch.empty_like(oh)
+        ovf = torch.zeros(Bt, dtype=torch.int32, device=DEV)
+        K.gemm_x3(Ah, Al, Bh, Bl, inv, C, P=P, D=D, alpha_v=al, beta_v=be, gamma_v=ga, out_h=oh, out_l=ol,
+                  out_scale=64.0, overflow=ovf, active=active, a_blocked=True, b_blocked=True, o_blocked=N % 32 == 0,
+                  single=single, ksplit=split)
+        outs.append((C, oh.float() + ol.float(), ovf))
+    (c1, h1, o1), (c2, h2, o2) = outs
+    for b in range(Bt):
+        if active[b]:
+            assert torch.allclose(c1[b], c2[b], rtol=0, atol=2e-6 * c1[b].abs().max().item())
+            assert torch.allclose(h1[b], h2[b], rtol=0, atol=64 * 2e-6 * c1[b].abs().max().item())
+        else:
+            assert torch.equal(c1[b], D[b]) and torch.equal(c2[b], D[b]) and torch.equal(h1[b], h2[b])
+    assert torch.equal(o1, o2)
