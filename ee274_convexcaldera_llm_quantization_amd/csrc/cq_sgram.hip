@@ -499,196 +499,6 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
     }
 }
 
-// ------------------------------------------------------------------ fp16 slab (unweighted Y)
-// With no column weights (H = I, and the m > n transposed problem) W is exact in fp16, so
-//   P = (W - (s/2) c) c^T = W c^T - (s/2) N,   N = c c^T (integers),
-// and the slab can hold W itself in fp16 plus the R staged rows' 2-bit codes (one u32 per l,
-// row r's field at bits 2r): 2R + 4 bytes per l instead of 4R, so twice the rows per workgroup
-// (fewer passes over the ELL) and ~40 % fewer LDS bytes per FMA.  Per ELL entry (l, c_j):
-// acc_r += c_j W[r, l] (fp32 FMA of an exact fp16 value), and N through SWAR bytes: with
-// q' = the rows' code fields at l negated when c_j = -1 (offset binary: 00 <-> 10) and all
-// 01 (= code 0) for padding, each field of q' is c_j c_rl + 1 in {0, 1, 2}; four u32
-// accumulators sum them per row in 8-bit lanes (flushed every SGH_FLUSH entries), so
-// N_rj = sum - width, exactly.  P_rj = acc_r - (s/2) N_rj (one rounding).  Same ELL, order and
-// output assembly as sgram_spmm_kernel; deterministic.
-constexpr int SGH_FLUSH = 120;   // entries per SWAR flush: 2 x 120 < 256
-
-template <int R>
-struct SghLayout {   // LDS: W plane(s) l-major, then the codes plane
-    static constexpr int WB = 2 * R;           // W bytes per l (R halves)
-    static constexpr int BYTES_PER_L = WB + 4;
-};
-
-// negated fields: 00 <-> 10, 01 stays (c -> -c in offset binary)
-__device__ __forceinline__ uint32_t sg_neg_fields(uint32_t q) { return q ^ ((~q & 0x55555555u) << 1); }
-
-template <int R>
-__device__ __forceinline__ void sgh_slice(const uint16_t* __restrict__ wpl, const uint32_t* __restrict__ cpl,
-                                          int64_t L, const uint32_t* __restrict__ ep, int64_t width, float hs,
-                                          float (&acc)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    int F[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) F[r] = 0;
-    uint32_t A[4] = {0u, 0u, 0u, 0u};
-    int pend = 0;
-    auto flush = [&]() {
-#pragma unroll
-        for (int r = 0; r < R; ++r) F[r] += (int)((A[r & 3] >> (8 * (r >> 2))) & 0xffu);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) A[k] = 0u;
-        pend = 0;
-    };
-    auto entry = [&](uint32_t e) {
-        const uint32_t f = e & 3u;
-        const float c = (float)((int)f - 1);
-        const int64_t l = e >> 2;
-        // W part: R halves of column l (16-byte reads for R >= 8)
-        if constexpr (R >= 8) {
-#pragma unroll
-            for (int h = 0; h < R / 8; ++h) {
-                const uint4 raw = *reinterpret_cast<const uint4*>(wpl + ((int64_t)h * L + l) * 8);
-                const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc[8 * h + u] = __builtin_fmaf(c, (float)hv[u], acc[8 * h + u]);
-            }
-        } else {
-            const uint2 raw = *reinterpret_cast<const uint2*>(wpl + l * 4);
-            const _Float16* hv = reinterpret_cast<const _Float16*>(&raw);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] = __builtin_fmaf(c, (float)hv[u], acc[u]);
-        }
-        // N part
-        const uint32_t q = cpl[l];
-        const uint32_t qs = f == 2u ? q : (f == 0u ? sg_neg_fields(q) : 0x55555555u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) A[k] += (qs >> (2 * k)) & 0x03030303u;
-        if (++pend == SGH_FLUSH) flush();
-    };
-    int64_t t = 0;
-    if (width >= SG_PF) {
-        uint32_t cur[SG_PF];
-#pragma unroll
-        for (int q = 0; q < SG_PF; ++q) cur[q] = ep[q * SG_SLICE];
-        for (t = SG_PF; t + SG_PF <= width; t += SG_PF) {
-            uint32_t nxt[SG_PF];
-#pragma unroll
-            for (int q = 0; q < SG_PF; ++q) nxt[q] = ep[(t + q) * SG_SLICE];
-#pragma unroll
-            for (int q = 0; q < SG_PF; ++q) entry(cur[q]);
-#pragma unroll
-            for (int q = 0; q < SG_PF; ++q) cur[q] = nxt[q];
-        }
-#pragma unroll
-        for (int q = 0; q < SG_PF; ++q) entry(cur[q]);
-    }
-    for (; t < width; ++t) entry(ep[t * SG_SLICE]);
-    flush();
-    const int wdt = (int)width;
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = __builtin_fmaf(-hs, (float)(F[r] - wdt), acc[r]);
-}
-
-// P[b, i0 + r, j] for r < R, every row j of c, from the fp16 slab.  Results of the wave's
-// NSW slices held in registers, assembled 4 rows at a time in LDS (the slab's space) and
-// stored over j (k <= 4096, 4 k floats <= the slab's bytes: host check).
-template <int R, int NSW>
-__global__ __launch_bounds__(1024) void sgram_spmm_h_kernel(const _Float16* __restrict__ W,
-                                                           const uint8_t* __restrict__ packed,
-                                                           const float* __restrict__ qscale, int64_t k, int64_t L,
-                                                           const uint32_t* __restrict__ ell,
-                                                           const int32_t* __restrict__ perm,
-                                                           const int64_t* __restrict__ slice_off, int64_t stride_ell,
-                                                           float* __restrict__ P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sgh_lds[];
-    uint16_t* wpl = reinterpret_cast<uint16_t*>(sgh_lds);
-    uint32_t* cpl = sgh_lds + (int64_t)L * R / 2;   // after the W plane(s) (2R bytes per l)
-    const int64_t b = blockIdx.y;
-    const int64_t i0 = (int64_t)blockIdx.x * R;
-    const float hs = 0.5f * qscale[b];
-    const int64_t KL = k * L;
-    const uint16_t* Wb = reinterpret_cast<const uint16_t*>(W) + b * KL;
-    const uint8_t* pb = packed + b * (KL / 4);
-    // stage: thread -> 8 consecutive l; per l the R rows' halves (planes of 8 rows, 16 B per l;
-    // R = 4: one 8-byte plane) and the rows' code fields packed into one u32
-    for (int64_t l0 = (int64_t)threadIdx.x * 8; l0 < L; l0 += SG_THREADS * 8) {
-        uint32_t cw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        uint16_t wv[8][R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t i = i0 + r;
-            uint4 raw = make_uint4(0u, 0u, 0u, 0u);
-            uint32_t two = 0x5555u;   // code 0 for rows past k
-            if (i < k) {
-                raw = *reinterpret_cast<const uint4*>(Wb + i * L + l0);
-                two = *reinterpret_cast<const uint16_t*>(pb + (i * L + l0) / 4);
-            }
-            const uint16_t* hv = reinterpret_cast<const uint16_t*>(&raw);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                wv[u][r] = hv[u];
-                const uint32_t byte = (u < 4) ? (two & 0xffu) : (two >> 8);
-                cw[u] |= ((byte >> (6 - 2 * (u & 3))) & 3u) << (2 * r);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t l = l0 + u;
-            if constexpr (R >= 8) {
-#pragma unroll
-                for (int h = 0; h < R / 8; ++h) {
-                    uint4 v;
-                    v.x = (uint32_t)wv[u][8 * h] | ((uint32_t)wv[u][8 * h + 1] << 16);
-                    v.y = (uint32_t)wv[u][8 * h + 2] | ((uint32_t)wv[u][8 * h + 3] << 16);
-                    v.z = (uint32_t)wv[u][8 * h + 4] | ((uint32_t)wv[u][8 * h + 5] << 16);
-                    v.w = (uint32_t)wv[u][8 * h + 6] | ((uint32_t)wv[u][8 * h + 7] << 16);
-                    *reinterpret_cast<uint4*>(wpl + ((int64_t)h * L + l) * 8) = v;
-                }
-            } else {
-                uint2 v;
-                v.x = (uint32_t)wv[u][0] | ((uint32_t)wv[u][1] << 16);
-                v.y = (uint32_t)wv[u][2] | ((uint32_t)wv[u][3] << 16);
-                *reinterpret_cast<uint2*>(wpl + l * 4) = v;
-            }
-            cpl[l] = cw[u] | (R < 16 ? (0x55555555u & ~((1u << (2 * R)) - 1u)) : 0u);   // unused rows: code 0
-        }
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
-    const int64_t* so = slice_off + b * (ns + 1);
-    const uint32_t* eb = ell + b * stride_ell + lane;
-    const int32_t* pm = perm + b * k;
-    float* Pb = P + b * k * k;
-    float acc[NSW][R];
-#pragma unroll
-    for (int q = 0; q < NSW; ++q) {
-        const int64_t sl = wv + SG_WAVES * q;
-        if (sl < ns) sgh_slice<R>(wpl, cpl, L, eb + so[sl] * SG_SLICE, so[sl + 1] - so[sl], hs, acc[q]);
-    }
-    float* outb = reinterpret_cast<float*>(sgh_lds);   // k x 4 floats, j-major
-#pragma unroll
-    for (int r0 = 0; r0 < R; r0 += 4) {
-        __syncthreads();   // the slab (first round) / the previous round's block is fully read
-#pragma unroll
-        for (int q = 0; q < NSW; ++q) {
-            const int64_t pp = (wv + SG_WAVES * q) * SG_SLICE + lane;
-            if (pp < k)
-                *reinterpret_cast<float4*>(outb + pm[pp] * 4) =
-                    make_float4(acc[q][r0], acc[q][r0 + 1], acc[q][r0 + 2], acc[q][r0 + 3]);
-        }
-        __syncthreads();
-        for (int64_t j = threadIdx.x; j < k; j += SG_THREADS) {
-            const float4 x = *reinterpret_cast<const float4*>(outb + j * 4);
-            const float v[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (i0 + r0 + r < k) Pb[(i0 + r0 + r) * k + j] = v[r];
-        }
-    }
-}
-
 __device__ __forceinline__ float sg_split_scale(double bound) {
     int e = 0;
     if (bound > 0.0 && isfinite(bound)) frexp(bound, &e);
@@ -855,7 +665,9 @@ __global__ __launch_bounds__(256) void codes_transpose_kernel(const uint32_t* __
 // (CM_WPL per lane and block of 64 CM_WPL words) are loaded in one batch, and the next row's
 // first block while the current row is consumed.  TRANS: out is r x rows (ld ldo), written
 // through an LDS tile of the workgroup's 64 rows (coalesced over rows); else rows x r.
-constexpr int CM_LIST = 1024;   // list entries per wave (one block of 4 x 64 words holds <= 4096)
+// list entries per wave: a row of c^T holds ~1 % nonzeros (~40 at 4096 columns); a fuller
+// block is consumed in parts (the small list keeps 4 workgroups per CU in LDS)
+constexpr int CM_LIST = 256;
 constexpr int CM_WPL = 4;       // words per lane per block
 constexpr int CM_G = 16;        // entries per gather batch
 template <int RV, bool TRANS>
@@ -924,19 +736,33 @@ __global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __res
                     pre += __popcll(mk & lt) << bt;
                     tot += __popcll(mk) << bt;
                 }
-                if (cnt + tot > CM_LIST) {   // list full (tot <= 1024 = CM_LIST): consume it first
-                    __builtin_amdgcn_wave_barrier();
-                    consume();
-                    __builtin_amdgcn_wave_barrier();
-                }
-                int pos = cnt + pre;
                 const int64_t wi = w0 + 64 * t + lane;
-                while (nz) {
-                    const int p = __builtin_ctz(nz);
-                    nz &= nz - 1u;
-                    list[pos++] = (uint32_t)((16 * wi + sg_u_of_bit(p)) << 2) | ((cur[t] >> p) & 3u);
+                if (cnt + tot <= CM_LIST) {
+                    int pos = cnt + pre;
+                    while (nz) {
+                        const int p = __builtin_ctz(nz);
+                        nz &= nz - 1u;
+                        list[pos++] = (uint32_t)((16 * wi + sg_u_of_bit(p)) << 2) | ((cur[t] >> p) & 3u);
+                    }
+                    cnt += tot;
+                } else {   // the list cannot take this word group: in lane order, a list-full at a time
+                    for (int src = 0; src < 64; ++src) {
+                        const uint32_t wsrc = (uint32_t)__shfl((int)cur[t], src, 64);
+                        uint32_t nzs = sg_nz_mask(wsrc);
+                        const int64_t wis = w0 + 64 * t + src;
+                        while (nzs) {   // wave-uniform
+                            const int p = __builtin_ctz(nzs);
+                            nzs &= nzs - 1u;
+                            if (cnt == CM_LIST) {
+                                __builtin_amdgcn_wave_barrier();
+                                consume();
+                                __builtin_amdgcn_wave_barrier();
+                            }
+                            if (lane == 0) list[cnt] = (uint32_t)((16 * wis + sg_u_of_bit(p)) << 2) | ((wsrc >> p) & 3u);
+                            ++cnt;
+                        }
+                    }
                 }
-                cnt += tot;
             }
             // the next block of this row, or the first block of the next row, in flight while
             // this list is consumed
@@ -1113,36 +939,12 @@ int cq_sgram_rows(int64_t L) {
     return 0;
 }
 
-// fp16-slab rows per workgroup for contraction length L (0: not applicable): the slab
-// (2R + 4 bytes per l) fits 150 KB and the 4-row output block (4 k floats) fits the slab
-static int sgh_rows(int64_t k, int64_t L) {
-    if (k > 4096) return 0;   // <= 4 slices per wave held in registers
-    // (R = 16 would hold 64 results per lane and spill: 128 VGPRs + 88 spilled)
-    for (int r : {8, 4}) {
-        const size_t slab = (size_t)L * (2 * r + 4);
-        if (slab <= 150 * 1024 && (size_t)k * 4 * sizeof(float) <= slab) return r;
-    }
-    return 0;
-}
-
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
                   int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
                   const int64_t* slice_off, int64_t stride_ell, float* P, void* stream) {
     CQ_REQUIRE(W && packed && qscale && ell && perm && slice_off && P, "cq_sgram_spmm: null argument");
     CQ_REQUIRE(dtype == CQ_F16, "cq_sgram_spmm: fp16 W only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L % 64 == 0, "cq_sgram_spmm: bad shape");
-    const int rh = wcol ? 0 : sgh_rows(k, L);
-    if (rh > 0) {   // unweighted: the fp16 slab
-        const size_t lds = (size_t)L * (2 * rh + 4);
-        const dim3 grid((unsigned)ceil_div(k, rh), (unsigned)batch);
-        const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
-#define CQ_SH(RR) sgram_spmm_h_kernel<RR, 4><<<grid, SG_THREADS, lds, as_stream(stream)>>>(Wh, packed, qscale, k, L, \
-                                                                                          ell, perm, slice_off, \
-                                                                                          stride_ell, P)
-        if (rh == 8) CQ_SH(8); else CQ_SH(4);
-#undef CQ_SH
-        return check_launch("cq_sgram_spmm");
-    }
     const int R = cq_sgram_rows(L);
     CQ_REQUIRE(R > 0, "cq_sgram_spmm: rows of %lld values do not fit the LDS", (long long)L);
     size_t lds = (size_t)L * R * sizeof(float);
