@@ -86,8 +86,12 @@ __global__ __launch_bounds__(BT) void bj_init_kernel(double* __restrict__ A_all,
     }
 }
 
-// One workgroup per (pair q, matrix b): diagonalise the 64 x 64 subproblem in LDS.
-__global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all, int p, int nblk, int step,
+// One workgroup per (pair q, matrix b): diagonalise the 64 x 64 subproblem in LDS.  ST threads:
+// 256, or 1024 when the launch has fewer subproblems than the chip has CUs (a single caldera()
+// call: 3 pairs at p = 192), so each round's rotation updates take a quarter of the time
+// (every element is updated by one thread with the same arithmetic either way).
+template <int ST>
+__global__ __launch_bounds__(ST) void bj_solve_kernel(double* __restrict__ A_all, int p, int nblk, int step,
                                                       double thr, double* __restrict__ Vs_all,
                                                       int* __restrict__ rot_all, const int* __restrict__ done,
                                                       double* __restrict__ part_off, double* __restrict__ part_dg,
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
     rr(nblk, step, q, a, c);
     if (tid < D) gi[tid] = gidx(a, c, tid, p);
     __syncthreads();
-    for (int t = tid; t < D * D; t += BT) {
+    for (int t = tid; t < D * D; t += ST) {
         const int u = t / D, v = t % D;
         const int gu = gi[u], gv = gi[v];
         As[u * LDP + v] = (gu >= 0 && gv >= 0) ? A[(int64_t)gu * p + gv] : 0.0;
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
             }
             __syncthreads();
             // A <- J^T A J on the 32 x 32 pair-blocks (each element belongs to one block)
-            for (int t = tid; t < NB * NB; t += BT) {
+            for (int t = tid; t < NB * NB; t += ST) {
                 const int qa = t / NB, qb = t % NB;
                 const double sa = sn[qa], sb = sn[qb];
                 if (sa == 0.0 && sb == 0.0) continue;
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
                 As[ja * LDP + ib] = z10; As[ja * LDP + jb] = z11;
             }
             // V <- V J (columns i, j of every row)
-            for (int t = tid; t < D * NB; t += BT) {
+            for (int t = tid; t < D * NB; t += ST) {
                 const int u = t / NB, qq = t % NB;
                 const double ss = sn[qq];
                 if (ss == 0.0) continue;
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
     }
     // write back the (block-)diagonalised subproblem, its V, and its square sums
     double off = 0.0, dg = 0.0;
-    for (int t = tid; t < D * D; t += BT) {
+    for (int t = tid; t < D * D; t += ST) {
         const int u = t / D, v = t % D;
         const int gu = gi[u], gv = gi[v];
         if (gu < 0 || gv < 0) continue;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(BT) void bj_solve_kernel(double* __restrict__ A_all
     }
     double* Vs = Vs_all + (b * npair + q) * (int64_t)(D * D);
     if (rotated)
-        for (int t = tid; t < D * D; t += BT) Vs[t] = Vsm[(t / D) * LDP + (t % D)];
+        for (int t = tid; t < D * D; t += ST) Vs[t] = Vsm[(t / D) * LDP + (t % D)];
     const double offs = block_sum_f64(off, red);
     const double dgs = block_sum_f64(dg, red);
     if (tid == 0) {
@@ -428,8 +432,12 @@ int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double
     if (phase & BJ_SWEEPS) {
         for (int sw = 0; sw < nsweeps; ++sw) {
             for (int st = 0; st < nblk - 1; ++st) {
-                bj_solve_kernel<<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(A, (int)p, nblk, st, thr, Vs, rot,
-                                                                                       done, poff, pdg, nslots);
+                if (npair * batch < kCUs)
+                    bj_solve_kernel<1024><<<dim3((unsigned)npair, (unsigned)batch), 1024, 0, s>>>(
+                        A, (int)p, nblk, st, thr, Vs, rot, done, poff, pdg, nslots);
+                else
+                    bj_solve_kernel<BT><<<dim3((unsigned)npair, (unsigned)batch), BT, 0, s>>>(
+                        A, (int)p, nblk, st, thr, Vs, rot, done, poff, pdg, nslots);
                 const int nupd = noff + (want_v ? npair * nch : 0);   // 0: one pair, values only
                 if (nupd > 0)
                     bj_update_kernel<<<dim3((unsigned)nupd, (unsigned)batch), BT, 0, s>>>(

@@ -106,12 +106,36 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
             hist[v] = acc;
             acc += c;
         }
-        for (int64_t j = 0; j < k; ++j) pm[hist[min(nz[j], SG_BINS - 1)]++] = (int32_t)j;
-        if (row_corr) {   // the rows' norm corrections, summed in row order
-            double cs = 0.0;
-            for (int64_t j = 0; j < k; ++j) cs += row_corr[b * k + j];
-            corr_out[b] = cs;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        // stable placement, 64 rows at a time by wave 0: per distinct bin of the chunk (ballot),
+        // its rows take consecutive positions in row order
+        const int lane = threadIdx.x;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (int64_t c0 = 0; c0 < k; c0 += 64) {
+            const int64_t j = c0 + lane;
+            const int bin = j < k ? min(nz[j], SG_BINS - 1) : -1;
+            uint64_t todo = __ballot(j < k);
+            while (todo) {
+                const int leader = __builtin_ctzll(todo);
+                const int bl = __shfl(bin, leader, 64);
+                const uint64_t mk = __ballot(bin == bl);
+                const int base = hist[bl];
+                if (bin == bl) pm[base + __popcll(mk & lt)] = (int32_t)j;
+                __builtin_amdgcn_wave_barrier();
+                if (lane == leader) hist[bl] = base + __popcll(mk);
+                __builtin_amdgcn_wave_barrier();
+                todo &= ~mk;
+            }
         }
+    }
+    if (row_corr) {   // the rows' norm corrections: fixed per-thread subsets, fixed reduction
+        __shared__ double red[16];
+        double cs = 0.0;
+        for (int64_t j = threadIdx.x; j < k; j += blockDim.x) cs += row_corr[b * k + j];
+        cs = block_sum_f64(cs, red);
+        if (threadIdx.x == 0) corr_out[b] = cs;
     }
     __syncthreads();
     const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;

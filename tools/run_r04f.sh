@@ -18,3 +18,6 @@ done
 mkdir -p $O/kt_cfg2
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt_cfg2/t -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-api-path > $O/kt_cfg2/s.log 2>&1 || exit $?
 python3 tools/ktrace_summary.py $O/kt_cfg2 > $O/kt_cfg2/summary.txt; head -30 $O/kt_cfg2/summary.txt | cut -c1-150
+mkdir -p $O/kt_single
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_single/t -o run --output-format csv -- python3 tools/bench_single.py 3 > $O/kt_single/s.log 2>&1 || exit $?
+python3 tools/ktrace_summary.py $O/kt_single > $O/kt_single/summary.txt; head -16 $O/kt_single/summary.txt | cut -c1-150; grep median $O/kt_single/s.log
