@@ -534,11 +534,19 @@ class BlockJacobi:
                                             _p(ev), _p(V32), None, _p(sw), _p(self.pending), _p(self.ws),
                                             self.ws.numel(), _stream(self.A.device)), "cq_jacobi_eigh_staged")
 
-    def sweeps(self, n: int, begin: bool = False) -> int:
-        """n more sweeps; returns the number of matrices still unconverged (host read-back)."""
+    def launch(self, n: int, begin: bool = False):
+        """n more sweeps (stream-ordered, no host sync)."""
         self._call((self.BEGIN if begin else 0) | self.SWEEPS, n)
         self.swept += n
+
+    def pending_count(self) -> int:
+        """Matrices still unconverged after the sweeps launched so far (host read-back)."""
         return int(self.pending.item())
+
+    def sweeps(self, n: int, begin: bool = False) -> int:
+        """n more sweeps; returns the number of matrices still unconverged (host read-back)."""
+        self.launch(n, begin)
+        return self.pending_count()
 
     def finish(self):
         dev = self.A.device

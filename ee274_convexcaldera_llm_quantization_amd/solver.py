@@ -135,7 +135,7 @@ JACOBI_MAX_SWEEPS = 30
 # stream-ordered): a first batch of sweeps sized from the previous call, then BJ_STEP more at a
 # time while the device count of unconverged matrices (one int read back) is nonzero
 BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
-BJ_SMALL_BATCH = 8  # batches this small take the block Jacobi at every p
+BJ_SMALL_SUBPROBLEMS = 256  # batches with at most this many 64 x 64 block-Jacobi subproblems take it at every p
 STALL_RATIO = 0.98
 
 
@@ -200,9 +200,12 @@ class RankRSolver:
         # Rayleigh-Ritz sweep budget: fixed for the one-workgroup Jacobi (its sweep loop runs
         # inside one kernel), adaptive for the block Jacobi (each sweep is a set of launches)
         # block Jacobi over many workgroups where one CU cannot hold the problem (p > 192), and
-        # for small batches, where the one-workgroup-per-matrix kernel leaves the chip idle (one
-        # caldera() call: ~4 ms per 192 x 192 eigensolve on one CU)
-        self.block_jacobi = self.p > 192 or B <= BJ_SMALL_BATCH
+        # for batches whose 64 x 64 subproblems (p / 64 per matrix) do not outnumber the CUs,
+        # where the one-workgroup-per-matrix kernel (~4 ms per 192 x 192 eigensolve on one CU)
+        # would leave most of the chip idle: one caldera() call, config 4's batches of 64, the
+        # 8-GPU model run's batches of 16
+        nblk = -(-self.p // 32)
+        self.block_jacobi = self.p > 192 or B * ((nblk + (nblk & 1)) // 2) <= BJ_SMALL_SUBPROBLEMS
         self.bj_first = BJ_FIRST  # block Jacobi: sweeps launched before the first read-back
         self._bufs = None
         self._G = None
@@ -302,7 +305,7 @@ class RankRSolver:
         return out, info
 
     def _rr(self, X, *keep, single=False, values_only=False):
-        """Rayleigh-Ritz on the block X.  single: Z = G X with one fp16 product (cheap outer
+        """Rayleigh-Ritz on the block X (generator: yields before the block Jacobi's read-backs).  single: Z = G X with one fp16 product (cheap outer
         iterations: the Ritz values only set the next filter's bounds, and the residuals it
         reports sit at the ~1.5e-4 floor of that product, far above the tolerance, so no
         matrix can be declared converged on them).  values_only: Ritz values only, X returned
@@ -322,10 +325,10 @@ class RankRSolver:
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps
-            theta, _, _, sw = self._eigh(T, self.jacobi_tol_values, want_vectors=False)
+            theta, _, _, sw = yield from self._eigh(T, self.jacobi_tol_values, want_vectors=False)
             self._last_sw = sw
             return theta, X, None
-        theta, V32, _, sw = self._eigh(T, self.jacobi_tol)
+        theta, V32, _, sw = yield from self._eigh(T, self.jacobi_tol)
         self._last_sw = sw
         Xo = self._free(X, Z, *keep)
         K.gemm(X, V32, C=Xo)
@@ -337,14 +340,20 @@ class RankRSolver:
         """Rayleigh-Ritz eigensolve (descending).  p <= 192: one launch to convergence (A in
         one CU's LDS).  p > 192: block Jacobi in stages -- bj_first sweeps, then BJ_STEP at a
         time while matrices remain unconverged (one int read back per stage); bj_first follows
-        what the last call needed, so a warm call usually reads back once."""
+        what the last call needed, so a warm call usually reads back once.  Generator: yields
+        before each read-back, so batches interleaved on other streams (overlap.py) keep
+        issuing while this one waits."""
         if not self.block_jacobi:
             return K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=tol, want_vectors=want_vectors)
         bj = K.BlockJacobi(T, tol, want_vectors)
         first = min(self.bj_first, JACOBI_MAX_SWEEPS)
-        left = bj.sweeps(first, begin=True)
+        bj.launch(first, begin=True)
+        yield
+        left = bj.pending_count()
         while left and bj.swept < JACOBI_MAX_SWEEPS:
-            left = bj.sweeps(min(BJ_STEP, JACOBI_MAX_SWEEPS - bj.swept))
+            bj.launch(min(BJ_STEP, JACOBI_MAX_SWEEPS - bj.swept))
+            yield
+            left = bj.pending_count()
         self.bj_first = bj.swept if bj.swept > first else max(BJ_MIN_FIRST, first - 1)
         self.stats.bj_readbacks += 1 + (bj.swept - first + BJ_STEP - 1) // BJ_STEP
         return bj.finish()
@@ -546,7 +555,7 @@ class RankRSolver:
                 X[:, self.valid_k:, :] = 0.0
             X, _ = self._cholqr(X)
             X, _ = self._cholqr(X)
-            theta, X, Z = self._rr(X, single=self.cheap_cold > 0, values_only=self.cheap_cold > 0)
+            theta, X, Z = yield from self._rr(X, single=self.cheap_cold > 0, values_only=self.cheap_cold > 0)
             ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
             yield
             ends = ends.cpu().numpy()
@@ -590,7 +599,7 @@ class RankRSolver:
                 Xf = self._filter(X, coef, single=cheap)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._cholqr(Xa, X)
-                theta_n, Xn, Zn = self._rr(Xb, X, single=cheap, values_only=cheap)
+                theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
                 # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
                 # stopping test: estimated relative error of the rank-r projection of Y (a
                 # residual relative to theta_0 over-converges flat spectra and under-converges
@@ -659,7 +668,7 @@ class RankRSolver:
             if not live.any():
                 break
         if Z is None:  # left the loop on a values-only iteration (MAX_OUTER): rotate once
-            theta, X, Z = self._rr(X)
+            theta, X, Z = yield from self._rr(X)
         self.stats.history.append((cold, used, list(self.stats.resid_hist)))
         # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
         # one CholQR pass restores orthonormality without moving the converged subspace
