@@ -91,13 +91,24 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
                                                            int32_t* __restrict__ perm, int64_t* __restrict__ slice_off,
                                                            int64_t* __restrict__ total, const double* __restrict__ row_corr,
                                                            double* __restrict__ corr_out) {
+    // stable counting sort, the four waves on four contiguous row ranges: per-wave bin counts,
+    // bin starts (descending), each wave's base per bin = start + the counts of the waves before
+    // it; then every wave places its rows in row order (ballots per distinct bin of a 64-row chunk)
     __shared__ int32_t hist[SG_BINS];
+    __shared__ int32_t wbase[4][SG_BINS];
     const int64_t b = blockIdx.x;
     const int32_t* nz = row_nnz + b * k;
     int32_t* pm = perm + b * k;
-    for (int v = threadIdx.x; v < SG_BINS; v += blockDim.x) hist[v] = 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t per = (k + 255) / 256 * 64;   // rows per wave, whole 64-row chunks
+    const int64_t r0 = wv * per, r1 = min<int64_t>(k, r0 + per);
+    for (int v = threadIdx.x; v < SG_BINS; v += blockDim.x)
+        for (int w = 0; w < 4; ++w) wbase[w][v] = 0;
     __syncthreads();
-    for (int64_t j = threadIdx.x; j < k; j += blockDim.x) atomicAdd(&hist[min(nz[j], SG_BINS - 1)], 1);
+    for (int64_t j = r0 + lane; j < r1; j += 64) atomicAdd(&wbase[wv][min(nz[j], SG_BINS - 1)], 1);
+    __syncthreads();
+    for (int v = threadIdx.x; v < SG_BINS; v += blockDim.x)
+        hist[v] = wbase[0][v] + wbase[1][v] + wbase[2][v] + wbase[3][v];
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t acc = 0;  // descending: bin v starts after every row with a larger count
@@ -108,23 +119,30 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
         }
     }
     __syncthreads();
-    if (threadIdx.x < 64) {
-        // stable placement, 64 rows at a time by wave 0: per distinct bin of the chunk (ballot),
-        // its rows take consecutive positions in row order
-        const int lane = threadIdx.x;
+    for (int v = threadIdx.x; v < SG_BINS; v += blockDim.x) {
+        int32_t acc = hist[v];
+        for (int w = 0; w < 4; ++w) {
+            const int32_t c = wbase[w][v];
+            wbase[w][v] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    {
         const uint64_t lt = (1ull << lane) - 1ull;
-        for (int64_t c0 = 0; c0 < k; c0 += 64) {
+        int32_t* base_w = wbase[wv];
+        for (int64_t c0 = r0; c0 < r1; c0 += 64) {
             const int64_t j = c0 + lane;
-            const int bin = j < k ? min(nz[j], SG_BINS - 1) : -1;
-            uint64_t todo = __ballot(j < k);
+            const int bin = j < r1 ? min(nz[j], SG_BINS - 1) : -1;
+            uint64_t todo = __ballot(j < r1);
             while (todo) {
                 const int leader = __builtin_ctzll(todo);
                 const int bl = __shfl(bin, leader, 64);
                 const uint64_t mk = __ballot(bin == bl);
-                const int base = hist[bl];
+                const int base = base_w[bl];
                 if (bin == bl) pm[base + __popcll(mk & lt)] = (int32_t)j;
                 __builtin_amdgcn_wave_barrier();
-                if (lane == leader) hist[bl] = base + __popcll(mk);
+                if (lane == leader) base_w[bl] = base + __popcll(mk);
                 __builtin_amdgcn_wave_barrier();
                 todo &= ~mk;
             }
