@@ -101,8 +101,8 @@ __global__ __launch_bounds__(ST) void bj_solve_kernel(double* __restrict__ A_all
     if (done[b]) return;
     __shared__ double As[D * LDP];
     __shared__ double Vsm[D * LDP];
-    __shared__ double cs[NB], sn[NB];
-    __shared__ int pi_[NB], pj_[NB];
+    __shared__ double2 csn[NB];   // (cos, sin) of slot q's rotation: one 16-byte read
+    __shared__ int2 pij[NB];      // its (i, j): one 8-byte read
     __shared__ int gi[D];
     __shared__ int any_rot;
     __shared__ double red[16];
@@ -130,16 +130,18 @@ __global__ __launch_bounds__(ST) void bj_solve_kernel(double* __restrict__ A_all
                 double cc, ss;
                 rot_params(As[i * LDP + i], As[j * LDP + j], As[i * LDP + j], thr, cc, ss);
                 if (ss != 0.0) any_rot = 1;
-                cs[tid] = cc; sn[tid] = ss; pi_[tid] = i; pj_[tid] = j;
+                csn[tid] = make_double2(cc, ss); pij[tid] = make_int2(i, j);
             }
             __syncthreads();
             // A <- J^T A J on the 32 x 32 pair-blocks (each element belongs to one block)
             for (int t = tid; t < NB * NB; t += ST) {
                 const int qa = t / NB, qb = t % NB;
-                const double sa = sn[qa], sb = sn[qb];
+                const double2 ra = csn[qa], rb = csn[qb];
+                const double sa = ra.y, sb = rb.y;
                 if (sa == 0.0 && sb == 0.0) continue;
-                const double ca = cs[qa], cb = cs[qb];
-                const int ia = pi_[qa], ja = pj_[qa], ib = pi_[qb], jb = pj_[qb];
+                const double ca = ra.x, cb = rb.x;
+                const int2 ea = pij[qa], eb = pij[qb];
+                const int ia = ea.x, ja = ea.y, ib = eb.x, jb = eb.y;
                 const double x00 = As[ia * LDP + ib], x01 = As[ia * LDP + jb];
                 const double x10 = As[ja * LDP + ib], x11 = As[ja * LDP + jb];
                 const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
@@ -153,10 +155,12 @@ __global__ __launch_bounds__(ST) void bj_solve_kernel(double* __restrict__ A_all
             // V <- V J (columns i, j of every row)
             for (int t = tid; t < D * NB; t += ST) {
                 const int u = t / NB, qq = t % NB;
-                const double ss = sn[qq];
+                const double2 rq = csn[qq];
+                const double ss = rq.y;
                 if (ss == 0.0) continue;
-                const double cc = cs[qq];
-                const int i = pi_[qq], j = pj_[qq];
+                const double cc = rq.x;
+                const int2 eq = pij[qq];
+                const int i = eq.x, j = eq.y;
                 const double vi = Vsm[u * LDP + i], vj = Vsm[u * LDP + j];
                 Vsm[u * LDP + i] = cc * vi - ss * vj;
                 Vsm[u * LDP + j] = ss * vi + cc * vj;

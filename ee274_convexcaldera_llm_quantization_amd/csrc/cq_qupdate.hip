@@ -26,7 +26,8 @@ namespace cq {
 // The end-of-chunk wait is counted (the ring's newest slot stays in flight); only pass 1's
 // code stores, gathered over 16 chunks into whole 128-B row segments, need a full drain
 // (vmcnt also counts stores, which may complete out of order with the loads).
-constexpr int QP_WAVES = 8;               // default waves per workgroup (template parameter NW)
+constexpr int QP_WAVES = 8;               // default waves per workgroup (template parameter NW);
+                                          // the 2-bit list path at K <= 128 runs 12 (qp_cand_waves)
 constexpr int QP_WD = 5;                  // W ring slots (WL path)
 constexpr size_t QP_LDS_MAX = 156 * 1024;
 
@@ -52,10 +53,12 @@ __device__ __forceinline__ void qp_issue_r(const uint16_t* __restrict__ Rh, cons
     constexpr int RPI = 512 / RROW;            // rows per wave-instruction
     constexpr int LPR = RROW / 8;              // lanes per row
     constexpr int NI = 2 * QP_BN / RPI;        // instructions per stage
-    static_assert(NI % NW == 0, "stage split over the waves");
+    // waves take instructions wid, wid + NW, ... (NW need not divide NI: the counted waits
+    // only count the W loads issued after a stage)
 #pragma unroll
-    for (int u = 0; u < NI / NW; ++u) {
-        const int I = wid * (NI / NW) + u;
+    for (int u = 0; u < (NI + NW - 1) / NW; ++u) {
+        const int I = wid + u * NW;
+        if (I >= NI) break;
         const int half = I / (NI / 2), rowbase = RPI * (I % (NI / 2));
         const int row = rowbase + lane / LPR;
         const int logical = (lane % LPR) ^ qp_swz(row);
@@ -253,7 +256,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     // so the epilogue's VALU work of row block rb overlaps the MFMAs of rb + 1 (independent
     // registers) instead of waiting for all of them; the MFMA order per accumulator (K steps,
     // then al x lh, ah x ll, ah x lh) is the same as mma()'s, so the sums are bit-identical.
-    constexpr bool UPF = KSMAX <= 4 && (PASS == 0 || PASS == 2);
+    constexpr bool UPF = KSMAX <= 4 && (PASS == 0 || PASS == 2) && NW <= 8;
     auto compute = [&](int64_t ch, const uint4 (&wc)[RB][WV], const _Float16* st) -> bool {
         const int64_t n0 = ch * QP_BN;
         bool stored = false;
@@ -538,7 +541,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     }
 }
 
-static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) <= QP_LDS_MAX && qp_lds_bytes(QP_WAVES, 2, 8, true) <= QP_LDS_MAX,
+static_assert(qp_lds_bytes(QP_WAVES, 3, 4, true) <= QP_LDS_MAX && qp_lds_bytes(QP_WAVES, 2, 8, true) <= QP_LDS_MAX &&
+                  qp_lds_bytes(12, 2, 4, true) <= QP_LDS_MAX,
               "Q-update LDS: R^T stages + W ring fit one CU (160 KB, static reduction scratch aside)");
 
 template <int PASS, int BITS, int DT, int RB, int KSMAX, int NW, bool WL>
@@ -651,7 +655,11 @@ __global__ void qp_finalize_cand_kernel(QUK q, int panels, int nw, float* scale,
     }
 }
 
-int qp_cand_rows(int K) { return 16 * (K <= 128 ? 3 : 2); }
+// list path geometry: K <= 128 runs 12 waves of 2 row blocks (three waves per SIMD at <= 168
+// VGPRs: the fragments are read per K step instead of up front), K <= 256 8 waves of 2
+constexpr int QP_CAND_NW_SMALL = 12;
+int qp_cand_rows(int K) { (void)K; return 32; }
+int qp_cand_waves(int K) { return K <= 128 ? QP_CAND_NW_SMALL : QP_WAVES; }
 
 bool qp_cand_ok(int64_t m, int64_t n, int K) {
     // the code kernel holds a wave region's packed codes (rows x n / 4 bytes) in LDS
@@ -663,25 +671,25 @@ int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uin
                        int K, int64_t batch, float eps, float* scale_out, double* err_out, hipStream_t s) {
     const int64_t m = q.m, n = q.n;
     const bool small = K <= 128;
-    const int rb = small ? 3 : 2;
-    const int64_t panels = ceil_div(m, (int64_t)QP_WAVES * 16 * rb);
-    if (panels * batch * QP_WAVES >= (1ll << 31)) return -1;
+    const int rb = 2, nw = qp_cand_waves(K);
+    const int64_t panels = ceil_div(m, (int64_t)nw * 16 * rb);
+    if (panels * batch * nw >= (1ll << 31)) return -1;
     const unsigned g = (unsigned)(panels * batch);
     const unsigned gf = (unsigned)std::min<int64_t>(panels * batch, kCUs);   // fallback pass 1
     const int rpw = 16 * rb;
     const size_t lds = (size_t)rpw * n / 4;
     q.only_fallback = 0;
-#define CQ_QPC(PS, RBV, KSV)                                                               \
-    q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, QP_WAVES, true><<<PS == 2 ? g : gf, QP_WAVES * 64, \
-        qp_lds_bytes(QP_WAVES, RBV, KSV, true), s>>>(                                              \
+#define CQ_QPC(PS, RBV, KSV, NWV)                                                          \
+    q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, NWV, true><<<PS == 2 ? g : gf, NWV * 64,    \
+        qp_lds_bytes(NWV, RBV, KSV, true), s>>>(                                           \
         q, Lh, Ll, Rth, Rtl, K, (int)panels)
-    if (small) CQ_QPC(2, 3, 4); else CQ_QPC(2, 2, 8);
-    qp_codes_kernel<<<(unsigned)(panels * batch * QP_WAVES), 256, lds, s>>>(q, (int)panels, QP_WAVES, rpw);
+    if (small) CQ_QPC(2, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(2, 2, 8, QP_WAVES);
+    qp_codes_kernel<<<(unsigned)(panels * batch * nw), 256, lds, s>>>(q, (int)panels, nw, rpw);
     q.only_fallback = 1;
-    if (small) CQ_QPC(1, 3, 4); else CQ_QPC(1, 2, 8);
+    if (small) CQ_QPC(1, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(1, 2, 8, QP_WAVES);
 #undef CQ_QPC
     q.only_fallback = 0;
-    qp_finalize_cand_kernel<<<(unsigned)batch, 64, 0, s>>>(q, (int)panels, QP_WAVES, scale_out, err_out);
+    qp_finalize_cand_kernel<<<(unsigned)batch, 64, 0, s>>>(q, (int)panels, nw, scale_out, err_out);
     (void)eps;
     return panels;
 }

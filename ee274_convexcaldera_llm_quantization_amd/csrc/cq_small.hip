@@ -259,11 +259,9 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int P = p + (p & 1);
     const int H = P / 2;
-    double* cs = reinterpret_cast<double*>(smem_raw);   // H
-    double* sn = cs + H;                                // H
-    int* lo = reinterpret_cast<int*>(sn + H);           // H  (smaller index of pair k)
-    int* hi = lo + H;                                   // H
-    int* flp = hi + H;                                  // H  (seat 2k holds the larger index)
+    double2* csn = reinterpret_cast<double2*>(smem_raw);  // H: (cos, sin) of pair k's rotation
+    int2* lohi = reinterpret_cast<int2*>(csn + H);         // H: (smaller, larger) index of pair k
+    int* flp = reinterpret_cast<int*>(lohi + H);           // H  (seat 2k holds the larger index)
     int* seat = flp + H;                                // P
     int* seat2 = seat + P;                              // P
     int* rnk = seat2 + P;                               // P
@@ -296,6 +294,25 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
         }
     __syncthreads();
     const double skip_rel = fmax(1e-17, 0.01 * tol);
+    // this thread's pair blocks (qa <= qb) of the JBR == 1 update, fixed for the whole solve
+    // (only the indices the pairs hold change between rounds): H (H + 1) / 2 <= 4656 blocks
+    // for p <= 192, at most JMB per thread
+    constexpr int JMB = 5;
+    const int nblk = H * (H + 1) / 2;
+    int bqa[JMB], bqb[JMB];
+#pragma unroll
+    for (int u = 0; u < JMB; ++u) {
+        const int e = tid + u * NTH;
+        bqa[u] = -1;
+        bqb[u] = 0;
+        if (JBR == 1 && e < nblk) {
+            int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+            if (qb * (qb + 1) / 2 > e) --qb;
+            if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
+            bqa[u] = e - qb * (qb + 1) / 2;
+            bqb[u] = qb;
+        }
+    }
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                         act = 1;
                     }
                 }
-                cs[k] = c; sn[k] = s; lo[k] = i; hi[k] = j; flp[k] = se > so;
+                csn[k] = make_double2(c, s); lohi[k] = make_int2(i, j); flp[k] = se > so;
                 // seats of the next round (circle shift with fixed adjacent pairs)
                 seat2[2 * k] = (k == 0) ? se : (k == 1) ? seat[1] : seat[2 * k - 2];
                 seat2[2 * k + 1] = (k == H - 1) ? se : seat[2 * k + 3];
@@ -337,19 +354,19 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             const bool any = __syncthreads_or(act);
             if (any) {
                 // ---- A <- J^T A J on pair blocks (qa <= qb) in LDS
-                const int nblk = H * (H + 1) / 2;
                 if constexpr (JBR == 1) {
-                    // one pair block at a time, few live values (V stays in registers)
-#pragma unroll 1
-                    for (int e = tid; e < nblk; e += NTH) {
-                        int qb = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-                        if (qb * (qb + 1) / 2 > e) --qb;
-                        if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
-                        const int qa = e - qb * (qb + 1) / 2;
-                        const double sa = sn[qa], sb = sn[qb];
+                    // one pair block at a time, few live values (V stays in registers); a
+                    // pair's rotation and indices are two 16- and 8-byte reads
+#pragma unroll
+                    for (int u = 0; u < JMB; ++u) {
+                        const int qa = bqa[u], qb = bqb[u];
+                        if (qa < 0) continue;
+                        const double2 rca = csn[qa], rcb = csn[qb];
+                        const double sa = rca.y, sb = rcb.y;
                         if (sa == 0.0 && sb == 0.0) continue;
-                        const double ca = cs[qa], cb = cs[qb];
-                        const int ia = lo[qa], ja = hi[qa], ib = lo[qb], jb = hi[qb];
+                        const double ca = rca.x, cb = rcb.x;
+                        const int2 pa = lohi[qa], pb = lohi[qb];
+                        const int ia = pa.x, ja = pa.y, ib = pb.x, jb = pb.y;
                         const bool va = ja < p, vb = jb < p;
                         if (qa == qb) {
                             if (!va) continue;
@@ -392,8 +409,8 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                             if (qb * (qb + 1) / 2 > e) --qb;
                             if ((qb + 1) * (qb + 2) / 2 <= e) ++qb;
                             const int qa = e - qb * (qb + 1) / 2;
-                            ca[u] = cs[qa]; sa[u] = sn[qa]; cb[u] = cs[qb]; sb[u] = sn[qb];
-                            const int ia = lo[qa], ja = hi[qa], ib = lo[qb], jb = hi[qb];
+                            ca[u] = csn[qa].x; sa[u] = csn[qa].y; cb[u] = csn[qb].x; sb[u] = csn[qb].y;
+                            const int ia = lohi[qa].x, ja = lohi[qa].y, ib = lohi[qb].x, jb = lohi[qb].y;
                             const bool va = ja < p, vb = jb < p;
                             if ((sa[u] != 0.0 || sb[u] != 0.0) && (qa != qb || va)) {
                                 live[u] = true;
@@ -435,7 +452,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                     if (!wantv) break;
                     const int k = k0 + u;
                     if (k < H) {
-                        const float c = (float)cs[k], s = (float)sn[k];
+                        const float c = (float)csn[k].x, s = (float)csn[k].y;
                         if (s != 0.f) {
                             const bool f = flp[k] != 0;
 #pragma unroll

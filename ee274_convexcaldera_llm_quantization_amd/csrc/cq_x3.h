@@ -86,6 +86,7 @@ int64_t qp_launch(QUK& q, int dtype, int bits, const uint16_t* Lh, const uint16_
 // The single-recompute 2-bit path's geometry (rows per wave) and whether it applies: fp16 W,
 // K <= 256, a wave region's packed codes fit the code kernel's LDS.
 int qp_cand_rows(int K);
+int qp_cand_waves(int K);
 bool qp_cand_ok(int64_t m, int64_t n, int K);
 // Launches pass 2, the code kernel, the fallback pass 1 and the finalize (scale, error,
 // fallback flags); q.ovf / q.absmax zeroed, q.list / q.cnt / q.part0 / q.partF sized by

@@ -1426,8 +1426,9 @@ static int64_t qu_tiles(int64_t m, int64_t n) {
 // the single-recompute 2-bit path's buffers (qp_launch_cand) for the larger of its two
 // geometries (rows per wave 32 or 48): overflow flags | counts | pass-2 partials |
 // corrections | group ids | group residuals (1 / QP_CAP_DIV of a region's 8-element groups)
-static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int64_t* regions_out, int64_t* cap_out) {
-    const int64_t regions = ceil_div(m, (int64_t)rpw * 8) * 8, cap = ceil_div((int64_t)rpw * n / 8, QP_CAP_DIV);
+static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int nw, int64_t* regions_out,
+                           int64_t* cap_out) {
+    const int64_t regions = ceil_div(m, (int64_t)rpw * nw) * nw, cap = ceil_div((int64_t)rpw * n / 8, QP_CAP_DIV);
     if (regions_out) *regions_out = regions;
     if (cap_out) *cap_out = cap;
     return align_up((size_t)batch * 4, 256) + align_up((size_t)batch * regions * 4, 256) +
@@ -1435,7 +1436,8 @@ static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int64_t
            (size_t)batch * regions * cap * 32;
 }
 static size_t qu_cand_bytes(int64_t m, int64_t n, int64_t batch) {
-    return std::max(qu_cand_geom(m, n, batch, 32, nullptr, nullptr), qu_cand_geom(m, n, batch, 48, nullptr, nullptr));
+    return std::max(qu_cand_geom(m, n, batch, qp_cand_rows(128), qp_cand_waves(128), nullptr, nullptr),
+                    qu_cand_geom(m, n, batch, qp_cand_rows(256), qp_cand_waves(256), nullptr, nullptr));
 }
 
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint) {
@@ -1453,7 +1455,7 @@ int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out
     if (!(r > 0 && r % XW_BK == 0 && qp_cand_ok(m, n, (int)r)))
         return set_error(CQ_EINVAL, "cq_q_update_list_geometry: (m, n, r) do not take the list path");
     const int rpw = qp_cand_rows((int)r);
-    qu_cand_geom(m, n, 1, rpw, nullptr, cap_out);
+    qu_cand_geom(m, n, 1, rpw, qp_cand_waves((int)r), nullptr, cap_out);
     *rows_out = rpw;
     return CQ_OK;
 }
@@ -1525,7 +1527,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     if (pk && !known && scale_hint && bits == 2 && packed && !codes && dtype == CQ_F16 &&
         qp_cand_ok(m, n, (int)r)) {
         int64_t regions = 0, cap = 0;
-        qu_cand_geom(m, n, batch, qp_cand_rows((int)r), &regions, &cap);
+        qu_cand_geom(m, n, batch, qp_cand_rows((int)r), qp_cand_waves((int)r), &regions, &cap);
         char* c = reinterpret_cast<char*>(q.part) + align_up((size_t)batch * tiles * sizeof(double), 256);
         q.ovf = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * 4, 256);
         q.cnt = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * 4, 256);

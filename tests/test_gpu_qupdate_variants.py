@@ -43,7 +43,7 @@ def test_q_update_list_at_capacity(extra):
     dev = torch.device("cuda:0")
     B, n, r = 2, 64, 32
     rows, cap = K.q_update_list_geometry(8 * 48, n, r)
-    m = 8 * rows                          # one panel of 8 wave regions
+    m = 8 * rows                          # 8 wave regions (the first panel)
     g = torch.Generator().manual_seed(4242)
     W = torch.randn(B, m, n, generator=g) * 0.01
     groups = [(i, 8 * c) for i in range(rows) for c in range(n // 8)]   # (row, first column) of region 0
@@ -85,7 +85,7 @@ def test_q_update_single_recompute_matches_two_pass(case, weighted):
     fp32 over runs of 4 by pass 1 and of 8 by the list path, whose nonzero codes' terms are
     corrected in fp64); matrices whose list cannot be
     complete (scale < 0.9 hint, an overflowing list, a non-finite hint) take pass 1 and give
-    the two-pass outputs exactly.  Mixed batches exercise both in one call, and the hint may
+    the two-pass codes and scales exactly and its error to fp64 summation order.  Mixed batches exercise both in one call, and the hint may
     alias the scale output (the engine's use: st.Qs is both)."""
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     tag, B, m, n, r, bits, dt = case
@@ -129,6 +129,8 @@ def test_q_update_single_recompute_matches_two_pass(case, weighted):
             assert torch.equal(sc, s0), name
             for i in range(B):
                 if want_fb[i]:
-                    assert e[i].item() == e0[i].item(), (name, i)
+                    # pass 1 again, on the list path's panel geometry (12 waves of 32 rows at
+                    # K <= 128): the same fp32 terms, summed in fp64 over other panels
+                    assert abs(e[i].item() - e0[i].item()) <= 1e-12 * e0[i].item(), (name, i)
                 else:
                     assert abs(e[i].item() - e0[i].item()) <= 1e-7 * e0[i].item(), (name, i, e[i].item(), e0[i].item())
