@@ -313,6 +313,9 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
             bqb[u] = qb;
         }
     }
+    // seat and next-round seat arrays swap roles every round (one barrier fewer than a copy)
+    int* scur = seat;
+    int* snxt = seat2;
     int sweep = 0;
     for (; sweep < max_sweeps; ++sweep) {
         double off = 0.0, dg = 0.0;
@@ -329,7 +332,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
         for (int rd = 0; rd < P - 1; ++rd) {
             int act = 0;
             for (int k = tid; k < H; k += NTH) {
-                const int se = seat[2 * k], so = seat[2 * k + 1];
+                const int se = scur[2 * k], so = scur[2 * k + 1];
                 const int i = min(se, so), j = max(se, so);
                 double c = 1.0, s = 0.0;
                 if (j < p) {
@@ -348,8 +351,8 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                 }
                 csn[k] = make_double2(c, s); lohi[k] = make_int2(i, j); flp[k] = se > so;
                 // seats of the next round (circle shift with fixed adjacent pairs)
-                seat2[2 * k] = (k == 0) ? se : (k == 1) ? seat[1] : seat[2 * k - 2];
-                seat2[2 * k + 1] = (k == H - 1) ? se : seat[2 * k + 3];
+                snxt[2 * k] = (k == 0) ? se : (k == 1) ? scur[1] : scur[2 * k - 2];
+                snxt[2 * k + 1] = (k == H - 1) ? se : scur[2 * k + 3];
             }
             const bool any = __syncthreads_or(act);
             if (any) {
@@ -487,9 +490,13 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
 #pragma unroll
                 for (int u = 0; u < PPT; ++u) { ev[u][r] = ne[u]; od[u][r] = no[u]; }
             }
+            // every thread is done with this round's pair data and A before the next round's
+            // rotations read A and overwrite them; the next round reads snxt, written before the
+            // round's first barrier, and writes the array read before it
             __syncthreads();
-            for (int s2 = tid; s2 < P; s2 += NTH) seat[s2] = seat2[s2];
-            __syncthreads();
+            int* const t2 = scur;
+            scur = snxt;
+            snxt = t2;
         }
     }
     if (tid == 0 && sweeps_out) sweeps_out[b] = sweep;
@@ -508,7 +515,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
     for (int u = 0; u < PPT; ++u) {
         const int k = k0 + u;
         if (k >= H) continue;
-        const int pe = seat[2 * k], po = seat[2 * k + 1];
+        const int pe = scur[2 * k], po = scur[2 * k + 1];
 #pragma unroll
         for (int r = 0; r < RPT; ++r) {
             const int x = x0 + r;
