@@ -260,12 +260,13 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
     const int P = p + (p & 1);
     const int H = P / 2;
     double2* csn = reinterpret_cast<double2*>(smem_raw);  // H: (cos, sin) of pair k's rotation
-    int2* lohi = reinterpret_cast<int2*>(csn + H);         // H: (smaller, larger) index of pair k
+    int4* lohi = reinterpret_cast<int4*>(csn + H);         // H: pair k's (smaller, larger) index and
+                                                           // their packed-row offsets (pko)
     int* flp = reinterpret_cast<int*>(lohi + H);           // H  (seat 2k holds the larger index)
     int* seat = flp + H;                                // P
     int* seat2 = seat + P;                              // P
     int* rnk = seat2 + P;                               // P
-    double* a = reinterpret_cast<double*>(rnk + P + ((7 * H + 3 * P) & 1));
+    double* a = reinterpret_cast<double*>(rnk + P + ((9 * H + 3 * P) & 1));
     __shared__ double red[16];
     __shared__ int stop;
     const int64_t b = blockIdx.x;
@@ -279,6 +280,10 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
         if (i > j) { const int t = i; i = j; j = t; }
         return i * p - ((i * (i - 1)) >> 1) + (j - i);
     };
+    // packed offset of row i's diagonal minus i: element (i, j), i <= j, at pko(i) + j
+    auto pko = [p](int i) -> int { return i * p - ((i * (i - 1)) >> 1) - i; };
+    // element (x, y) from the two indices and their row offsets
+    auto pkx = [](int x, int ox, int y, int oy) -> int { return x <= y ? ox + y : oy + x; };
     for (int i = wid; i < p; i += (NTH / 64))
         for (int c = lane; c < p; c += 64)
             if (c >= i) a[pk(i, c)] = 0.5 * (Ag[i * p + c] + Ag[c * p + i]);
@@ -349,7 +354,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                         act = 1;
                     }
                 }
-                csn[k] = make_double2(c, s); lohi[k] = make_int2(i, j); flp[k] = se > so;
+                csn[k] = make_double2(c, s); lohi[k] = make_int4(i, j, pko(i), pko(j)); flp[k] = se > so;
                 // seats of the next round (circle shift with fixed adjacent pairs)
                 snxt[2 * k] = (k == 0) ? se : (k == 1) ? scur[1] : scur[2 * k - 2];
                 snxt[2 * k + 1] = (k == H - 1) ? se : scur[2 * k + 3];
@@ -359,7 +364,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                 // ---- A <- J^T A J on pair blocks (qa <= qb) in LDS
                 if constexpr (JBR == 1) {
                     // one pair block at a time, few live values (V stays in registers); a
-                    // pair's rotation and indices are two 16- and 8-byte reads
+                    // pair's rotation and its indices with their row offsets are two 16-byte reads
 #pragma unroll
                     for (int u = 0; u < JMB; ++u) {
                         const int qa = bqa[u], qb = bqb[u];
@@ -368,12 +373,13 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                         const double sa = rca.y, sb = rcb.y;
                         if (sa == 0.0 && sb == 0.0) continue;
                         const double ca = rca.x, cb = rcb.x;
-                        const int2 pa = lohi[qa], pb = lohi[qb];
+                        const int4 pa = lohi[qa], pb = lohi[qb];
                         const int ia = pa.x, ja = pa.y, ib = pb.x, jb = pb.y;
+                        const int oia = pa.z, oja = pa.w, oib = pb.z, ojb = pb.w;
                         const bool va = ja < p, vb = jb < p;
                         if (qa == qb) {
                             if (!va) continue;
-                            const int o0 = pk(ia, ia), o1 = pk(ia, ja), o3 = pk(ja, ja);
+                            const int o0 = pkx(ia, oia, ia, oia), o1 = pkx(ia, oia, ja, oja), o3 = pkx(ja, oja, ja, oja);
                             const double x0 = a[o0], x1 = a[o1], x3 = a[o3];
                             const double y00 = cb * x0 - sb * x1, y01 = sb * x0 + cb * x1;
                             const double y10 = cb * x1 - sb * x3, y11 = sb * x1 + cb * x3;
@@ -381,10 +387,10 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                             a[o3] = sa * y01 + ca * y11;
                             a[o1] = 0.0;
                         } else {
-                            const int o0 = pk(ia, ib);
-                            const int o1 = vb ? pk(ia, jb) : -1;
-                            const int o2 = va ? pk(ja, ib) : -1;
-                            const int o3 = (va && vb) ? pk(ja, jb) : -1;
+                            const int o0 = pkx(ia, oia, ib, oib);
+                            const int o1 = vb ? pkx(ia, oia, jb, ojb) : -1;
+                            const int o2 = va ? pkx(ja, oja, ib, oib) : -1;
+                            const int o3 = (va && vb) ? pkx(ja, oja, jb, ojb) : -1;
                             const double x0 = a[o0];
                             const double x1 = o1 >= 0 ? a[o1] : 0.0;
                             const double x2 = o2 >= 0 ? a[o2] : 0.0;
@@ -534,7 +540,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
 
 static size_t jacobi_reg_bytes(int p) {
     const int P = p + (p & 1), H = P / 2;
-    return (size_t)2 * H * sizeof(double) + (size_t)(3 * H + 3 * P + 1) * sizeof(int) + 8 +
+    return (size_t)2 * H * sizeof(double) + (size_t)(5 * H + 3 * P + 1) * sizeof(int) + 8 +
            (size_t)p * (p + 1) / 2 * sizeof(double) + 16;
 }
 
