@@ -50,7 +50,7 @@ __device__ __forceinline__ int gidx(int a, int c, int u, int p) {
 
 __device__ __forceinline__ void rot_params(double aii, double ajj, double aij, double thr, double& c, double& s) {
     c = 1.0; s = 0.0;
-    if (fabs(aij) > 1e-300 && fabs(aij) > thr * sqrt(fabs(aii * ajj))) {
+    if (fabs(aij) > 1e-300 && aij * aij > (thr * thr) * fabs(aii * ajj)) {
         const double th = (ajj - aii) / (2.0 * aij);
         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
         c = 1.0 / sqrt(1.0 + t * t);

@@ -299,6 +299,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
         }
     __syncthreads();
     const double skip_rel = fmax(1e-17, 0.01 * tol);
+    const double skip_rel2 = skip_rel * skip_rel;   // the threshold test squared: no sqrt per pair
     // this thread's pair blocks (qa <= qb) of the JBR == 1 update, fixed for the whole solve
     // (only the indices the pairs hold change between rounds): H (H + 1) / 2 <= 4656 blocks
     // for p <= 192, at most JMB per thread
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(NTH) void jacobi_reg_kernel(const double* __restric
                     // threshold Jacobi: elements below tol/100 of their diagonal scale are left
                     // alone (their total stays under the off-norm tolerance), so the last sweeps
                     // skip most pair-block updates
-                    if (fabs(aij) > 1e-300 && fabs(aij) > skip_rel * sqrt(fabs(aii * ajj))) {
+                    if (fabs(aij) > 1e-300 && aij * aij > skip_rel2 * fabs(aii * ajj)) {
                         const double th = (ajj - aii) / (2.0 * aij);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
                         c = 1.0 / sqrt(1.0 + t * t);
