@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
     }
 }
 
-constexpr int SG_FILL_CAP = 512;
+constexpr int SG_FILL_CAP = 256;   // rows with more nonzeros take the plain order (LDS: 6 workgroups per CU)
 constexpr int SG_FILL_RW = 4;   // sorted positions (rows) per wave
 
 // Entry order.  The SpMM reads E's l-th 16-byte slab entry (LDS bank group l mod 16) for the 64

@@ -96,7 +96,7 @@ def test_sparse_gram_matches_fp64(B, m, n, weighted):
 def _expected_ell_rows(codes, perm, row_nnz):
     """The sliced-ELL entry order (cq_sgram.hip, sgram_fill_kernel) restated on the host: per
     sorted position p (row j = perm[p]) the nonzero codes (l << 2 | code + 1), grouped by
-    residue l mod 16 in increasing l; rows of at most 512 entries take residue (p + t) mod 16 at
+    residue l mod 16 in increasing l; rows of at most 256 entries take residue (p + t) mod 16 at
     step t while it has entries left, else the residue with the most left (ties: the smaller);
     longer rows the residues in the order p, p + 1, ... (mod 16)."""
     out = []
@@ -106,7 +106,7 @@ def _expected_ell_rows(codes, perm, row_nnz):
         ent = {u: [int((l << 2) | (row[l] + 1)) for l in ls if l % 16 == u] for u in range(16)}
         q = p & 15
         seq = []
-        if row_nnz[j] > 512:
+        if row_nnz[j] > 256:   # SG_FILL_CAP
             for i in range(16):
                 seq += ent[(q + i) & 15]
         else:
@@ -127,12 +127,12 @@ def _expected_ell_rows(codes, perm, row_nnz):
 def test_sparse_gram_ell_order(k, L, dens):
     """The ELL fill (sgram_count + sgram_fill) against the host restatement of its entry order:
     counts, row sort, per-row entry sequence (bank-group rotation, greedy fallback, rows past
-    512 entries in residue-rotated order) and padding, entry for entry."""
+    256 entries in residue-rotated order) and padding, entry for entry."""
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     rng = np.random.default_rng(k + L)
     B = 2
     codes = np.where(rng.random((B, k, L)) < dens, rng.choice([-1, 1], size=(B, k, L)), 0).astype(np.int8)
-    codes[0, 5, : L // 2] = 1          # a row past 512 entries when L >= 1026
+    codes[0, 5, : L // 2] = 1          # a row past 256 entries
     codes[1, 7, :] = 0                 # an empty row
     off = (codes + 1).astype(np.uint8).reshape(B, k, L // 4, 4)
     packed = (off[..., 0] << 6) | (off[..., 1] << 4) | (off[..., 2] << 2) | off[..., 3]
