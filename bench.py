@@ -541,7 +541,7 @@ def main():
                            else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")}
     if gprobe:
         # the LR update's MFMA-bound kernel (north_star: "MFMA utilisation on the LR update"):
-        # the split-fp16 Gram (gemm_x3v_kernel<false>, sym_out), 3 fp16 MFMA products over the
+        # the split-fp16 Gram (gemm_x3v_kernel<0>, sym_out), 3 fp16 MFMA products over the
         # upper half of the symmetric k x k output (fp32-equivalent flops k^2 n).  With sparse
         # 2-bit codes (sgram.py) it runs once per run on W's halves (A = W W^T, kind gram_A) and
         # every LR step forms G = A - s (P + P^T) from the codes (kind gram_sparse, HBM-bound)
@@ -557,8 +557,8 @@ def main():
                 "bytes_per_launch": gp["bytes_per_launch"],
                 "operand": "Y = (W - Q) diag(ycol) per LR step" if kind == "gram" else
                            "W diag(ycol), once per decomposition (A of the sparse-code Gram)",
-                "kernel": ("gemm_x3v_kernel<false> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"
-                           if kind == "gram" else "gemm_x3v_kernel<true|false> (Gram of W: one fp16 product when "
+                "kernel": ("gemm_x3v_kernel<0> (split-fp16 Gram, sym_out: writes G's K-blocked halves)"
+                           if kind == "gram" else "gemm_x3v_kernel<1|0> (Gram of W: one fp16 product when "
                            "H = I, W being exact in fp16; split-fp16 otherwise)")}
         if "gram_sparse" in gprobe:
             gp = gprobe["gram_sparse"]

@@ -68,6 +68,7 @@ class X3Args(ctypes.Structure):
         ("single", c_int),
         ("ksplit", c_int),
         ("split_ws", c_vp),
+        ("b_exact", c_int),
     ]
 
 
@@ -167,7 +168,7 @@ def load(path: str = LIB_PATH):
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.cq_abi_version() != 1:
+    if lib.cq_abi_version() != 2:
         raise RuntimeError("libcaldera_hip.so ABI version mismatch")
     _lib = lib
     return lib
@@ -665,14 +666,16 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
-            single=False, ksplit=None):
+            single=False, ksplit=None, b_exact=False):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
     sym_bound (B,) fp64: symmetric Gram mode (tri): the K-blocked split of C is written from
     its upper triangle with scale s[b] from the bound (scale_out, inv_out = 1/(s out_scale));
     C may then be None.  lda / M (a_blocked only): A holds lda >= M rows of which the first M
-    are used (C has M rows)."""
+    are used (C has M rows).  b_exact: B is exactly fp16 (Bl = 0, e.g. W's halves written
+    under a split scale >= 1); Bl is not read and may be None."""
+    assert Bl is not None or b_exact or single
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, MA, Kd = Ah.shape
     M = MA if M is None else M
@@ -686,7 +689,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g = X3Args()
     g.M, g.N, g.K, g.batch = M, N, Kd, Bt
     g.Ah, g.Al, g.lda, g.stride_a = Ah.data_ptr(), Al.data_ptr(), (MA if a_blocked else Kd), MA * Kd
-    g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), Bl.data_ptr(), (N if b_blocked else Kd), N * Kd
+    g.Bh, g.Bl, g.ldb, g.stride_b = Bh.data_ptr(), (Bl.data_ptr() if Bl is not None else None), (
+        N if b_blocked else Kd), N * Kd
     g.inv_scale = inv_scale.data_ptr()
     g.C, g.ldc, g.stride_c = (C.data_ptr() if C is not None else None), N, M * N
     if P is not None:
@@ -706,6 +710,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.a_blocked = int(a_blocked)
     g.o_blocked = int(bool(o_blocked))
     g.single = int(bool(single))
+    g.b_exact = int(bool(b_exact))
     # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
     # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups
     tiles = -(-N // 384) * -(-M // 192) * Bt

@@ -18,6 +18,7 @@
 // halves of the next iterate, or the Gram's mirrored K-blocked halves).
 #include <type_traits>
 #include <numeric>
+#include <cstdlib>
 
 #include "cq_x3.h"
 
@@ -60,6 +61,14 @@ constexpr size_t XW_LDS_BYTES = (size_t)2 * XW_STAGE * sizeof(_Float16);  // 144
 constexpr int XW_PER_WAVE = (2 * XW_BM / 16 + 2 * XW_BN / 16) / (XW_THREADS / 64);  // 6
 static_assert(XW_PER_WAVE == 6, "load split");
 
+// One 16-B-per-lane LDS-DMA load; nt (wave-uniform): non-temporal, for bytes one tile reads once
+__device__ __forceinline__ void xw_load(const _Float16* src, _Float16* dst, bool nt) {
+    if (nt)
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 2);
+    else
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
 // Load plan: the wave-uniform part of each of this wave's 6 LDS-DMA loads (which image,
 // which 16-row group) is scalar; the per-lane part is a 32-bit element offset computed once
 // per tile, so a K step costs one 64-bit add per load (keeps the loop free of spills).
@@ -92,8 +101,7 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _F
         const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
-        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
-                                         16, 0, 0);
+        xw_load(base + off[u], dst, !isA && a.b_nt);
     }
 }
 
@@ -263,8 +271,7 @@ __device__ __forceinline__ void xv1_issue(const X3K& a, int64_t b, int64_t k0, _
         const _Float16* base = isA ? a.Ah + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? 0 : XW_APART) + (16 * sub) * XW_BK;
-        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst,
-                                         16, 0, 0);
+        xw_load(base + off[u], dst, !isA && a.b_nt);
     }
 }
 
@@ -327,6 +334,114 @@ __device__ __forceinline__ void xv1_mainloop(const X3K& a, int64_t b, int64_t m0
     }
 }
 
+// Exact-B K loop (two products, al x bh + ah x bh): B is an fp16 matrix itself (W's halves
+// under a split scale >= 1: lo = 0), so Bl is neither loaded nor multiplied.  A stage is
+// 48 KB (A hi | A lo | B hi) and three fit the 144 KB: loads of steps t+1, t+2 are in flight
+// while step t computes (4 LDS-DMA wave-instructions per wave and step, counted vmcnt across
+// the barrier as in xv1_mainloop).  The same MFMAs in the same order as xv_mainloop minus the
+// ah x bl term, whose product is exactly zero: the same bits.
+constexpr int XV2_NS = 3;
+constexpr int XV2_STAGE = 2 * XW_APART + XW_BPART;  // halves
+constexpr int XW2_PER_WAVE = 4;
+static_assert((size_t)XV2_NS * XV2_STAGE * sizeof(_Float16) <= XW_LDS_BYTES, "exact-B ring fits the LDS");
+static_assert(XW2_PER_WAVE * (XW_THREADS / 64) == 2 * XW_BM / 16 + XW_BN / 16, "exact-B load split");
+
+__device__ __forceinline__ void xw2_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
+                                         uint32_t (&off)[XW2_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW2_PER_WAVE; ++u) {
+        const int I = wid * XW2_PER_WAVE + u;  // 0..47: Ah 0-11, Al 12-23, Bh 24-47
+        const bool isA = I < 24;
+        const int sub = isA ? I % 12 : I - 24;
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ xg_swz(row);
+        const int64_t lim = isA ? a.M : a.N;
+        int64_t gr = (isA ? m0 : n0) + row;
+        gr = gr < lim ? gr : lim - 1;
+        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * 32 + c * 8 : gr * a.lda + c * 8)
+                                : (a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8));
+    }
+}
+
+__device__ __forceinline__ void xv2_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                          const uint32_t (&off)[XW2_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XW2_PER_WAVE; ++u) {
+        const int I = wid * XW2_PER_WAVE + u;
+        const bool isA = I < 24;
+        const int part = I >= 12 && isA;
+        const int sub = isA ? I % 12 : I - 24;
+        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
+                                   : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
+        _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART) + (16 * sub) * XW_BK;
+        xw_load(base + off[u], dst, !isA && a.b_nt);
+    }
+}
+
+__device__ __forceinline__ void xv2_wait(int64_t after) {
+    // this wave's loads of the stage issued after step t (at most XV2_NS - 2 = 1 at the wait,
+    // step t + 2 being issued after it) may stay in flight
+    if (after >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void xv2_mainloop(const X3K& a, int64_t b, int64_t m0, int64_t n0, int64_t nt,
+                                             _Float16* smem, int wid, int lane, int wm, int wn,
+                                             f32x4v (&acc)[6][4], int64_t kb = 0) {
+    static_assert(XV2_NS == 3 && XW2_PER_WAVE == 4, "xv2_wait's counts");
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    wid = __builtin_amdgcn_readfirstlane(wid);
+    uint32_t off[XW2_PER_WAVE];
+    if (nt > 0) {
+        xw2_plan(a, m0, n0, wid, lane, off);
+        for (int64_t s = 0; s < XV2_NS - 1 && s < nt; ++s)
+            xv2_issue(a, b, (kb + s) * XW_BK, smem + s * XV2_STAGE, wid, off);
+    }
+    const int64_t rs0 = m0 + 96 * wm, cs0 = n0 + 64 * wn;
+    uint32_t live = (rs0 < a.M && cs0 < a.N && (!a.tri || cs0 + 63 >= rs0)) ? 1u : 0u;
+    live = __builtin_amdgcn_readfirstlane(live);
+    int slot = 0, nslot = XV2_NS - 1;  // slot of step t, slot the stage of step t + 2 goes to
+    if (!live) {  // dead 96 x 64 block: its share of the loads and barriers only
+        for (int64_t t = 0; t < nt; ++t) {
+            xv2_wait(nt - 1 - t);
+            __builtin_amdgcn_s_barrier();
+            if (t + XV2_NS - 1 < nt) xv2_issue(a, b, (kb + t + XV2_NS - 1) * XW_BK, smem + nslot * XV2_STAGE, wid, off);
+            nslot = nslot == XV2_NS - 1 ? 0 : nslot + 1;
+        }
+        return;
+    }
+    for (int64_t t = 0; t < nt; ++t) {
+        xv2_wait(nt - 1 - t);
+        __builtin_amdgcn_s_barrier();  // stage t landed everywhere; the slot of t - 1 fully read
+        if (t + XV2_NS - 1 < nt) xv2_issue(a, b, (kb + t + XV2_NS - 1) * XW_BK, smem + nslot * XV2_STAGE, wid, off);
+        {
+            const _Float16* sA = smem + slot * XV2_STAGE;
+            const _Float16* sB = sA + 2 * XW_APART;
+            f16x8 bh[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bh[j] = xg_frag(sB, 64 * wn + 16 * j + l16, lq);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int row = 96 * wm + 16 * i + l16;
+                const f16x8 ah = xg_frag(sA, row, lq);
+                const f16x8 al = xg_frag(sA + XW_APART, row, lq);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        slot = slot == XV2_NS - 1 ? 0 : slot + 1;
+        nslot = nslot == XV2_NS - 1 ? 0 : nslot + 1;
+    }
+}
+
 // Gram tile order.  Only the tiles on or above the diagonal are launched: 384 x 384 blocks
 // (I, J >= I) of tiles tm = 2I, 2I + 1 (192 rows) by tn = J.  The blocks are enumerated per
 // matrix in 4 x 4 super-blocks (row-major over super-blocks, then over their blocks), and
@@ -372,7 +487,8 @@ __device__ void gram_tile(const X3K& a, int64_t orig, int64_t& b, int64_t& tm, i
     tm = tn = 0;  // unreachable for lin < total
 }
 
-template <bool X1>
+// XM: 0 = three split products, 1 = one hi x hi product, 2 = exact B (two products, Bl unread)
+template <int XM>
 __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     extern __shared__ __attribute__((aligned(16))) char xv_smem_raw[];
     _Float16* smem = reinterpret_cast<_Float16*>(xv_smem_raw);
@@ -407,8 +523,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
         kb = ks * nk / a.ksplit;
         kn = (ks + 1) * nk / a.ksplit - kb;
     }
-    if constexpr (X1) {
+    if constexpr (XM == 1) {
         xv1_mainloop(a, b, m0, n0, live ? kn : 0, smem, wid, lane, wm, wn, acc, kb);
+    } else if constexpr (XM == 2) {
+        xv2_mainloop(a, b, m0, n0, live ? kn : 0, smem, wid, lane, wm, wn, acc, kb);
     } else {
         xv_mainloop<false>(a, b, m0, n0, live ? kn : 0, smem, wid, lane, wm, wn, acc, kb);
     }
@@ -1018,7 +1136,10 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
         const float bnd = (wmax[b] + qs) * ycmax;
         if (bnd > 0.f && isfinite(bnd)) frexpf(bnd, &e2);
     }
-    const float sc = ldexpf(1.f, 14 - e2);
+    // fp16 W alone (no codes, no column weights): a scale >= 1 keeps W * sc exact in fp16
+    // (lo = 0), so the lo halves may be skipped and their products dropped (gemm_x3 b_exact)
+    const bool exact = DT == CQ_F16 && !qc && !ycol;
+    const float sc = exact ? fmaxf(ldexpf(1.f, 14 - e2), 1.f) : ldexpf(1.f, 14 - e2);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && scale_out) scale_out[b] = sc;
     const int t = threadIdx.x;
     const int r = t >> 3, c8 = (t & 7) * 8;          // row in tile, first of 8 columns
@@ -1099,7 +1220,7 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
             }
             const int64_t o = b * MN + (j >> 5) * m * 32 + i * 32 + (j & 31);
             *reinterpret_cast<uint4*>(hi + o) = *reinterpret_cast<const uint4*>(h8);
-            *reinterpret_cast<uint4*>(lo + o) = *reinterpret_cast<const uint4*>(l8);
+            if (lo) *reinterpret_cast<uint4*>(lo + o) = *reinterpret_cast<const uint4*>(l8);
         }
         if (thi) {  // blocked over rows (Y^T as a row-major n x m operand): (i / 32) * n * 32 + j * 32 + i % 32
 #pragma unroll
@@ -1115,7 +1236,7 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
             }
             const int64_t o = b * MN + (i0 >> 5) * n * 32 + (j0 + jc) * 32 + r8;
             *reinterpret_cast<uint4*>(thi + o) = *reinterpret_cast<const uint4*>(h8);
-            *reinterpret_cast<uint4*>(tlo + o) = *reinterpret_cast<const uint4*>(l8);
+            if (tlo) *reinterpret_cast<uint4*>(tlo + o) = *reinterpret_cast<const uint4*>(l8);
             __syncthreads();
         }
     }
@@ -1618,7 +1739,9 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     CQ_REQUIRE(m % 32 == 0 && n % 64 == 0, "cq_residual_split: m % 32 and n % 64 must be 0");
     CQ_REQUIRE(!packed || qscale, "cq_residual_split: scale required with codes");
     CQ_REQUIRE(!packed || bits == 2 || bits == 4 || bits == 8 || bits == 16 || bits == 32, "Bit-width not supported!");
-    CQ_REQUIRE(!hi == !lo && !thi == !tlo, "cq_residual_split: halves go in pairs");
+    const bool exact = dtype == CQ_F16 && !packed && !ycol;  // lo = 0: the lo halves are optional
+    CQ_REQUIRE((!lo || hi) && (!tlo || thi) && (exact || (!hi == !lo && !thi == !tlo)),
+               "cq_residual_split: halves go in pairs (lo optional only for fp16 W without codes or ycol)");
     CQ_REQUIRE((!hi && !thi) || scale_out, "cq_residual_split: halves need scale_out");
     CQ_REQUIRE(!sq_out || (ws && ws_bytes >= cq_residual_split_workspace(m, n, batch)), "cq_residual_split: workspace too small");
     const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(m / 32, 16));
@@ -1643,7 +1766,8 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
 
 int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(g, "cq_gemm_x3: null args");
-    CQ_REQUIRE(g->Ah && g->Al && g->Bh && g->Bl && (g->C || g->sym_out) && g->inv_scale, "cq_gemm_x3: null operand");
+    CQ_REQUIRE(g->Ah && g->Al && g->Bh && (g->Bl || g->single || g->b_exact) && (g->C || g->sym_out) && g->inv_scale,
+               "cq_gemm_x3: null operand");
     CQ_REQUIRE(!g->sym_out || (g->tri && g->out_h && g->out_l && g->out_bound && g->scale_out && g->inv_out &&
                                g->out_scale > 0.f && g->N % 32 == 0),
                "cq_gemm_x3: sym_out needs tri, out_h/out_l, out_bound, scale_out, inv_out, N % 32 == 0");
@@ -1708,8 +1832,15 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         total *= a.ksplit;
     }
     CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-    if (a.single) gemm_x3v_kernel<true><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
-    else gemm_x3v_kernel<false><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    {   // one tile row: every B panel is read by one workgroup, once -- non-temporal loads keep
+        // it from evicting the A slices the row's tiles re-read (filter G X^T, R = U^T W: 1-3 %
+        // less time per launch in A/B runs, profiles/r04ab_*; CQ_X3_NT=0 turns it off)
+        static const char* e = getenv("CQ_X3_NT");
+        a.b_nt = (!(e && e[0] == '0') && !a.tri && !a.sym_out && a.tiles_m == 1) ? 1 : 0;
+    }
+    if (a.single) gemm_x3v_kernel<1><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    else if (g->b_exact) gemm_x3v_kernel<2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
+    else gemm_x3v_kernel<0><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     if (a.ksplit > 1)
         x3_splitk_epi_kernel<<<dim3((unsigned)ceil_div(g->M * (g->N / 4), 256), (unsigned)g->batch), 256, 0,
                                as_stream(stream)>>>(a);

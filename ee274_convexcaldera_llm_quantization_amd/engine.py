@@ -487,7 +487,7 @@ class CalderaEngine:
                 self._sg_w = None
                 sv._alloc(dev)
                 self._wth = scratch.get("lr.wth", (B, m, n), torch.float16, dev)
-                self._wtl = scratch.get("lr.wtl", (B, m, n), torch.float16, dev)
+                self._wtl = None  # W's halves are exact (lo = 0, sgram.gram_A): b_exact products
                 self._ysw = torch.empty(B, dtype=torch.float32, device=dev)
                 self._wsq = torch.empty(B, dtype=torch.float64, device=dev)
                 gev = GRAM_PROBE.start("gram_A", 1.0 * n * n * m * B, 2.0 * m * n * B + 4.0 * n * n * B)
@@ -511,7 +511,8 @@ class CalderaEngine:
                 sv._alloc(dev)
                 if lite:
                     self._wth = scratch.get("lr.wth", (B, n, m), torch.float16, dev)
-                    self._wtl = scratch.get("lr.wtl", (B, n, m), torch.float16, dev)
+                    # unweighted: (W)^T's halves are exact (lo = 0, sgram.gram_A), not written
+                    self._wtl = scratch.get("lr.wtl", (B, n, m), torch.float16, dev) if weighted else None
                     self._ysw = torch.empty(B, dtype=torch.float32, device=dev)
                     self._wsq = torch.empty(B, dtype=torch.float64, device=dev)
                 # fp16 MFMA work: one product over the upper half (H = I: W's halves are W and 0),
@@ -683,7 +684,7 @@ class CalderaEngine:
             K.codes_matmul(st.Qc, m, n, X, r, cv, trans=True)
             Lt = torch.empty((B, r, m), dtype=torch.float32, device=L.device)
             K.gemm_x3(xh, xl, self._wth, self._wtl, 1.0 / (self._ysw * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
-                      lda=p, M=r, D=cv, gamma_v=-st.Qs)
+                      lda=p, M=r, D=cv, gamma_v=-st.Qs, b_exact=self._wtl is None)
             K.transpose_split(Lt, out=L)
             return
         if self._yrh is None or isinstance(sv, RandSVD) or sv.direct:
@@ -714,7 +715,7 @@ class CalderaEngine:
         K.codes_matmul(ct, n, m, X, r, utc, roww=ycol, trans=True)
         inv = 1.0 / (self._ysw * X3_SCALE)
         K.gemm_x3(xh, xl, self._wth, self._wtl, inv, R, a_blocked=True, b_blocked=True, lda=p, M=r, D=utc,
-                  gamma_v=-st.Qs)
+                  gamma_v=-st.Qs, b_exact=self._wtl is None)
 
     def _ut_y(self, sv, R):
         """R = U^T Y (U = the solver's Ritz block, first r columns; m <= n) as a split-fp16

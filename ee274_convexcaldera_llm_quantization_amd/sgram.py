@@ -34,13 +34,17 @@ def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch
     (cq_gemm_x3 Gram of W's K-blocked halves, written into yh/yl (B, m, n); H = I makes them
     exact, lo = 0).  Gh/Gl receive a split of A that the caller overwrites later.  The same pass
     can also write the halves of (W diag(ycol))^T (wth/wtl (B, n, m), K-blocked over m: the B
-    operand of R = U^T Y) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,)."""
+    operand of R = U^T Y) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,).
+    Without ycol the halves are exact (fp16 W under a split scale >= 1: lo = 0): the lo halves
+    are not written (wtl may be None; its products run as gemm_x3 b_exact)."""
     B, m, n = Ws.shape
     dev = Ws.device
     if ys is None:
         ys = torch.empty(B, dtype=torch.float32, device=dev)
-    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=yl, thi=wth, tlo=wtl, scale=ys,
-                     sq=wsq)
+    exact = ycol is None and Ws.dtype == torch.float16
+    assert exact or wth is None or wtl is not None
+    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=None if exact else yl, thi=wth,
+                     tlo=None if exact else wtl, scale=ys, sq=wsq)
     bound = torch.full((B,), 2.0 ** 60, dtype=torch.float64, device=dev)  # any bound >= max|A|: halves unused
     so = torch.empty(B, dtype=torch.float32, device=dev)
     io = torch.empty(B, dtype=torch.float32, device=dev)

@@ -426,7 +426,7 @@ class RankRSolver:
         # bytes a recurrence step moves: G halves (4 B/elem) + X^T halves + prev, cur in,
         # new out (fp32) + new halves out
         nb = float(self.B) * (4.0 * self.k * self.k + 20.0 * self.p * self.k)
-        kn = "gemm_x3v_kernel<false> (split-fp16 G X, Chebyshev filter)"
+        kn = "gemm_x3v_kernel<0> (split-fp16 G X, Chebyshev filter)"
         # the probe (bench.py's roofline) times the split-fp16 steps only: a single-product
         # step moves 2k^2 + 18pk bytes per matrix, not the 4k^2 + 20pk counted here
         probe = EVENT_PROBE.start if not single else (lambda *a: None)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CQ_ABI_VERSION 1
+#define CQ_ABI_VERSION 2
 
 #define CQ_OK 0
 #define CQ_EINVAL (-1)   /* bad argument (shape, bits, null pointer) */
@@ -319,6 +319,9 @@ typedef struct cq_x3_args {
                                       then fill the chip: one caldera() call), their fp32 partials
                                       summed in chunk order by an epilogue kernel */
     float* split_ws;               /* ksplit x batch x M x N fp32 partials (ksplit > 1) */
+    int b_exact;                   /* B is exactly fp16 (Bl = 0, e.g. W's halves under a split
+                                      scale >= 1): two products al x bh + ah x bh, Bl not read
+                                      (may be NULL); the same bits as the three products */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
@@ -332,7 +335,9 @@ int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out
  * K-blocked split halves of Y over its columns (hi/lo, layout of cq_split_f16 blocked) and
  * over its rows (thi/tlo: Y^T as an n x m operand, blocked), and sq_out[b] = ||Y||_F^2
  * (fp64).  The halves' scale (scale_out[b]) is the power of two for the bound
- * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|.  m % 32 == 0, n % 64 == 0.
+ * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|, and at least 1 for fp16 W without codes or
+ * ycol: Y's halves are then exact (lo = 0) and lo / tlo may be NULL (gemm_x3 b_exact reads
+ * only the hi halves).  m % 32 == 0, n % 64 == 0.
  * bits == 32: `packed` is a dense fp32 Q and qscale[b] a bound on max|Q[b]|. */
 size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch);
 int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,

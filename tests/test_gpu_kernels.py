@@ -490,6 +490,58 @@ def test_gemm_x3_single_product_matches_fp64(K, M, N, Kd, blocked):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("Bt,M,N,Kd,lda", [(2, 128, 4096, 4096, 192), (3, 100, 1000, 32, 104),
+                                             (2, 192, 400, 64, 192), (2, 250, 776, 96, 256),
+                                             (2, 64, 384, 160, 96)])
+def test_gemm_x3_exact_b_matches_three_products(K, Bt, M, N, Kd, lda):
+    """b_exact (B exactly fp16, Bl = 0 not read, 3-stage ring of A hi | A lo | B hi): the same
+    bits as the three-product kernel given Bl = 0, with the gamma epilogue of R = U^T W - s U^T c,
+    A rows lda > M (the block's first r columns), short K (ring prologue deeper than the loop)
+    and ragged tiles."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
+    A = torch.randn(Bt, lda, Kd, device=DEV, generator=g)
+    Wm = (torch.randn(Bt, N, Kd, device=DEV, generator=g) * 0.05).half().float()
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 10, blocked=True)
+    Bh, Bl = K.split_f16(Wm.contiguous(), 2.0 ** 14, blocked=True)
+    assert int(Bl.view(torch.int16).abs().max()) == 0
+    inv = torch.full((Bt,), 2.0 ** -24, device=DEV)
+    D = torch.randn(Bt, M, N, device=DEV, generator=g)
+    gam = torch.randn(Bt, device=DEV, generator=g)
+    C3 = torch.full((Bt, M, N), float("nan"), device=DEV)
+    C2 = torch.full_like(C3, float("nan"))
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C3, a_blocked=True, b_blocked=True, lda=lda, M=M, D=D, gamma_v=gam, ksplit=1)
+    K.gemm_x3(Ah, Al, Bh, None, inv, C2, a_blocked=True, b_blocked=True, lda=lda, M=M, D=D, gamma_v=gam, ksplit=1,
+              b_exact=True)
+    assert torch.equal(C2, C3)
+    # split-K (the automatic choice for a batch with few tiles) sums the same partials
+    C2k = torch.full_like(C3, float("nan"))
+    K.gemm_x3(Ah, Al, Bh, None, inv, C2k, a_blocked=True, b_blocked=True, lda=lda, M=M, D=D, gamma_v=gam,
+              b_exact=True)
+    C3k = torch.full_like(C3, float("nan"))
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C3k, a_blocked=True, b_blocked=True, lda=lda, M=M, D=D, gamma_v=gam)
+    assert torch.equal(C2k, C3k)
+
+
+def test_residual_split_exact_w_skips_lo(K):
+    """fp16 W without codes or column weights: scale >= 1 (also for max|W| >= 2^14), hi = W * s
+    exactly, lo / tlo optional (zero when written)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B, m, n = 2, 96, 320
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * torch.tensor([0.02, 1e4], device=DEV).view(B, 1, 1)).half()
+    wmax = K.absmax(W)
+    hi, lo, thi, tlo = (torch.empty(B, m, n, dtype=torch.float16, device=DEV) for _ in range(4))
+    sc = torch.empty(B, device=DEV)
+    K.residual_split(W, None, None, 2, wmax, hi=hi, lo=lo, thi=thi, tlo=tlo, scale=sc)
+    assert float(sc[1]) == 1.0 and float(sc[0]) > 1.0
+    assert int(lo.view(torch.int16).abs().max()) == 0 and int(tlo.view(torch.int16).abs().max()) == 0
+    h_ref, _ = K.split_f16(W.float().contiguous(), sc, blocked=True)
+    assert torch.equal(hi, h_ref)
+    hi2, thi2 = torch.empty_like(hi), torch.empty_like(hi)
+    sc2 = torch.empty_like(sc)
+    K.residual_split(W, None, None, 2, wmax, hi=hi2, thi=thi2, scale=sc2)
+    assert torch.equal(hi2, hi) and torch.equal(thi2, thi) and torch.equal(sc2, sc)
+
+
 def test_gemm_x3_tri_upper_exact(K):
     """tri mode: the upper triangle of Y Y^T equals the full product's bit for bit."""
     g = torch.Generator(device=DEV).manual_seed(21)

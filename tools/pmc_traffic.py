@@ -13,9 +13,9 @@ grid = ((k + XW_BN - 1) // XW_BN) * ((p + XW_BM - 1) // XW_BM) * B * XW_THREADS
 
 def vals(d, name, single):
     """Dispatches of the filter grid; single: the one-product (hi x hi) instantiation
-    gemm_x3v_kernel<true> of the cheap outer iterations, else the split-fp16 <false> one."""
+    gemm_x3v_kernel<1> of the cheap outer iterations, else the split-fp16 <0> one."""
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
-    tag = "gemm_x3v_kernel<true>" if single else "gemm_x3v_kernel<false>"
+    tag = "gemm_x3v_kernel<1>" if single else "gemm_x3v_kernel<0>"
     return [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
             if tag in r["Kernel_Name"] and int(r["Grid_Size"]) == grid and r["Counter_Name"] == name]
 
@@ -28,11 +28,11 @@ single = None
 if fe1 and wr1:
     f1, w1 = statistics.mean(fe1), statistics.mean(wr1)
     # hi halves only: G hi 2k^2 + X^T hi 2pk, P and D 8pk in, C 4pk + halves 4pk out
-    single = {"kernel": "gemm_x3v_kernel<true> (one fp16 product, cheap outer iterations)", "dispatches": len(fe1),
+    single = {"kernel": "gemm_x3v_kernel<1> (one fp16 product, cheap outer iterations)", "dispatches": len(fe1),
               "FETCH_SIZE_KB_avg": f1, "WRITE_SIZE_KB_avg": w1, "hbm_bytes_per_launch": (2 * f1 + w1) * 1024,
               "algorithmic_bytes_per_launch": B * (2.0 * k * k + 18.0 * p * k)}
 out = {
-    "kernel": "gemm_x3v_kernel<false> (split-fp16 G X, Chebyshev filter)",
+    "kernel": "gemm_x3v_kernel<0> (split-fp16 G X, Chebyshev filter)",
     "config": {"batch": B, "p": p, "k": k},
     "dispatches": len(fe),
     "FETCH_SIZE_KB_avg": fk, "WRITE_SIZE_KB_avg": wk,
