@@ -17,7 +17,7 @@ A=$(pick SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_IN
 B=$(pick SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS \
          SQ_ACTIVE_INST_MISC SQ_LDS_BANK_CONFLICT)
 echo "pass A: $A"; echo "pass B: $B"
-REGEX='gemm_x3v|q_update_p|qp_codes|sgram'
+REGEX=${REGEX:-'gemm_x3v|q_update_p|qp_codes|sgram'}
 i=0
 for grp in "$A" "$B"; do
   i=$((i + 1))
