@@ -40,6 +40,7 @@ class GemmArgs(ctypes.Structure):
         ("w", c_vp), ("stride_w", c_i64),
         ("err_out", c_vp),
         ("syrk", c_int),
+        ("b_triu", c_int),
     ]
 
 
@@ -421,8 +422,9 @@ def _mat(t: torch.Tensor):
 
 def gemm(A, B, *, ta=False, tb=False, C=None, alpha=1.0, beta=0.0, D=None, gamma=0.0,
          epi=EPI_LINEAR, absmax=None, w=None, err_out=None, alpha_v=None, beta_v=None,
-         gamma_v=None, batch=None, syrk=False):
-    """Batched C = alpha op(A) op(B) + beta C + gamma D (or RESID / WERR epilogues)."""
+         gamma_v=None, batch=None, syrk=False, b_triu=False):
+    """Batched C = alpha op(A) op(B) + beta C + gamma D (or RESID / WERR epilogues).
+    b_triu: B (not transposed) is upper triangular -- its zero K slices are skipped."""
     _require_hip(A, B, C, D, w)
     A_, lda, sa = _mat(A)
     B_, ldb, sb = _mat(B)
@@ -459,6 +461,7 @@ def gemm(A, B, *, ta=False, tb=False, C=None, alpha=1.0, beta=0.0, D=None, gamma
         g.stride_w = w.shape[-1] if (w.dim() == 2 and w.shape[0] > 1) else 0
     g.err_out = err_out.data_ptr() if err_out is not None else None
     g.syrk = int(bool(syrk))
+    g.b_triu = int(bool(b_triu))
     lib = load()
     dev = A.device
     nws = lib.cq_gemm_workspace(ctypes.byref(g))

@@ -39,6 +39,7 @@ struct KArgs {
     double* part;
     int vec_a, vec_b;
     int64_t tri;
+    int b_triu;  // op(B) upper triangular (op(B)[k][n] = 0 for k > n): zero K slices skipped
 };
 
 // Stage one BM x BK slice of op(A) into registers (4 floats x 2 per thread).
@@ -210,7 +211,8 @@ __device__ __forceinline__ void gemm_epilogue(const KArgs& a, f32x16 (&acc)[2][N
 
 // NB = 32-wide MFMA column blocks per wave (2: 128x128 tile, 1: 128x64 tile for narrow N).
 // a.tri != 0: SYRK mode — grid.x enumerates the upper-triangular 128x128 tiles only.
-template <bool TA, bool TB, int EPI, bool DF16, int NB>
+// TRIU: a.b_triu (own instantiation: the slice test costs the plain kernel its third wave per SIMD)
+template <bool TA, bool TB, int EPI, bool DF16, int NB, bool TRIU = false>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
     constexpr int BNT = 64 * NB;
     __shared__ __attribute__((aligned(16))) float smem[2 * BK * LDA_S + 2 * BK * LDB_S];
@@ -259,18 +261,25 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
         }
         const float* As = As0 + cur * BK * LDA_S;
         const float* Bs = Bs0 + cur * BK * LDB_S;
+        // TRIU (op(B) upper triangular): a wave whose last column n0 + 32 NB (wn + 1) - 1 lies
+        // before this slice sees only zeros of op(B) and skips the slice's MFMAs (exact zero
+        // products: the same bits).  A per-32-column-block skip cost the allocator a wave per SIMD.
+        bool live = true;
+        if constexpr (TRIU) live = t * BK <= n0 + 32 * NB * (wn + 1) - 1;
+        if (live) {
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            const float* ar = As + (kk + lk) * LDA_S + wm * 64 + li;
-            const float* br = Bs + (kk + lk) * LDB_S + wn * (32 * NB) + li;
-            const float a0 = ar[0], a1 = ar[32];
-            float bv[NB];
+            for (int kk = 0; kk < BK; kk += 2) {
+                const float* ar = As + (kk + lk) * LDA_S + wm * 64 + li;
+                const float* br = Bs + (kk + lk) * LDB_S + wn * (32 * NB) + li;
+                const float a0 = ar[0], a1 = ar[32];
+                float bv[NB];
 #pragma unroll
-            for (int j = 0; j < NB; ++j) bv[j] = br[32 * j];
+                for (int j = 0; j < NB; ++j) bv[j] = br[32 * j];
 #pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[j], acc[0][j], 0, 0, 0);
-                acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[j], acc[1][j], 0, 0, 0);
+                for (int j = 0; j < NB; ++j) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[j], acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[j], acc[1][j], 0, 0, 0);
+                }
             }
         }
         if (t + 1 < nt) {
@@ -444,6 +453,12 @@ using namespace cq;
 
 template <int EPI, bool DF16, int NB>
 static void launch_gemm_nb(bool ta, bool tb, dim3 grid, hipStream_t s, const KArgs& k) {
+    if constexpr (EPI == CQ_EPI_LINEAR && !DF16) {
+        if (!ta && !tb && k.b_triu) {
+            gemm_f32_kernel<false, false, EPI, DF16, NB, true><<<grid, kGemmThreads, 0, s>>>(k);
+            return;
+        }
+    }
     if (!ta && !tb) gemm_f32_kernel<false, false, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
     else if (!ta && tb) gemm_f32_kernel<false, true, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
     else if (ta && !tb) gemm_f32_kernel<true, false, EPI, DF16, NB><<<grid, kGemmThreads, 0, s>>>(k);
@@ -513,6 +528,9 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
     const int nb = g->syrk ? 2 : pick_nb(g->N);
     dim3 grid((unsigned)ceil_div(g->N, 64 * nb), (unsigned)ceil_div(g->M, BM), (unsigned)g->batch);
     k.tri = 0;
+    k.b_triu = g->b_triu;
+    CQ_REQUIRE(!g->b_triu || (!g->trans_a && !g->trans_b && !g->syrk && g->epi == CQ_EPI_LINEAR),
+               "cq_gemm_f32: b_triu needs a plain product (no transposes, LINEAR epilogue)");
     if (g->syrk) {
         const int64_t T = ceil_div(g->N, BM);
         k.tri = T;

@@ -301,7 +301,7 @@ class RankRSolver:
         out = self._free(X, *keep)
         M = K.gram_f64(X, X)
         Wt32, _, info = K.spd_whiten(M)
-        K.gemm(X, Wt32, C=out)
+        K.gemm(X, Wt32, C=out, b_triu=True)  # Wt upper triangular (zeros stored)
         return out, info
 
     def _rr(self, X, *keep, single=False, values_only=False):
@@ -725,7 +725,7 @@ class RandSVD:
         for _ in range(2):  # CholQR2
             M = K.gram_f64(X, X)
             Wt32, _, _ = K.spd_whiten(M)
-            X = K.gemm(X, Wt32, C=torch.empty_like(X))
+            X = K.gemm(X, Wt32, C=torch.empty_like(X), b_triu=True)
         return X
 
     def solve_iter(self, Y: torch.Tensor, warm: bool = True, y_split=None):

@@ -184,6 +184,9 @@ typedef struct cq_gemm_args {
     int syrk;                        /* 1: C = alpha op(A) op(B) is symmetric (A = B^T up to
                                         op): only upper 128x128 tiles are computed, then
                                         mirrored (LINEAR, beta = gamma = 0)               */
+    int b_triu;                      /* 1: B (not transposed) is upper triangular, B[k][n] = 0
+                                        for k > n (a CholQR whitening factor): the K slices
+                                        that meet only its zeros are skipped (same bits)   */
 } cq_gemm_args;
 
 size_t cq_gemm_workspace(const cq_gemm_args* a);

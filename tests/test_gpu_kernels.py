@@ -522,6 +522,18 @@ def test_gemm_x3_exact_b_matches_three_products(K, Bt, M, N, Kd, lda):
     assert torch.equal(C2k, C3k)
 
 
+@pytest.mark.parametrize("M,N", [(4096, 192), (1000, 64), (300, 100), (520, 300), (96, 384)])
+def test_gemm_b_triu_matches_plain(K, M, N):
+    """b_triu (CholQR's X Wt with Wt upper triangular, zeros stored): the same bits as the
+    plain product -- the skipped K slices only meet exact zeros of B."""
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    A = torch.randn(3, M, N, device=DEV, generator=g)
+    Bt = torch.triu(torch.randn(3, N, N, device=DEV, generator=g))
+    C0 = K.gemm(A, Bt, C=torch.empty(3, M, N, device=DEV))
+    C1 = K.gemm(A, Bt, C=torch.full((3, M, N), float("nan"), device=DEV), b_triu=True)
+    assert torch.equal(C0, C1)
+
+
 def test_residual_split_exact_w_skips_lo(K):
     """fp16 W without codes or column weights: scale >= 1 (also for max|W| >= 2^14), hi = W * s
     exactly, lo / tlo optional (zero when written)."""

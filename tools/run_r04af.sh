@@ -1,0 +1,17 @@
+# GPU box, round 4 (aa): triangular CholQR multiply -- new tests, suite, config 2
+# bench + kernel trace, config 4t bench.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r04af}; mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_kernels.py -k "exact or triu" -q -x --timeout 120 --timeout-method thread > $O/new_tests.log 2>&1
+rc=$?; echo "new tests rc=$rc"; tail -3 $O/new_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
+tail -1 $O/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("api_single"))'
+mkdir -p $O/kt_cfg2
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt_cfg2/t -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-api-path > $O/kt_cfg2/s.log 2>&1 || exit $?
+python3 tools/ktrace_summary.py $O/kt_cfg2 > $O/kt_cfg2/summary.txt; grep -i "x3v\|residual\|total" $O/kt_cfg2/summary.txt | head -6 | cut -c1-150
+timeout -k 10 500 python3 -u bench.py --workload cfg4t --steps 2 --warmup 1 --no-cpu-baseline --no-api-path > $O/bench_cfg4t.log 2>&1 || exit $?
+tail -1 $O/bench_cfg4t.log | cut -c1-120
