@@ -108,8 +108,12 @@ __global__ __launch_bounds__(kGramThreads) void gram_f64_mfma_kernel(
     int64_t M, int64_t N, int64_t K, int64_t kchunk, int splits, const float* __restrict__ A,
     int64_t lda, int64_t sa, const float* __restrict__ B, int64_t ldb, int64_t sb, int sym,
     double* __restrict__ part) {
-    __shared__ float As[2][GK][GT + 4];
-    __shared__ float Bs[2][GK][GT + 4];
+    // row pitch: GT + 16 floats puts the fragment reads' four K rows (lane >> 4) 16 banks apart
+    // (conflict-free; GT + 4 overlapped them: 3.2 conflict cycles per LDS instruction in PMC);
+    // the TK stash writes columns and keeps GT + 4
+    constexpr int GP = TK ? GT + 4 : GT + 16;
+    __shared__ float As[2][GK][GP];
+    __shared__ float Bs[2][GK][GP];
     const int64_t b = blockIdx.z / splits;
     const int split = blockIdx.z % splits;
     if (sym && blockIdx.x < blockIdx.y) return;
