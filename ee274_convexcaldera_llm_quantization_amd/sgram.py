@@ -31,26 +31,36 @@ def applicable(m: int, n: int, W: torch.Tensor, q_bits: int, packed: bool, dense
 def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch.Tensor, Gh, Gl, out_scale: float,
            yh: torch.Tensor, yl: torch.Tensor, ys=None, wth=None, wtl=None, wsq=None):
     """A (B, m, m) fp32 upper triangle = (W diag(ycol)) (W diag(ycol))^T on split-fp16 products
-    (cq_gemm_x3 Gram of W's K-blocked halves, written into yh/yl (B, m, n); H = I makes them
-    exact, lo = 0).  Gh/Gl receive a split of A that the caller overwrites later.  The same pass
-    can also write the halves of (W diag(ycol))^T (wth/wtl (B, n, m), K-blocked over m: the B
-    operand of R = U^T Y) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,).
-    Without ycol the halves are exact (fp16 W under a split scale >= 1: lo = 0): the lo halves
-    are not written (wtl may be None; its products run as gemm_x3 b_exact)."""
+    (cq_gemm_x3 Gram, tri + sym_out).  H = I: the K-blocked halves of W written into yh are
+    exact (fp16 W under a split scale >= 1, lo = 0) and one fp16 product gives the same bits as
+    three.  Diagonal H: A = (W diag(ycol^2)) W^T from the split halves of W diag(ycol^2) (yh/yl)
+    against W itself (fp16, exact: b_exact, two products instead of three; the B operand is W's
+    row-major storage, no halves written).  Gh/Gl receive a split of A that the caller
+    overwrites later.  The same work writes the halves of (W diag(ycol))^T (wth/wtl (B, n, m),
+    K-blocked over m: the B operand of R = U^T Y; wtl may be None without ycol, its products
+    then run as b_exact) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,)."""
     B, m, n = Ws.shape
     dev = Ws.device
     if ys is None:
         ys = torch.empty(B, dtype=torch.float32, device=dev)
-    exact = ycol is None and Ws.dtype == torch.float16
-    assert exact or wth is None or wtl is not None
-    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, hi=yh, lo=None if exact else yl, thi=wth,
-                     tlo=None if exact else wtl, scale=ys, sq=wsq)
     bound = torch.full((B,), 2.0 ** 60, dtype=torch.float64, device=dev)  # any bound >= max|A|: halves unused
     so = torch.empty(B, dtype=torch.float32, device=dev)
     io = torch.empty(B, dtype=torch.float32, device=dev)
-    # H = I: W's halves are W itself (fp16) and zeros -- one fp16 product gives the same bits
-    K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), A, tri=True, a_blocked=True, b_blocked=True, out_h=Gh, out_l=Gl,
-              out_scale=out_scale, sym_bound=bound, scale_out=so, inv_out=io, single=ycol is None)
+    gram = dict(tri=True, a_blocked=True, out_h=Gh, out_l=Gl, out_scale=out_scale, sym_bound=bound, scale_out=so,
+                inv_out=io)
+    if ycol is None:
+        assert Ws.dtype == torch.float16
+        K.residual_split(Ws, None, None, 2, wmax, hi=yh, thi=wth, scale=ys, sq=wsq)
+        # H = I: W's halves are W itself (fp16) and zeros -- one fp16 product gives the same bits
+        K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), A, b_blocked=True, single=True, **gram)
+        return
+    assert wth is None or wtl is not None
+    if wth is not None or wsq is not None:  # (W diag(ycol))^T's halves and ||W diag(ycol)||^2
+        K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, thi=wth, tlo=wtl, scale=ys, sq=wsq)
+    y2 = (ycol * ycol).contiguous()
+    ys2 = torch.empty(B, dtype=torch.float32, device=dev)
+    K.residual_split(Ws, None, None, 2, wmax, ycol=y2, ycol_max=ycol_max * ycol_max, hi=yh, lo=yl, scale=ys2)
+    K.gemm_x3(yh, yl, Ws, None, 1.0 / ys2, A, b_blocked=False, b_exact=True, **gram)
 
 
 class SparseGram:
