@@ -125,7 +125,7 @@ _SIGS = {
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
-                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_size, c_vp]),
     "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
     "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
@@ -905,15 +905,17 @@ def sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, scale_out, inv_out, G3
 
 
 def residual_split(Ws, packed, qscale, bits, wmax, *, ycol=None, ycol_max=1.0, res=None, Y=None, hi=None, lo=None,
-                   thi=None, tlo=None, scale=None, sq=None):
-    """Fused LR-step residual (see include/caldera_hip.h cq_residual_split).  Ws (B, m, n)."""
-    _require_hip(Ws, packed, qscale, wmax, ycol, res, Y, hi, lo, thi, tlo, scale, sq)
+                   thi=None, tlo=None, scale=None, sq=None, ycol_hi=None, ycol_hi_max=1.0, scale_hi=None):
+    """Fused LR-step residual (see include/caldera_hip.h cq_residual_split).  Ws (B, m, n).
+    ycol_hi: hi/lo are the halves of res * ycol_hi (their scale in scale_hi) instead."""
+    _require_hip(Ws, packed, qscale, wmax, ycol, res, Y, hi, lo, thi, tlo, scale, sq, ycol_hi, scale_hi)
     B, m, n = Ws.shape
     dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[Ws.dtype]
     lib = load()
     ws = workspace(lib.cq_residual_split_workspace(m, n, B), Ws.device) if sq is not None else None
     _check(lib.cq_residual_split(dt, _p(Ws), _p(packed), _p(qscale), int(bits), _p(ycol), float(ycol_max), _p(wmax),
-                                 B, m, n, _p(res), _p(Y), _p(hi), _p(lo), _p(thi), _p(tlo), _p(scale), _p(sq), _p(ws),
+                                 B, m, n, _p(res), _p(Y), _p(hi), _p(lo), _p(thi), _p(tlo), _p(scale), _p(sq),
+                                 _p(ycol_hi), float(ycol_hi_max), _p(scale_hi), _p(ws),
                                  0 if ws is None else ws.numel(), _stream(Ws.device)), "cq_residual_split")
 
 

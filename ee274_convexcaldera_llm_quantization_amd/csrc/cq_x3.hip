@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
     const float* __restrict__ ycol, const float* __restrict__ wmax, float ycmax, int64_t m, int64_t n,
     float* __restrict__ res, float* __restrict__ Y, _Float16* __restrict__ hi, _Float16* __restrict__ lo,
     _Float16* __restrict__ thi, _Float16* __restrict__ tlo, float* __restrict__ scale_out,
-    double* __restrict__ part) {
+    double* __restrict__ part, const float* __restrict__ ycol_hi, float ychmax, float* __restrict__ scale_hi_out) {
     __shared__ float tile[64][33];
     __shared__ double red[4];
     constexpr float k = BITS == 32 ? 1.f : (float)((1 << (BITS - 1)) - 1);
@@ -1141,6 +1141,15 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
     const bool exact = DT == CQ_F16 && !qc && !ycol;
     const float sc = exact ? fmaxf(ldexpf(1.f, 14 - e2), 1.f) : ldexpf(1.f, 14 - e2);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && scale_out) scale_out[b] = sc;
+    // ycol_hi: the column-blocked halves (hi/lo) are of res * ycol_hi instead, at their own scale
+    float sch = sc;
+    if (ycol_hi) {
+        int e3 = 0;
+        const float bnd = (wmax[b] + qs) * ychmax;
+        if (bnd > 0.f && isfinite(bnd)) frexpf(bnd, &e3);
+        sch = ldexpf(1.f, 14 - e3);
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) scale_hi_out[b] = sch;
+    }
     const int t = threadIdx.x;
     const int r = t >> 3, c8 = (t & 7) * 8;          // row in tile, first of 8 columns
     const int64_t j0 = (int64_t)blockIdx.x * 64;
@@ -1214,7 +1223,7 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
             _Float16 h8[8], l8[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const float xs = yv[u] * sc;
+                const float xs = ycol_hi ? rv[u] * ycol_hi[j + u] * sch : yv[u] * sc;
                 h8[u] = (_Float16)xs;
                 l8[u] = (_Float16)(xs - (float)h8[u]);
             }
@@ -1734,7 +1743,8 @@ size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch) {
 int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,
                       const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m, int64_t n,
                       float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo, uint16_t* thi, uint16_t* tlo,
-                      float* scale_out, double* sq_out, void* ws, size_t ws_bytes, void* stream) {
+                      float* scale_out, double* sq_out, const float* ycol_hi, float ycol_hi_max, float* scale_hi_out,
+                      void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(Ws && wmax && batch > 0 && batch < 65536 && m > 0 && n > 0, "cq_residual_split: bad args");
     CQ_REQUIRE(m % 32 == 0 && n % 64 == 0, "cq_residual_split: m % 32 and n % 64 must be 0");
     CQ_REQUIRE(!packed || qscale, "cq_residual_split: scale required with codes");
@@ -1743,6 +1753,7 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     CQ_REQUIRE((!lo || hi) && (!tlo || thi) && (exact || (!hi == !lo && !thi == !tlo)),
                "cq_residual_split: halves go in pairs (lo optional only for fp16 W without codes or ycol)");
     CQ_REQUIRE((!hi && !thi) || scale_out, "cq_residual_split: halves need scale_out");
+    CQ_REQUIRE(!ycol_hi || (hi && lo && scale_hi_out), "cq_residual_split: ycol_hi needs hi, lo and scale_hi_out");
     CQ_REQUIRE(!sq_out || (ws && ws_bytes >= cq_residual_split_workspace(m, n, batch)), "cq_residual_split: workspace too small");
     const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(m / 32, 16));
     dim3 grid((unsigned)(n / 64), (unsigned)gy, (unsigned)batch);
@@ -1750,7 +1761,7 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     double* part = sq_out ? reinterpret_cast<double*>(ws) : nullptr;
     auto h = [](uint16_t* p) { return reinterpret_cast<_Float16*>(p); };
 #define CQ_RS(DT, B) residual_split_kernel<DT, B><<<grid, 256, 0, s>>>(Ws, packed, qscale, ycol, wmax, ycol_max, m, n, \
-        res_out, Y_out, h(hi), h(lo), h(thi), h(tlo), scale_out, part)
+        res_out, Y_out, h(hi), h(lo), h(thi), h(tlo), scale_out, part, ycol_hi, ycol_hi_max, scale_hi_out)
     const int bsel = packed ? bits : 2;
     if (dtype == CQ_F16) {
         switch (bsel) { case 2: CQ_RS(CQ_F16, 2); break; case 4: CQ_RS(CQ_F16, 4); break;

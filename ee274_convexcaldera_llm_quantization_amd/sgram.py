@@ -55,11 +55,12 @@ def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch
         K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), A, b_blocked=True, single=True, **gram)
         return
     assert wth is None or wtl is not None
-    if wth is not None or wsq is not None:  # (W diag(ycol))^T's halves and ||W diag(ycol)||^2
-        K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, thi=wth, tlo=wtl, scale=ys, sq=wsq)
+    # one pass: (W diag(ycol))^T's halves and ||W diag(ycol)||^2 with ycol, the Gram operand's
+    # halves of W diag(ycol^2) at their own scale (ycol_hi)
     y2 = (ycol * ycol).contiguous()
     ys2 = torch.empty(B, dtype=torch.float32, device=dev)
-    K.residual_split(Ws, None, None, 2, wmax, ycol=y2, ycol_max=ycol_max * ycol_max, hi=yh, lo=yl, scale=ys2)
+    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, thi=wth, tlo=wtl, scale=ys, sq=wsq,
+                     hi=yh, lo=yl, ycol_hi=y2, ycol_hi_max=ycol_max * ycol_max, scale_hi=ys2)
     K.gemm_x3(yh, yl, Ws, None, 1.0 / ys2, A, b_blocked=False, b_exact=True, **gram)
 
 

@@ -340,13 +340,17 @@ int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out
  * (fp64).  The halves' scale (scale_out[b]) is the power of two for the bound
  * (wmax[b] + Q_scale[b]) * ycol_max >= max|Y|, and at least 1 for fp16 W without codes or
  * ycol: Y's halves are then exact (lo = 0) and lo / tlo may be NULL (gemm_x3 b_exact reads
- * only the hi halves).  m % 32 == 0, n % 64 == 0.
+ * only the hi halves).  ycol_hi (optional, with hi/lo): the column-blocked halves are of
+ * res * ycol_hi instead (the weighted Gram's W diag(ycol^2) operand), at the power of two for
+ * (wmax[b] + Q_scale[b]) * ycol_hi_max, written to scale_hi_out[b]; everything else keeps ycol.
+ * m % 32 == 0, n % 64 == 0.
  * bits == 32: `packed` is a dense fp32 Q and qscale[b] a bound on max|Q[b]|. */
 size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch);
 int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const float* qscale, int bits,
                       const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m,
                       int64_t n, float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo,
-                      uint16_t* thi, uint16_t* tlo, float* scale_out, double* sq_out, void* ws,
+                      uint16_t* thi, uint16_t* tlo, float* scale_out, double* sq_out,
+                      const float* ycol_hi, float ycol_hi_max, float* scale_hi_out, void* ws,
                       size_t ws_bytes, void* stream);
 
 /* Gram of the LR step's Y from sparse 2-bit codes (cq_sgram.hip).  Replaces, for m <= n,

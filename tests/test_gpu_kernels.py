@@ -534,6 +534,32 @@ def test_gemm_b_triu_matches_plain(K, M, N):
     assert torch.equal(C0, C1)
 
 
+def test_residual_split_ycol_hi_matches_two_passes(K):
+    """ycol_hi (the weighted Gram's operand): one pass writes the transposed halves and ||Y||^2
+    with ycol and the column-blocked halves of res * ycol^2 at their own scale -- the same bits
+    as two separate passes."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    B, m, n = 2, 96, 320
+    W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.3).half()
+    ycol = torch.rand(n, device=DEV, generator=g) * 2.0 + 0.1
+    y2 = (ycol * ycol).contiguous()
+    ymax = float(ycol.max())
+    wmax = K.absmax(W)
+    e = lambda: torch.empty(B, m, n, dtype=torch.float16, device=DEV)  # noqa: E731
+    hi, lo, thi, tlo = e(), e(), e(), e()
+    sc, sc2 = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    sq = torch.empty(B, dtype=torch.float64, device=DEV)
+    K.residual_split(W, None, None, 2, wmax, ycol=ycol, ycol_max=ymax, thi=thi, tlo=tlo, scale=sc, sq=sq, hi=hi, lo=lo,
+                     ycol_hi=y2, ycol_hi_max=ymax * ymax, scale_hi=sc2)
+    rhi, rlo, rthi, rtlo = e(), e(), e(), e()
+    rsc, rsc2 = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    rsq = torch.empty(B, dtype=torch.float64, device=DEV)
+    K.residual_split(W, None, None, 2, wmax, ycol=ycol, ycol_max=ymax, thi=rthi, tlo=rtlo, scale=rsc, sq=rsq)
+    K.residual_split(W, None, None, 2, wmax, ycol=y2, ycol_max=ymax * ymax, hi=rhi, lo=rlo, scale=rsc2)
+    for a, b in ((hi, rhi), (lo, rlo), (thi, rthi), (tlo, rtlo), (sc, rsc), (sc2, rsc2), (sq, rsq)):
+        assert torch.equal(a, b)
+
+
 def test_residual_split_exact_w_skips_lo(K):
     """fp16 W without codes or column weights: scale >= 1 (also for max|W| >= 2^14), hi = W * s
     exactly, lo / tlo optional (zero when written)."""
