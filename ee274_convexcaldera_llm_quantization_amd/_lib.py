@@ -70,6 +70,7 @@ class X3Args(ctypes.Structure):
         ("ksplit", c_int),
         ("split_ws", c_vp),
         ("b_exact", c_int),
+        ("colw", c_vp),
     ]
 
 
@@ -669,7 +670,7 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
-            single=False, ksplit=None, b_exact=False):
+            single=False, ksplit=None, b_exact=False, colw=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
@@ -677,7 +678,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     its upper triangle with scale s[b] from the bound (scale_out, inv_out = 1/(s out_scale));
     C may then be None.  lda / M (a_blocked only): A holds lda >= M rows of which the first M
     are used (C has M rows).  b_exact: B is exactly fp16 (Bl = 0, e.g. W's halves written
-    under a split scale >= 1); Bl is not read and may be None."""
+    under a split scale >= 1); Bl is not read and may be None.  colw (N,) fp32: the product
+    term of column j scaled by colw[j] (before beta P + gamma D)."""
     assert Bl is not None or b_exact or single
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, MA, Kd = Ah.shape
@@ -714,6 +716,9 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.o_blocked = int(bool(o_blocked))
     g.single = int(bool(single))
     g.b_exact = int(bool(b_exact))
+    if colw is not None:
+        assert colw.dtype == torch.float32 and colw.is_contiguous() and colw.numel() == N
+        g.colw = colw.data_ptr()
     # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
     # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups
     tiles = -(-N // 384) * -(-M // 192) * Bt

@@ -36,6 +36,7 @@ struct X3K {
     int ksplit;                // > 1: K cut into ksplit chunks, fp32 partials in part (split-K)
     float* part;               // [ksplit][batch][M][N]
     int b_nt = 0;              // B streamed once (one tile row): its LDS-DMA loads non-temporal
+    const float* colw = nullptr;  // [N] (or NULL): the product term scaled per C column
 };
 
 using f16x8g = __attribute__((ext_vector_type(8))) _Float16;

@@ -623,6 +623,11 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = al_ * (acc[i][j][r] * sc);
+            if (a.colw) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (col + r < a.N) v[r] *= a.colw[col + r];
+            }
             if (vec) {
                 if (a.P && be_ != 0.f) {
                     const float4 pv = *reinterpret_cast<const float4*>(a.P + b * a.sp + row * a.ldp + col);
@@ -695,6 +700,7 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         float w = al_ * s[r];
+        if (a.colw) w *= a.colw[col + r];
         if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + col + r];
         if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + col + r];
         a.C[b * a.sc + row * a.ldc + col + r] = w;
@@ -1811,6 +1817,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(!g->tri || (g->M == g->N && !g->P && !g->D && (!g->out_h || g->sym_out)),
                "cq_gemm_x3: tri needs a square plain product");
     a.single = g->single;
+    a.colw = g->colw;
+    CQ_REQUIRE(!g->colw || (!g->sym_out && !g->tri), "cq_gemm_x3: colw needs a plain product");
     // single + sym_out: the Gram of an exactly-fp16 operand (lo = 0; A = W W^T of the sparse-code
     // Gram, sgram.py): the split products add exact zeros, so one product gives the same bits
     a.sym_out = g->sym_out;

@@ -511,8 +511,9 @@ class CalderaEngine:
                 sv._alloc(dev)
                 if lite:
                     self._wth = scratch.get("lr.wth", (B, n, m), torch.float16, dev)
-                    # unweighted: (W)^T's halves are exact (lo = 0, sgram.gram_A), not written
-                    self._wtl = scratch.get("lr.wtl", (B, n, m), torch.float16, dev) if weighted else None
+                    # W^T's halves are exact (lo = 0, sgram.gram_A), not written; diagonal H
+                    # enters R = (U^T W) diag(ycol) in the product's epilogue
+                    self._wtl = None
                     self._ysw = torch.empty(B, dtype=torch.float32, device=dev)
                     self._wsq = torch.empty(B, dtype=torch.float64, device=dev)
                 # fp16 MFMA work: one product over the upper half (H = I: W's halves are W and 0),
@@ -700,10 +701,11 @@ class CalderaEngine:
         K.transpose_split(Lt, out=L)
 
     def _ut_w(self, sv, R, st, ycol):
-        """R~ = U^T Y = U^T (W diag(ycol)) - s (U^T c) diag(ycol) (m <= n, 2-bit Q = s c): the first
-        term a split-fp16 product of the block's transposed halves with (W diag(ycol))^T's halves
-        (written once per run by sgram.gram_A), the second from the codes' transpose by the sparse
-        product cq_codes_matmul, subtracted in the product's epilogue (gamma = -s)."""
+        """R~ = U^T Y = (U^T W) diag(ycol) - s (U^T c) diag(ycol) (m <= n, 2-bit Q = s c): the first
+        term a split-fp16 product of the block's transposed halves with W^T's exact halves
+        (written once per run by sgram.gram_A; two products, b_exact) with diag(ycol) applied in
+        its epilogue (colw), the second from the codes' transpose by the sparse product
+        cq_codes_matmul, subtracted in the same epilogue (gamma = -s)."""
         X = sv.X  # (B, m, p), orthonormal columns
         B, m, p = X.shape
         r, n = R.shape[1], R.shape[2]
@@ -715,7 +717,7 @@ class CalderaEngine:
         K.codes_matmul(ct, n, m, X, r, utc, roww=ycol, trans=True)
         inv = 1.0 / (self._ysw * X3_SCALE)
         K.gemm_x3(xh, xl, self._wth, self._wtl, inv, R, a_blocked=True, b_blocked=True, lda=p, M=r, D=utc,
-                  gamma_v=-st.Qs, b_exact=self._wtl is None)
+                  gamma_v=-st.Qs, b_exact=self._wtl is None, colw=None if ycol is None else ycol.contiguous())
 
     def _ut_y(self, sv, R):
         """R = U^T Y (U = the solver's Ritz block, first r columns; m <= n) as a split-fp16

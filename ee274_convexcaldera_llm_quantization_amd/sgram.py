@@ -36,9 +36,10 @@ def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch
     three.  Diagonal H: A = (W diag(ycol^2)) W^T from the split halves of W diag(ycol^2) (yh/yl)
     against W itself (fp16, exact: b_exact, two products instead of three; the B operand is W's
     row-major storage, no halves written).  Gh/Gl receive a split of A that the caller
-    overwrites later.  The same work writes the halves of (W diag(ycol))^T (wth/wtl (B, n, m),
-    K-blocked over m: the B operand of R = U^T Y; wtl may be None without ycol, its products
-    then run as b_exact) and ||W diag(ycol)||_F^2 (wsq, fp64), with their scale in ys (B,)."""
+    overwrites later.  The same work writes the exact halves of W^T (wth (B, n, m), K-blocked
+    over m, lo = 0: the B operand of R = (U^T W) diag(ycol), run as gemm_x3 b_exact with the
+    column weights in its epilogue) and ||W diag(ycol)||_F^2 (wsq, fp64), with the halves'
+    scale in ys (B,)."""
     B, m, n = Ws.shape
     dev = Ws.device
     if ys is None:
@@ -54,13 +55,16 @@ def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch
         # H = I: W's halves are W itself (fp16) and zeros -- one fp16 product gives the same bits
         K.gemm_x3(yh, yl, yh, yl, 1.0 / (ys * ys), A, b_blocked=True, single=True, **gram)
         return
-    assert wth is None or wtl is not None
-    # one pass: (W diag(ycol))^T's halves and ||W diag(ycol)||^2 with ycol, the Gram operand's
-    # halves of W diag(ycol^2) at their own scale (ycol_hi)
+    # one pass: W^T's exact halves (R = (U^T W) diag(ycol) takes the column weights in its
+    # epilogue, gemm_x3 colw) and the Gram operand's halves of W diag(ycol^2) at their own
+    # scale (ycol_hi); ||W diag(ycol)||^2 from the weighted square sum
+    assert wtl is None
     y2 = (ycol * ycol).contiguous()
     ys2 = torch.empty(B, dtype=torch.float32, device=dev)
-    K.residual_split(Ws, None, None, 2, wmax, ycol=ycol, ycol_max=ycol_max, thi=wth, tlo=wtl, scale=ys, sq=wsq,
-                     hi=yh, lo=yl, ycol_hi=y2, ycol_hi_max=ycol_max * ycol_max, scale_hi=ys2)
+    K.residual_split(Ws, None, None, 2, wmax, thi=wth, scale=ys, hi=yh, lo=yl, ycol_hi=y2,
+                     ycol_hi_max=ycol_max * ycol_max, scale_hi=ys2)
+    if wsq is not None:
+        wsq.copy_(K.weighted_sqsum(Ws, y2, n))
     K.gemm_x3(yh, yl, Ws, None, 1.0 / ys2, A, b_blocked=False, b_exact=True, **gram)
 
 

@@ -325,6 +325,10 @@ typedef struct cq_x3_args {
     int b_exact;                   /* B is exactly fp16 (Bl = 0, e.g. W's halves under a split
                                       scale >= 1): two products al x bh + ah x bh, Bl not read
                                       (may be NULL); the same bits as the three products */
+    const float* colw;             /* [N] or NULL (not with tri / sym_out): the product term of
+                                      C column j is scaled by colw[j] before beta P + gamma D
+                                      (R = (U^T W) diag(ycol) - s (U^T c) diag(ycol) from W's
+                                      exact halves)                                        */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
