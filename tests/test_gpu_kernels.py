@@ -560,6 +560,30 @@ def test_residual_split_ycol_hi_matches_two_passes(K):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("Bt,ks", [(3, 1), (1, None)])
+def test_gemm_x3_colw_epilogue(K, Bt, ks):
+    """colw (R = (U^T W) diag(ycol) - s U^T c diag(ycol)): the product term times colw[j], then
+    gamma D -- the same bits as scaling the plain product's columns afterwards, in the one-pass
+    kernel and in the split-K epilogue (ks None: automatic split-K for a single matrix)."""
+    g = torch.Generator(device=DEV).manual_seed(31 + Bt)
+    M, N, Kd, lda = 128, 1024, 2048, 192
+    A = torch.randn(Bt, lda, Kd, device=DEV, generator=g)
+    Wm = (torch.randn(Bt, N, Kd, device=DEV, generator=g) * 0.05).half().float()
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 10, blocked=True)
+    Bh, _ = K.split_f16(Wm.contiguous(), 2.0 ** 14, blocked=True)
+    inv = torch.full((Bt,), 2.0 ** -24, device=DEV)
+    D = torch.randn(Bt, M, N, device=DEV, generator=g)
+    gam = torch.randn(Bt, device=DEV, generator=g)
+    w = torch.rand(N, device=DEV, generator=g) + 0.5
+    C = torch.full((Bt, M, N), float("nan"), device=DEV)
+    K.gemm_x3(Ah, Al, Bh, None, inv, C, a_blocked=True, b_blocked=True, lda=lda, M=M, D=D, gamma_v=gam,
+              b_exact=True, colw=w, ksplit=ks)
+    C0 = torch.full_like(C, float("nan"))
+    K.gemm_x3(Ah, Al, Bh, None, inv, C0, a_blocked=True, b_blocked=True, lda=lda, M=M, b_exact=True, ksplit=ks)
+    ref = C0 * w.view(1, 1, N) + gam.view(Bt, 1, 1) * D
+    assert torch.equal(C, ref)
+
+
 def test_residual_split_exact_w_skips_lo(K):
     """fp16 W without codes or column weights: scale >= 1 (also for max|W| >= 2^14), hi = W * s
     exactly, lo / tlo optional (zero when written)."""
