@@ -35,7 +35,6 @@ struct X3K {
     float* inv_out;            // [batch] 1 / (scale * out_scale)
     int ksplit;                // > 1: K cut into ksplit chunks, fp32 partials in part (split-K)
     float* part;               // [ksplit][batch][M][N]
-    int b_nt = 0;              // B streamed once (one tile row): its LDS-DMA loads non-temporal
     const float* colw = nullptr;  // [N] (or NULL): the product term scaled per C column
 };
 

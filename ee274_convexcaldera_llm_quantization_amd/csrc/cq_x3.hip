@@ -18,7 +18,6 @@
 // halves of the next iterate, or the Gram's mirrored K-blocked halves).
 #include <type_traits>
 #include <numeric>
-#include <cstdlib>
 
 #include "cq_x3.h"
 
@@ -61,12 +60,10 @@ constexpr size_t XW_LDS_BYTES = (size_t)2 * XW_STAGE * sizeof(_Float16);  // 144
 constexpr int XW_PER_WAVE = (2 * XW_BM / 16 + 2 * XW_BN / 16) / (XW_THREADS / 64);  // 6
 static_assert(XW_PER_WAVE == 6, "load split");
 
-// One 16-B-per-lane LDS-DMA load; nt (wave-uniform): non-temporal, for bytes one tile reads once
-__device__ __forceinline__ void xw_load(const _Float16* src, _Float16* dst, bool nt) {
-    if (nt)
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 2);
-    else
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+// One 16-B-per-lane LDS-DMA load (default cache policy: non-temporal loads of the once-read
+// B panels measured 0.5-3 % slower, profiles/r04aq_nt_ab)
+__device__ __forceinline__ void xw_load(const _Float16* src, _Float16* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
 // Load plan: the wave-uniform part of each of this wave's 6 LDS-DMA loads (which image,
@@ -101,7 +98,7 @@ __device__ __forceinline__ void xw_issue(const X3K& a, int64_t b, int64_t k0, _F
         const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART + part * XW_BPART) + (16 * sub) * XW_BK;
-        xw_load(base + off[u], dst, !isA && a.b_nt);
+        xw_load(base + off[u], dst);
     }
 }
 
@@ -271,7 +268,7 @@ __device__ __forceinline__ void xv1_issue(const X3K& a, int64_t b, int64_t k0, _
         const _Float16* base = isA ? a.Ah + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? 0 : XW_APART) + (16 * sub) * XW_BK;
-        xw_load(base + off[u], dst, !isA && a.b_nt);
+        xw_load(base + off[u], dst);
     }
 }
 
@@ -374,7 +371,7 @@ __device__ __forceinline__ void xv2_issue(const X3K& a, int64_t b, int64_t k0, _
         const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
                                    : a.Bh + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
         _Float16* dst = stage + (isA ? part * XW_APART : 2 * XW_APART) + (16 * sub) * XW_BK;
-        xw_load(base + off[u], dst, !isA && a.b_nt);
+        xw_load(base + off[u], dst);
     }
 }
 
@@ -1851,12 +1848,6 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         total *= a.ksplit;
     }
     CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
-    {   // one tile row: every B panel is read by one workgroup, once -- non-temporal loads keep
-        // it from evicting the A slices the row's tiles re-read (filter G X^T, R = U^T W: 1-3 %
-        // less time per launch in A/B runs, profiles/r04ab_*; CQ_X3_NT=0 turns it off)
-        static const char* e = getenv("CQ_X3_NT");
-        a.b_nt = (!(e && e[0] == '0') && !a.tri && !a.sym_out && a.tiles_m == 1) ? 1 : 0;
-    }
     if (a.single) gemm_x3v_kernel<1><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     else if (g->b_exact) gemm_x3v_kernel<2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     else gemm_x3v_kernel<0><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
