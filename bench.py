@@ -7,7 +7,12 @@ alg.py:24-112) over B matrices resident in HBM.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload cfg2|cfg3|cfg5|model]
                   [--no-cpu-baseline] [--no-parity] [--no-api-path]
 
-Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank decomposes
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, WORLD_SIZE unset) starts
+`python -m torch.distributed.run --nproc-per-node N bench.py <same args>` as a child process
+before anything touches the GPU and exits with its return code (rank 0's JSON line goes to the
+shared stdout); launched by torch.distributed.run directly, WORLD_SIZE must equal --gpus.
+--dry-run: the same launcher and gather over gloo on the CPU with a stub decomposer (tiny
+matrices, no HIP device, no oracle): plumbing test of the N-rank path.  Every rank decomposes
 its own batch (matrices are independent: weak scaling) and, inside each timed step, its
 packed results (2-bit codes, L, R, scales) are gathered to rank 0 over RCCL -- the one
 collective of the path; the timed region is bracketed by barrier + synchronize and the max
@@ -31,6 +36,8 @@ rank 0 over RCCL -- strong scaling (the model is fixed), timed end to end includ
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -293,6 +300,54 @@ def run_model(args):
     def step():
         return S.decompose_sharded(items, decompose, rank=rank, world=world, max_batch=max_batch, device=dev)
 
+    emu = None
+    if args.emulate_world:
+        # strong-scaling projection on ONE GPU ("scaling 1->8 GPUs (cfg4) >= 6x"):
+        # time exactly rank r's round-robin share of the model at world W (shard_indices(224, W, r),
+        # the batch sizes a W-GPU run uses) plus the packing of its results for the gather, for
+        # every r (or --emulate-rank); the RCCL transfer itself is not included
+        assert world == 1, "--emulate-world runs on one GPU"
+        W_ = args.emulate_world
+        mb_e = args.model_batch or (16 if W_ >= 8 else 64)
+        grp_e = 4 if mb_e <= 16 else 2
+
+        def run_all_e(batches):
+            res = []
+            for g0 in range(0, len(batches), grp_e):
+                grp = batches[g0:g0 + grp_e]
+                engines = [CalderaEngine(ep) for _ in grp]
+                run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)],
+                                dev)
+                res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"],
+                                       d["R"], d["global_scale"], d["errors"])
+                        for b, e in zip(grp, engines) for (name, m, n, _), d in zip(b, e.last_packed)]
+            return res
+
+        def dec_e(batch_items):
+            return run_all_e([batch_items])
+        dec_e.run_all = run_all_e
+        ranks = [args.emulate_rank] if args.emulate_rank is not None else list(range(W_))
+        share_t = {}
+        for r_ in ranks:
+            def share_step():
+                res = S.decompose_sharded(items, dec_e, rank=r_, world=W_, max_batch=mb_e, gather=False, device=dev)
+                return S.pack_results(res, device=dev)  # what the rank hands to the gather
+            for _ in range(max(1, args.warmup)):
+                share_step()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(args.steps):
+                t0 = time.perf_counter()
+                share_step()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            share_t[r_] = sorted(ts)[len(ts) // 2]
+        emu = {"world": W_, "ranks_timed": ranks, "max_batch": mb_e, "interleaved_batches": grp_e,
+               "matrices_per_share": len(S.shard_indices(len(items), W_, ranks[0])),
+               "share_s": {str(k): v for k, v in share_t.items()}, "max_share_s": max(share_t.values()),
+               "note": "rank r's round-robin share decomposed + packed on one GPU (median of --steps); "
+                       "excludes the RCCL transfer to rank 0"}
+
     for _ in range(args.warmup):
         step()
     if world > 1:
@@ -329,11 +384,88 @@ def run_model(args):
             "gathered_bytes": int(sum(r.codes.numel() * r.codes.element_size() + r.L.numel() * 4 + r.R.numel() * 4
                                       for r in out)),
         }
+        if emu is not None:
+            emu["t_model_1gpu_s"] = el / args.steps
+            emu[f"projected_speedup_{emu['world']}"] = emu["t_model_1gpu_s"] / emu["max_share_s"]
+            result["strong_scaling_projection"] = emu
         if not args.no_parity:
             result["parity_pinned"] = model_parity(out, dev)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without WORLD_SIZE: run `python -m torch.distributed.run
+    --nproc-per-node N bench.py <argv>` as a fresh child process (this process has not touched
+    the GPU: importing torch does not) and return its exit code.  The ranks inherit stdout, so
+    rank 0's one JSON line is this command's output."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC (the box's only mode)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
+def run_dry(args):
+    """--dry-run: the N-rank step of main() without the GPU -- gloo process group on the CPU,
+    every rank 'decomposes' its batch with a deterministic stub (tiny matrices: packed 2-bit
+    codes, L, R of the result shapes; no arithmetic, no oracle), packs the results and gathers
+    them to rank 0 inside the timed step, barrier + max over ranks; rank 0 prints one JSON line."""
+    import torch.distributed as dist
+    from ee274_convexcaldera_llm_quantization_amd import sharding as S
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    B, m, n, r = args.batch or 4, 32, 64, 4
+
+    def step():
+        g = torch.Generator().manual_seed(rank)
+        res = [S.MatrixResult(f"rank{rank}.m{j}", m, n, r, 2, torch.randint(0, 256, (m * n // 4,), generator=g,
+                                                                               dtype=torch.uint8),
+                              1.0, torch.zeros(m, r), torch.zeros(r, n), 1.0, {"Q": [1.0], "LR": [1.0]})
+               for j in range(B)]
+        if world > 1:
+            pl = S.gather_to_rank0(S.pack_results(res), device=torch.device("cpu"))
+            return None if pl is None else [x for p in pl for x in S.unpack_results(p)]
+        return res
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = step()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        assert out is not None and len(out) == B * world, "gather incomplete"
+        print(json.dumps({
+            "metric": "dry run (stub decomposer, gloo): N-rank launch + gather plumbing, not a measurement",
+            "value": B * world * args.steps / el, "unit": "matrices/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "none (stub)", "data": "synthetic stub results",
+            "dry_run": True, "gathered_matrices": len(out),
+            "config": {"workload": "dry-run", "batch_per_gpu": B, "parallelism": f"dp{world} (matrix-sharded)"}}),
+            flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def main():
@@ -348,16 +480,33 @@ def main():
     ap.add_argument("--no-api-path", action="store_true")
     ap.add_argument("--model-batch", type=int, default=None,
                     help="--workload model: same-shape batch size (default 64 below 8 GPUs, 16 at 8)")
+    ap.add_argument("--emulate-world", type=int, default=None,
+                    help="--workload model on one GPU: also time each rank's share at this world size "
+                         "(projected strong scaling)")
+    ap.add_argument("--emulate-rank", type=int, default=None, help="with --emulate-world: only this rank")
     ap.add_argument("--solver-tol-steps", type=str, default=None,
                     help="comma-separated solver tolerances of the first LR updates (then the default)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="plumbing test of the N-rank path: gloo on the CPU, a stub decomposer on tiny "
+                         "matrices (no HIP device); the JSON line says dry_run")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's form `python bench.py --gpus N`: one process per GPU, started here
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one process per GPU "
+                         f"(python bench.py --gpus N, or torch.distributed.run --nproc-per-node N ... --gpus N)")
+    if args.dry_run:
+        return run_dry(args)
     if args.workload == "model":
         return run_model(args)
     wl = WORKLOADS[args.workload]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -616,4 +765,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -843,6 +843,9 @@ def codes_transpose(packed, rows, cols, out=None):
     return out
 
 
+CODES_MATMUL_MAX_R = 256  # cq_codes_matmul's r limit (cq_sgram.hip: RV <= 4 columns per lane)
+
+
 def codes_matmul(packed, rows, cols, X, r, out, *, colw=None, roww=None, trans=False):
     """out[b] = diag(roww) c[b] diag(colw) X[b][:, :r] (rows x r; trans: its transpose, r x rows) for
     2-bit packed codes c (B, rows, cols) and X (B, cols, ldx) fp32 (cq_codes_matmul)."""

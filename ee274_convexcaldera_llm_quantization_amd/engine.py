@@ -462,7 +462,12 @@ class CalderaEngine:
                 self._yl = scratch.get("lr.yl", gshape, torch.float16, dev)
                 self._ys = torch.empty(B, dtype=torch.float32, device=dev)
             ysq = torch.empty(B, dtype=torch.float64, device=dev)
-            x3_r = sv.left and not quantized and p.activation_aware_LR
+            # the LR error then comes by Pythagoras (below), which needs the error weights to be
+            # Y's own column weights: an H that passes allclose(H, I) (optimized_eigh, alg.py:11-23:
+            # unit eigenvalues) but is not exactly 1 keeps its h in the error (alg.py:286-302),
+            # so that case writes res and takes the fused error GEMM
+            pyth_ok = wts.ycol is not None or wts.err_unit
+            x3_r = sv.left and not quantized and p.activation_aware_LR and pyth_ok
             # quantised factors with unweighted Y (= res): the LPLR loop's m x n x r products run
             # on split-fp16 MFMAs from these halves (Y for Y R^T, res^T = Y^T for L^T res)
             x3_lplr = sv.left and quantized and not weighted and self.lplr_x3
@@ -473,12 +478,17 @@ class CalderaEngine:
             # R = U^T Y without a residual pass (2-bit codes, unquantised factors): U^T (W diag(ycol))
             # from W's transposed halves written once per run, minus s (U^T c) diag(ycol) from the
             # sparse codes (cq_codes_matmul); ||Y||^2 = ||W diag(ycol)||^2 + the codes' correction
-            lite = sparse_g and x3_r and not x3_lplr and p.Q_bits == 2 and self.r_from_codes
+            # (cq_codes_matmul takes r <= 256 columns of U: larger ranks keep the residual pass)
+            lite = (sparse_g and x3_r and not x3_lplr and p.Q_bits == 2 and self.r_from_codes
+                    and sv.r <= K.CODES_MATMUL_MAX_R)
             # m > n (gate/up projections): the same sparse-code Gram on the transposed problem,
             # G = Y^T Y = (W^T - s c^T)(W^T - s c^T)^T from W^T (once per run) and c^T (per step);
             # unweighted Y and unquantised factors (L = W V - s c V from W's halves and the codes)
             tall = (self.sparse_gram and not sv.left and st.has_Q and st.q_packed and not st.dense_q and not weighted
                     and not quantized and p.Q_bits == 2 and self.r_from_codes
+                    # nothing writes res on this path: the LR error must come by Pythagoras
+                    # (pyth_right below, unit error weights); codes_matmul takes r <= 256
+                    and wts.err_unit and wts.ycol is None and sv.r <= K.CODES_MATMUL_MAX_R
                     and sgram.applicable(n, m, Ws, p.Q_bits, True, wts.dense))
             if tall and self._sg_A is None:  # once per run: W^T, A = W^T W, W's halves, ||W||^2
                 self._wt16 = K.transpose_f16(Ws, out=scratch.get("sgram.wt", (B, n, m), torch.float16, dev))
@@ -652,7 +662,7 @@ class CalderaEngine:
         # activation-aware error: sum_j h_j (res - L R)^2  (alg.py:286-302, diagonal H)
         if wts.dense:
             return self._state_error(st, Ws, res, wts)
-        if sv.left and p.activation_aware_LR and not quantized and not rand:
+        if sv.left and p.activation_aware_LR and not quantized and not rand and (wts.ycol is not None or wts.err_unit):
             # L = U (orthonormal columns), L R = U U^T Y diag(1/sqrt(h)) with h the error
             # weights, so the weighted residual is (I - U U^T) Y and, by Pythagoras,
             # sum_j h_j (res - L R)_ij^2 = ||Y||^2 - ||U^T Y||^2 = ||Y||^2 - sum_j h_j R_ij^2

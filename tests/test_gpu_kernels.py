@@ -335,6 +335,34 @@ def test_jacobi_block_staged_equals_one_shot(K, want_vectors):
     assert (V1 is None and V2 is None) or torch.equal(V1, V2)
 
 
+@pytest.mark.parametrize("want_vectors", [True, False])
+@pytest.mark.parametrize("p", [2, 33, 64, 96, 192])
+def test_jacobi_block_staged_small_p(K, p, want_vectors):
+    """Small batches route every p (also p <= 192) to the staged block Jacobi
+    (solver.BJ_SMALL_SUBPROBLEMS): one matrix (B = 1: a single pair block at p <= 64, so the
+    values-only solve has no off-diagonal update), odd p (a ragged last block) and the
+    1024-thread subproblem solve.  Eigenvalues against LAPACK to fp64 accuracy; vectors
+    orthonormal and satisfying S V = V diag(ev) to fp32 accuracy."""
+    torch.manual_seed(100 + p)
+    X = torch.randn(1, 4 * p + 8, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    bj = K.BlockJacobi(S.clone().to(DEV), 1e-9, want_vectors)
+    left = bj.sweeps(2, begin=True)
+    while left and bj.swept < 40:
+        left = bj.sweeps(2)
+    ev, V32, _, sw = bj.finish()
+    assert left == 0
+    ref = torch.linalg.eigvalsh(S).flip(-1)
+    ev = ev.cpu()
+    assert ((ev - ref).abs() / ref[:, 0:1]).max().item() < 1e-12
+    if not want_vectors:
+        assert V32 is None
+        return
+    V = V32.cpu().double()
+    assert (V.transpose(1, 2) @ V - torch.eye(p, dtype=torch.float64)).abs().max() < 2e-5
+    assert (S @ V - V * ev.unsqueeze(1)).abs().max().item() < 2e-5 * ref.max().item()
+
+
 @pytest.mark.parametrize("p", [64, 128, 180, 192])
 def test_jacobi_register_path_accuracy(K, p):
     """p <= 192: fp64 A in LDS + fp32 V in registers (the solver's Rayleigh-Ritz path):

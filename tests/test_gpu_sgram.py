@@ -5,6 +5,8 @@ of W) and P = (W - (s/2) c) diag(w) c^T over the sliced-ELL codes.  Checked: the
 nonzero counts (exact), the fp32 G and its K-blocked split halves (fp32-grade against fp64,
 and against the dense split-fp16 Gram of Y that it replaces), for every LDS slab height
 (R = 8 / 4 / 2 rows of E by contraction length) and with and without column weights."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -189,3 +191,45 @@ def test_lr_step_from_codes_matches_residual_pass(m, n, weighted):
         qa = a["Q"].double() + a["L"].double() @ a["R"].double()
         qb = b["Q"].double() + b["L"].double() @ b["R"].double()
         assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qb)) < 2e-5
+
+
+@pytest.mark.parametrize("case", ["tall_not_aware_h", "wide_allclose_I", "tall_allclose_I", "rank_over_256"])
+def test_lr_step_gates_write_what_the_error_reads(case):
+    """Configurations the codes-only LR step must NOT take (round-4 advisor findings), run
+    against the residual-pass engine (r_from_codes off):
+    * m > n with activation_aware_LR=False and a non-unit diagonal H: the error weights are
+      not Y's column weights, so the LR error is the fused GEMM on res (alg.py:286-302) --
+      the codes-only step never writes res;
+    * an H that passes allclose(H, I) (optimized_eigh: unit eigenvalues, Y = res) but is not
+      exactly 1: the error keeps h, so again res must be written (wide and tall shapes);
+    * rank > 256: cq_codes_matmul takes r <= 256, larger ranks keep the residual pass."""
+    from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
+    m, n, rank, aware = {"tall_not_aware_h": (2048, 1024, 64, False), "wide_allclose_I": (1024, 2048, 64, True),
+                         "tall_allclose_I": (2048, 1024, 64, True), "rank_over_256": (1024, 2048, 272, True)}[case]
+    ep = EngineParams(Q_bits=2, L_bits=16, R_bits=16, rank=rank, iters=2, update_order=["Q", "LR"], sigma_reg=1e-8,
+                      activation_aware_LR=aware)
+    g = torch.Generator().manual_seed(len(case))
+    W = (torch.randn(1, m, n, generator=g) * 0.02).half().to(DEV)
+    if case == "tall_not_aware_h":
+        h = (torch.rand(n, generator=g) + 0.05).to(DEV)
+    elif case.endswith("allclose_I"):
+        h = (1.0 + 2e-6 * (torch.rand(n, generator=g) - 0.5)).to(DEV)
+    else:
+        h = None
+    outs = []
+    for codes in (True, False):
+        e = CalderaEngine(ep)
+        e.r_from_codes = codes
+        outs.append(e.run(W, h))
+        assert e.lr_steps_from_codes == 0, (case, codes, e.lr_steps_from_codes)
+    a, b = outs[0][0], outs[1][0]
+    for k in ("Q", "LR"):
+        assert all(math.isfinite(x) for x in a["errors"][k])
+        assert max(abs(x - y) for x, y in zip(a["errors"][k], b["errors"][k])) < 2e-6, (k, a["errors"], b["errors"])
+    # the LR errors against a direct fp64 evaluation of the final state's weighted error
+    Ws = a["W"].double().to(DEV)
+    E = Ws - a["Q"].double() - a["L"].double() @ a["R"].double()
+    hw = torch.ones(n, dtype=torch.float64, device=DEV) if h is None else h.double()
+    direct = math.sqrt(float((E * E * hw).sum() / (Ws * Ws * hw).sum()))
+    # (the kept iterate is the one with the smallest error after both update kinds ran)
+    assert min(abs(direct - x) for x in a["errors"]["LR"] + a["errors"]["Q"]) < 2e-6, (direct, a["errors"])
