@@ -486,6 +486,9 @@ def main():
     ap.add_argument("--emulate-rank", type=int, default=None, help="with --emulate-world: only this rank")
     ap.add_argument("--solver-tol-steps", type=str, default=None,
                     help="comma-separated solver tolerances of the first LR updates (then the default)")
+    ap.add_argument("--solver-refine-steps", type=str, default=None,
+                    help="per LR update, '+'-separated filter degrees of extra outer iterations after "
+                         "convergence, updates separated by ',' (e.g. '6' or '6+4,4')")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     ap.add_argument("--dry-run", action="store_true",
@@ -532,6 +535,8 @@ def main():
     h = None if h is None else h.to(dev)
     parts = max(1, args.streams or 1)
     tol_steps = tuple(float(x) for x in args.solver_tol_steps.split(",")) if args.solver_tol_steps else None
+    refine_steps = (tuple(tuple(int(d) for d in x.split("+") if d) for x in args.solver_refine_steps.split(","))
+                    if args.solver_refine_steps else None)
 
     def step():
         # the hot path: caldera() (alg.py:24-112) on B matrices resident in HBM, results
@@ -541,6 +546,8 @@ def main():
         engines = [CalderaEngine(ep) for _ in range(parts)]
         for e in engines:
             e.solver_tol_steps = tol_steps
+            if refine_steps is not None:
+                e.solver_refine_steps = refine_steps
         bnd = [B * i // parts for i in range(parts + 1)]
         outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], h, True) for i, e in enumerate(engines)], dev)
         # no reference cycles: the previous step's buffers must be freed as soon as the
@@ -727,7 +734,8 @@ def main():
     result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0), "stalled_matrices": st.get("stalls", 0),
                         "jacobi_unconverged": st.get("jacobi_unconverged", 0),
-                        "block_jacobi_readbacks": st.get("bj_readbacks", 0)}
+                        "block_jacobi_readbacks": st.get("bj_readbacks", 0),
+                        "refine_iters": st.get("refines", 0)}
     if rank == 0 and not args.no_parity:
         # parity of the LAST TIMED STEP's own results (rank 0: batch positions 0-3 = seeds 0-3)
         par = parity_of_timed_step(args.workload, decs, wl)

@@ -279,6 +279,8 @@ class CalderaEngine:
         # tolerances of the first LR updates (then solver_tol): the codes of the next Q update
         # are decided on the L R of the one before it (alg.py:262), see DESIGN.md §6
         self.solver_tol_steps = None
+        # per LR update: degrees of extra full outer iterations after the solver's test passed
+        self.solver_refine_steps = None
         self._lr_step = 0
         self.solver_p = solver_p
         self.filter_precision = filter_precision
@@ -435,6 +437,10 @@ class CalderaEngine:
             steps = self.solver_tol_steps or ()
             tol = steps[self._lr_step] if self._lr_step < len(steps) else self.solver_tol
             sv.tol = tol if weighted is False else tol * WEIGHTED_TOL_FACTOR
+            # refinement iterations after convergence for the first LR steps (solver_refine_steps[i]:
+            # filter degrees of the extra full outer iterations of the i-th LR update)
+            rs = self.solver_refine_steps or ()
+            sv.refine = tuple(rs[self._lr_step]) if self._lr_step < len(rs) else ()
         self._lr_step += 1
         y_split = None
         gram = None

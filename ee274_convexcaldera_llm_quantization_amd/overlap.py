@@ -39,10 +39,16 @@ def _part_streams(device, n):
     return lst[:n]
 
 
-def run_interleaved(gens, device):
-    """Round-robin over generators, each on its own stream of `device` (a fixed per-device
-    set).  Returns the list of their return values.  The caller's stream is joined before
-    and after."""
+def run_interleaved(gens, device, ready_first: bool = True):
+    """Drive generators, each on its own stream of `device` (a fixed per-device set).
+    Returns the list of their return values.  The caller's stream is joined before and after.
+
+    ready_first (default): a generator that yielded (it is about to read results back) gets an
+    event recorded behind the work it queued, and the host next resumes a generator whose
+    event has completed -- in round-robin order among those -- so it never blocks on one
+    stream while another stream's read-back is ready and its GPU queue runs dry.  Only when no
+    event has completed does it wait (spinning on the events).  False: plain round-robin,
+    each resume blocking on that generator's own stream."""
     if len(gens) == 1:
         return [run_to_end(gens[0])]
     caller = torch.cuda.current_stream(device)
@@ -52,14 +58,40 @@ def run_interleaved(gens, device):
     out = [None] * len(gens)
     live = list(range(len(gens)))
     try:
-        while live:
-            for i in list(live):
+        if not ready_first:
+            while live:
+                for i in list(live):
+                    torch.cuda.set_stream(streams[i])
+                    try:
+                        next(gens[i])
+                    except StopIteration as stop:
+                        out[i] = stop.value
+                        live.remove(i)
+        else:
+            events = [torch.cuda.Event() for _ in gens]
+            pending = [False] * len(gens)  # yielded, event recorded, not yet resumed
+            nxt = 0
+            while live:
+                # the first live generator at or after nxt (cyclically) that is ready: never
+                # started / resumed since its work completed
+                pick = None
+                order = sorted(live, key=lambda j: (j - nxt) % len(gens))
+                while pick is None:
+                    for j in order:
+                        if not pending[j] or events[j].query():
+                            pick = j
+                            break
+                i = pick
+                pending[i] = False
                 torch.cuda.set_stream(streams[i])
                 try:
                     next(gens[i])
+                    events[i].record(streams[i])
+                    pending[i] = True
                 except StopIteration as stop:
                     out[i] = stop.value
                     live.remove(i)
+                nxt = (i + 1) % len(gens)
     finally:
         torch.cuda.set_stream(caller)
     for s in streams:

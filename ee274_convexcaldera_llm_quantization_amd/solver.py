@@ -147,6 +147,7 @@ class SolverStats:
         self.jacobi_unconverged = 0  # Rayleigh-Ritz eigensolves that used all JACOBI_MAX_SWEEPS
         self.bj_readbacks = 0        # block-Jacobi stage read-backs (one int each)
         self.stalls = 0              # matrices whose solve ended at the products' precision floor
+        self.refines = 0             # refinement outer iterations run after convergence
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
@@ -155,7 +156,7 @@ class SolverStats:
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
                     jacobi_unconverged=self.jacobi_unconverged, bj_readbacks=self.bj_readbacks, stalls=self.stalls,
-                    max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks)
+                    max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks, refines=self.refines)
 
 
 class RankRSolver:
@@ -193,6 +194,7 @@ class RankRSolver:
         # errors ~1e-4 relative are ample for filter bounds): 243 -> 259 matrices/s
         self.jacobi_tol = jacobi_tol
         self.jacobi_tol_values = jacobi_tol_values
+        self.refine = ()   # extra full outer iterations after convergence (per call; engine.py)
         self.X = None      # warm-start Ritz block (B, k, p)
         self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
         self.stats = SolverStats()
@@ -570,6 +572,10 @@ class RankRSolver:
             Z = None
             degs = self.deg_warm
         self.stats.resid_hist = []
+        # refinement: after every matrix passed the test, `refine` more full outer iterations
+        # (filter of degree refine[i], CholQR2, Rayleigh-Ritz) for the whole batch -- set per
+        # call by the engine (its first LR steps decide the kept Q's codes)
+        refine = list(self.refine or ())
         used = []
         hist = []                               # per-matrix test values of the full iterations
         stalled = np.zeros(B, dtype=bool)
@@ -664,6 +670,11 @@ class RankRSolver:
                 stalled |= new_stall
             # converged (or stalled) matrices sit out the remaining filter products (X passes through)
             live = (resid > self.tol) & ~stalled
+            if not live.any() and refine:
+                degs = (refine.pop(0),)
+                n_outer = max(n_outer, self.cheap_cold if cold else self.cheap_warm)  # a full iteration
+                live = np.ones(B, dtype=bool)
+                self.stats.refines += 1
             self._active.copy_(torch.from_numpy(live.astype(np.int32)))
             if not live.any():
                 break

@@ -1,0 +1,171 @@
+// Probe (test infrastructure, not product code): what bounds the split-fp16 filter step
+// gemm_x3v_kernel<0> (cq_x3.hip xv_mainloop)?  Same tile (192 x 384 x 32, 12 waves of 96 x 64,
+// 16x16x32 MFMAs, 2-stage LDS-DMA ring, swizzled images) on the config-2 B = 256 shapes
+// (A = X^T halves 192 x 4096, B = G halves 4096 x 4096, K-blocked), random fp16 operands,
+// with parts of the work removed:
+//   mode 0  the product as in the engine (loads, fragment reads, 3 MFMAs per block and step)
+//   mode 1  G's LDS-DMA loads skipped on every odd K step (per-CU intake -1/3: what a
+//           symmetric-tile variant feeding G[I,J] to two products would save)
+//   mode 2  no loads after the first stage (intake 0: fragment reads + MFMAs + barriers)
+//   mode 3  loads as mode 0, fragments read from LDS once (no per-step fragment reads)
+//   mode 4  loads and fragment reads as mode 0, one MFMA per block and step instead of three
+// Results are numerically meaningless for modes 1-4 (stale LDS / reused fragments).
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -o probe_filter_intake probe_filter_intake.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x4v = __attribute__((ext_vector_type(4))) float;
+
+constexpr int BM = 192, BN = 384, BK = 32, THREADS = 768;
+constexpr int APART = BM * BK, BPART = BN * BK, STAGE = 2 * APART + 2 * BPART;
+constexpr size_t LDS_BYTES = (size_t)2 * STAGE * 2;
+constexpr int PER_WAVE = 6;
+
+__device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+__device__ __forceinline__ f16x8 frag(const _Float16* img, int row, int chunk) {
+    return *reinterpret_cast<const f16x8*>(img + row * BK + (chunk ^ swz(row)) * 8);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, const _Float16* Al, const _Float16* Bh,
+                                                           const _Float16* Bl, int64_t M, int64_t N, int64_t K,
+                                                           int64_t tiles_n, float* C) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    const int64_t b = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    const int64_t n0 = tn * BN;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid & 1, wn = wid >> 1, l16 = lane & 15, lq = lane >> 4;
+    uint32_t off[PER_WAVE];
+#pragma unroll
+    for (int u = 0; u < PER_WAVE; ++u) {
+        const int I = wid * PER_WAVE + u;
+        const bool isA = I < 24;
+        const int part = isA ? (I >= 12) : (I >= 48);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ swz(row);
+        int64_t gr = (isA ? 0 : n0) + row;
+        const int64_t lim = isA ? M : N;
+        gr = gr < lim ? gr : lim - 1;
+        off[u] = (uint32_t)(gr * 32 + c * 8);
+    }
+    auto issue = [&](int64_t k0, _Float16* st, bool withB) {
+#pragma unroll
+        for (int u = 0; u < PER_WAVE; ++u) {
+            const int I = wid * PER_WAVE + u;
+            const bool isA = I < 24;
+            if (!isA && !withB) continue;
+            const int part = isA ? (I >= 12) : (I >= 48);
+            const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+            const _Float16* base = isA ? (part ? Al : Ah) + b * M * K + (k0 >> 5) * (M * 32)
+                                       : (part ? Bl : Bh) + b * N * K + (k0 >> 5) * (N * 32);
+            _Float16* dst = st + (isA ? part * APART : 2 * APART + part * BPART) + (16 * sub) * BK;
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[u]),
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+    };
+    f32x4v acc[6][4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int64_t nt = K / BK;
+    issue(0, smem, true);
+    f16x8 bh[4], bl[4], ah[6], al[6];
+    for (int64_t t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < nt && MODE != 2) issue((t + 1) * BK, smem + ((t + 1) & 1) * STAGE, MODE != 1 || ((t + 1) & 1) == 0);
+        const _Float16* sA = smem + (t & 1) * STAGE;
+        const _Float16* sB = sA + 2 * APART;
+        if (MODE != 3 || t == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[j] = frag(sB, 64 * wn + 16 * j + l16, lq);
+                bl[j] = frag(sB + BPART, 64 * wn + 16 * j + l16, lq);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (MODE != 3 || t == 0) {
+                ah[i] = frag(sA, 96 * wm + 16 * i + l16, lq);
+                al[i] = frag(sA + APART, 96 * wm + 16 * i + l16, lq);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (MODE != 4) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = 96 * wm + 16 * i + l16, col = n0 + 64 * wn + 16 * j + 4 * lq;
+            if (col < N)
+                *reinterpret_cast<float4*>(C + (b * M + row) * N + col) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+}
+
+__global__ void fill_kernel(_Float16* p, int64_t n, uint32_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+        x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+        p[i] = (_Float16)(((float)(x & 0xffff) / 32768.f) - 1.f);
+    }
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+int main(int argc, char** argv) {
+    const int64_t B = argc > 1 ? atoll(argv[1]) : 256, M = 192, N = 4096, K = 4096;
+    const int64_t tiles_n = (N + BN - 1) / BN;
+    _Float16 *Ah, *Al, *Bh, *Bl;
+    float* C;
+    CK(hipMalloc(&Ah, B * M * K * 2)); CK(hipMalloc(&Al, B * M * K * 2));
+    CK(hipMalloc(&Bh, B * N * K * 2)); CK(hipMalloc(&Bl, B * N * K * 2));
+    CK(hipMalloc(&C, B * M * N * 4));
+    fill_kernel<<<4096, 256>>>(Ah, B * M * K, 1); fill_kernel<<<4096, 256>>>(Al, B * M * K, 2);
+    fill_kernel<<<4096, 256>>>(Bh, B * N * K, 3); fill_kernel<<<4096, 256>>>(Bl, B * N * K, 4);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const unsigned grid = (unsigned)(B * tiles_n);
+    const char* names[5] = {"full split product", "G loads skipped on odd K steps (intake -1/3)",
+                            "no loads after the first stage", "fragments read once (no per-step LDS reads)",
+                            "one MFMA per block and step (loads + reads as full)"};
+    for (int mode = 0; mode < 5; ++mode) {
+        auto launch = [&]() {
+            switch (mode) {
+                case 0: probe_kernel<0><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 1: probe_kernel<1><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 2: probe_kernel<2><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 3: probe_kernel<3><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                default: probe_kernel<4><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+            }
+        };
+        for (int w = 0; w < 3; ++w) launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 10;
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"mode\": %d, \"what\": \"%s\", \"batch\": %lld, \"ms_per_launch\": %.4f}\n", mode, names[mode],
+               (long long)B, ms / reps);
+        fflush(stdout);
+    }
+    return 0;
+}
