@@ -667,6 +667,11 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
     return hi, lo
 
 
+# automatic split-K of small-batch split-fp16 products (gemm_x3); False: every product in one
+# pass, so results do not depend on the batch a matrix is decomposed in (slower at small B)
+AUTO_SPLIT_K = True
+
+
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
@@ -720,9 +725,14 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         assert colw.dtype == torch.float32 and colw.is_contiguous() and colw.numel() == N
         g.colw = colw.data_ptr()
     # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
-    # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups
+    # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups.
+    # The chunked sum has another fp32 summation order than the one-pass product, so a matrix
+    # decomposed alone (or in a small batch) and the same matrix inside a large batch agree to
+    # the products' rounding, not bit for bit; AUTO_SPLIT_K = False pins one pass everywhere
     tiles = -(-N // 384) * -(-M // 192) * Bt
     splittable = not tri and sym_bound is None and C is not None and N % 4 == 0
+    if ksplit is None and not AUTO_SPLIT_K:
+        ksplit = 1
     if ksplit is None:  # automatic
         ks = min(Kd // 32 // 8, -(-512 // tiles)) if splittable and tiles < 256 and Kd >= 512 else 1
     else:
