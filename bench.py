@@ -489,6 +489,7 @@ def main():
     ap.add_argument("--solver-refine-steps", type=str, default=None,
                     help="per LR update, '+'-separated filter degrees of extra outer iterations after "
                          "convergence, updates separated by ',' (e.g. '6' or '6+4,4')")
+    ap.add_argument("--no-l-split", action="store_true", help="sparse Gram without the l-split ELL (A/B)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     ap.add_argument("--dry-run", action="store_true",
@@ -523,6 +524,9 @@ def main():
     from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     K.load()
+    if args.no_l_split:
+        from ee274_convexcaldera_llm_quantization_amd import sgram
+        sgram.L_SPLIT = False
     qp = make_params(wl)
     ep = EngineParams.from_caldera_params(qp)
     B = args.batch or wl["batch"]

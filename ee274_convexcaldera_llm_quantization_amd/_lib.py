@@ -127,12 +127,13 @@ _SIGS = {
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_size, c_vp]),
-    "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                               c_vp]),
-    "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp]),
+    "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_sgram_rows": (c_int, [c_i64]),
-    "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
-                              c_vp]),
+    "cq_sgram_split": (c_i64, [c_i64, c_i64]),
+    "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                              c_vp, c_vp]),
     "cq_sgram_combine": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp]),
     "cq_codes_transpose": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp]),
@@ -167,10 +168,15 @@ def load(path: str = LIB_PATH):
             raise RuntimeError(f"{path} is stale (built from other sources than csrc/ now holds, or "
                                f"unstamped): rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
+    other = path != LIB_PATH  # another build (A/B timing of a kernel change, tools/probes/build_rev.sh)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and other:
+            continue  # an older build: only the exports both know are declared
+        if fn is None:
+            raise RuntimeError(f"{path} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.cq_abi_version() != 2:
+    if lib.cq_abi_version() != 3 and not other:
         raise RuntimeError("libcaldera_hip.so ABI version mismatch")
     _lib = lib
     return lib
@@ -816,28 +822,38 @@ def absmax(X: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def sgram_split(k: int, L: int) -> int:
+    """The l-split point of the sparse-code Gram's ELL for a k x L code matrix (L: no split)."""
+    return int(load().cq_sgram_split(k, L))
+
+
 def sgram_count(packed, k, L, row_nnz, perm, slice_off, total, W=None, qscale=None, wcol=None, corr_ws=None,
-                corr_out=None):
+                corr_out=None, Lh=None, row_nnz1=None, slice_w1=None):
     """Sliced-ELL layout of the nonzero 2-bit codes per row (cq_sgram_count): packed (B, k*L/4).
     With W (B, k, L) fp16: corr_out (B,) fp64 = ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2
-    (wcol = ycol^2), corr_ws (B * k,) fp64 scratch."""
-    _require_hip(packed, row_nnz, perm, slice_off, total, W, qscale, wcol, corr_ws, corr_out)
+    (wcol = ycol^2), corr_ws (B * k,) fp64 scratch.  Lh < L (sgram_split): the l-split layout,
+    row_nnz1 (B * k,) int32 scratch, slice_w1 (B * ceil(k / 64),) int32 out."""
+    _require_hip(packed, row_nnz, perm, slice_off, total, W, qscale, wcol, corr_ws, corr_out, row_nnz1, slice_w1)
     B = total.numel()
-    assert row_nnz.numel() >= B * k and perm.numel() >= B * k and slice_off.numel() >= B * (-(-k // 64) + 1)
+    Lh = L if Lh is None else Lh
+    ns = -(-k // 64)
+    assert row_nnz.numel() >= B * k and perm.numel() >= B * k and slice_off.numel() >= B * (ns + 1)
+    assert Lh >= L or (row_nnz1.numel() >= B * k and slice_w1.numel() >= B * ns and slice_w1.dtype == torch.int32)
     if W is not None:
         assert W.dtype == torch.float16 and W.is_contiguous() and W.shape == (B, k, L)
         assert corr_ws.numel() >= B * k and corr_ws.dtype == torch.float64 and corr_out.numel() == B
-    _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total), _p(W),
-                                 _p(qscale), _p(wcol), _p(corr_ws), _p(corr_out), _stream(packed.device)),
-           "cq_sgram_count")
+    _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total), Lh,
+                                 _p(row_nnz1), _p(slice_w1), _p(W), _p(qscale), _p(wcol), _p(corr_ws), _p(corr_out),
+                                 _stream(packed.device)), "cq_sgram_count")
 
 
-def sgram_fill(packed, k, L, row_nnz, perm, slice_off, ell, stride):
-    _require_hip(packed, row_nnz, perm, slice_off, ell)
+def sgram_fill(packed, k, L, row_nnz, perm, slice_off, ell, stride, Lh=None, slice_w1=None):
+    _require_hip(packed, row_nnz, perm, slice_off, ell, slice_w1)
     B = slice_off.numel() // (-(-k // 64) + 1)
     assert ell.numel() >= B * stride
-    _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), stride, _p(ell),
-                                _stream(packed.device)), "cq_sgram_fill")
+    Lh = L if Lh is None else Lh
+    _check(load().cq_sgram_fill(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(slice_w1), Lh,
+                                stride, _p(ell), _stream(packed.device)), "cq_sgram_fill")
 
 
 def codes_transpose(packed, rows, cols, out=None):
@@ -901,15 +917,16 @@ def sgram_rows(L: int) -> int:
     return int(load().cq_sgram_rows(L))
 
 
-def sgram_spmm(W, packed, qscale, wcol, ell, perm, slice_off, stride, P):
+def sgram_spmm(W, packed, qscale, wcol, ell, perm, slice_off, stride, P, Lh=None, slice_w1=None):
     """P (B, k, k) = (W - (s/2) c) diag(wcol) c^T over the ELL codes (cq_sgram_spmm); wcol = the Gram's
-    column weights w = ycol^2 (None: 1)."""
-    _require_hip(W, packed, qscale, wcol, ell, perm, slice_off, P)
+    column weights w = ycol^2 (None: 1).  Lh / slice_w1: the l-split layout of sgram_count."""
+    _require_hip(W, packed, qscale, wcol, ell, perm, slice_off, P, slice_w1)
     B, k, L = W.shape
     assert W.dtype == torch.float16 and W.is_contiguous() and P.shape == (B, k, k) and P.is_contiguous()
     assert wcol is None or (wcol.numel() == L and wcol.dtype == torch.float32)
+    Lh = L if Lh is None else Lh
     _check(load().cq_sgram_spmm(CQ_F16, _p(W), _p(packed), _p(qscale), _p(wcol), B, k, L, _p(ell), _p(perm),
-                                _p(slice_off), stride, _p(P), _stream(W.device)), "cq_sgram_spmm")
+                                _p(slice_off), _p(slice_w1), Lh, stride, _p(P), _stream(W.device)), "cq_sgram_spmm")
 
 
 def sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, scale_out, inv_out, G32=None):

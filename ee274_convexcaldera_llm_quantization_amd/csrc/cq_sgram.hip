@@ -47,21 +47,24 @@ __device__ __forceinline__ int sg_u_of_bit(int p) { return 4 * (p >> 3) + ((6 - 
 __global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
                                                           int32_t* __restrict__ row_nnz, const _Float16* __restrict__ W,
                                                           const float* __restrict__ qscale,
-                                                          const float* __restrict__ wcol, double* __restrict__ row_corr) {
+                                                          const float* __restrict__ wcol, double* __restrict__ row_corr,
+                                                          int64_t Lh, int32_t* __restrict__ row_nnz1) {
     const int lane = threadIdx.x & 63;
     const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t b = blockIdx.y;
     if (j >= k) return;
     const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
     const int64_t nw = L / 16;
-    uint32_t cnt = 0;
+    uint32_t cnt = 0, cnt1 = 0;
     double corr = 0.0;
     const double s = W ? (double)qscale[b] : 0.0;
     const _Float16* Wr = W ? W + b * k * L + j * L : nullptr;
+    const int64_t nw1 = Lh / 16;   // words of the contraction's first part (l < Lh)
     for (int64_t w = lane; w < nw; w += 64) {
         const uint32_t word = row[w];
         uint32_t nz = sg_nz_mask(word);
         cnt += __popc(nz);
+        if (w < nw1) cnt1 += __popc(nz);
         if (W) {
             while (nz) {
                 const int p = __builtin_ctz(nz);
@@ -75,6 +78,10 @@ __global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restr
     }
     cnt = wave_sum(cnt);
     if (lane == 0) row_nnz[b * k + j] = (int32_t)cnt;
+    if (row_nnz1) {
+        cnt1 = wave_sum(cnt1);
+        if (lane == 0) row_nnz1[b * k + j] = (int32_t)cnt1;
+    }
     if (W) {
         corr = wave_sum(corr);
         if (lane == 0) row_corr[b * k + j] = corr;
@@ -90,7 +97,9 @@ constexpr int SG_BINS = 1024;
 __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __restrict__ row_nnz, int64_t k,
                                                            int32_t* __restrict__ perm, int64_t* __restrict__ slice_off,
                                                            int64_t* __restrict__ total, const double* __restrict__ row_corr,
-                                                           double* __restrict__ corr_out) {
+                                                           double* __restrict__ corr_out,
+                                                           const int32_t* __restrict__ row_nnz1,
+                                                           int32_t* __restrict__ slice_w1) {
     // stable counting sort, the four waves on four contiguous row ranges: per-wave bin counts,
     // bin starts (descending), each wave's base per bin = start + the counts of the waves before
     // it; then every wave places its rows in row order (ballots per distinct bin of a 64-row chunk)
@@ -158,10 +167,20 @@ __global__ __launch_bounds__(256) void sgram_slices_kernel(const int32_t* __rest
     __syncthreads();
     const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
     int64_t* so = slice_off + b * (ns + 1);
+    // l-split (row_nnz1 given): a slice holds its rows' first-part entries (l < Lh) in its
+    // first w1 64-entry rows and the second part's after them, each part padded to the
+    // slice's widest row of that part
+    const int32_t* nz1 = row_nnz1 ? row_nnz1 + b * k : nullptr;
     for (int64_t s = threadIdx.x; s < ns; s += blockDim.x) {
-        int32_t w = 0;
-        for (int64_t p = s * SG_SLICE; p < (s + 1) * SG_SLICE && p < k; ++p) w = max(w, nz[pm[p]]);
-        so[s + 1] = w;  // widths, prefixed below
+        int32_t w = 0, w1 = 0, w2 = 0;
+        for (int64_t p = s * SG_SLICE; p < (s + 1) * SG_SLICE && p < k; ++p) {
+            const int32_t c = nz[pm[p]], c1 = nz1 ? nz1[pm[p]] : c;
+            w = max(w, c);
+            w1 = max(w1, c1);
+            w2 = max(w2, c - c1);
+        }
+        so[s + 1] = nz1 ? w1 + w2 : w;  // widths, prefixed below
+        if (slice_w1) slice_w1[b * ns + s] = nz1 ? w1 : w;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -187,59 +206,78 @@ constexpr int SG_FILL_RW = 4;   // sorted positions (rows) per wave
 // (sg_fill_plain).  One wave per SG_FILL_RW rows: each row's nonzeros are compacted in l order
 // (one pass over its words) and stably counting-sorted by residue; the greedy order then runs
 // for the SG_FILL_RW rows at once, 16 lanes (one per residue) each.
-__device__ void sg_fill_plain(const uint32_t* __restrict__ row, int64_t nw, int q, int lane, uint32_t* out) {
-    int64_t base = 0;
+// l-split: entries with l < Lh go to the row's first part (out), the others to its second part
+// (out2: the slice's first-part width further on); Lh >= L: one part.  n1 = first-part entries
+__device__ void sg_fill_plain(const uint32_t* __restrict__ row, int64_t nw, int q, int lane, uint32_t* out,
+                              uint32_t* out2, int64_t nw1, int& n1) {
+    int64_t base = 0, base2 = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
     for (int i = 0; i < 16; ++i) {
         const int u = (q + i) & 15;
         for (int64_t w0 = 0; w0 < nw; w0 += 64) {
             const int64_t w = w0 + lane;
             const uint32_t f = w < nw ? sg_field(row[w], u) : 1u;
-            const bool nz = f != 1u;
-            const uint64_t msk = __ballot(nz);
-            if (nz) out[(base + __popcll(msk & ((1ull << lane) - 1ull))) * SG_SLICE] = (uint32_t)((16 * w + u) << 2) | f;
-            base += __popcll(msk);
+            const bool nz = f != 1u, first = w < nw1;
+            const uint64_t m1 = __ballot(nz && first), m2 = __ballot(nz && !first);
+            const uint32_t e = (uint32_t)((16 * w + u) << 2) | f;
+            if (nz && first) out[(base + __popcll(m1 & lt)) * SG_SLICE] = e;
+            if (nz && !first) out2[(base2 + __popcll(m2 & lt)) * SG_SLICE] = e;
+            base += __popcll(m1);
+            base2 += __popcll(m2);
         }
     }
+    n1 = (int)base;
 }
 
-__global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
+__global__ __launch_bounds__(256, 6) void sgram_fill_kernel(const uint8_t* __restrict__ packed, int64_t k, int64_t L,
                                                          const int32_t* __restrict__ row_nnz,
                                                          const int32_t* __restrict__ perm,
-                                                         const int64_t* __restrict__ slice_off, int64_t stride_ell,
-                                                         uint32_t* __restrict__ ell) {
+                                                         const int64_t* __restrict__ slice_off,
+                                                         const int32_t* __restrict__ slice_w1, int64_t Lh,
+                                                         int64_t stride_ell, uint32_t* __restrict__ ell) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wv) * SG_FILL_RW;
     const int64_t b = blockIdx.y;
     if (p0 >= k) return;
     __shared__ uint32_t nat[4][SG_FILL_CAP];
     __shared__ uint32_t grp[4][SG_FILL_RW][SG_FILL_CAP];
-    __shared__ int rsb[4][SG_FILL_RW][16], rcb[4][SG_FILL_RW][16];
+    __shared__ int rsb[4][SG_FILL_RW][2][16], rcb[4][SG_FILL_RW][2][16];
     const int64_t nw = L / 16;
+    const bool split = Lh < L;
+    const int64_t nw1 = split ? Lh / 16 : nw;
+    const int np = split ? 2 : 1;   // parts of the contraction
     const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
     const uint64_t lt = (1ull << lane) - 1ull;
-    int cntr[SG_FILL_RW];   // entries of each row taking the greedy order (0: none / plain)
+    int cntr[SG_FILL_RW];   // entries of each row (< 0: written in the plain order)
+    int c1r[SG_FILL_RW];    // of them in the first part (l < Lh)
     uint32_t* outr[SG_FILL_RW];
-    int64_t widr[SG_FILL_RW];
+    int64_t widr[SG_FILL_RW], w1r[SG_FILL_RW];
 #pragma unroll
     for (int r = 0; r < SG_FILL_RW; ++r) {
         cntr[r] = 0;
+        c1r[r] = 0;
         outr[r] = nullptr;
         widr[r] = 0;
+        w1r[r] = 0;
         const int64_t p = p0 + r;
         if (p >= k) continue;
         const int64_t j = perm[b * k + p];
         const int64_t s = p / SG_SLICE;
         const int64_t off = slice_off[b * (ns + 1) + s];
         widr[r] = slice_off[b * (ns + 1) + s + 1] - off;
+        w1r[r] = split ? slice_w1[b * ns + s] : widr[r];
         outr[r] = ell + b * stride_ell + off * SG_SLICE + (p % SG_SLICE);
         const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
         if (row_nnz[b * k + j] > SG_FILL_CAP) {
-            sg_fill_plain(row, nw, (int)(p & 15), lane, outr[r]);
+            int n1 = 0;
+            sg_fill_plain(row, nw, (int)(p & 15), lane, outr[r], outr[r] + w1r[r] * SG_SLICE, nw1, n1);
             cntr[r] = -row_nnz[b * k + j];   // written; padding below
+            c1r[r] = n1;
             continue;
         }
-        // the row's nonzeros in increasing l: per word, codes u = 0..15 in order
-        int cnt = 0;
+        // the row's nonzeros in increasing l: per word, codes u = 0..15 in order (the first
+        // part, l < Lh, is the prefix of c1 entries)
+        int cnt = 0, cnt1 = 0;
         for (int64_t w0 = 0; w0 < nw; w0 += 64) {
             const int64_t w = w0 + lane;
             const uint32_t word = w < nw ? row[w] : 0x55555555u;
@@ -254,6 +292,11 @@ __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restri
                 pre += __popcll(mk & lt) << bt;
                 tot += __popcll(mk) << bt;
             }
+            if (split) {
+                const int cf = w < nw1 ? c : 0;
+#pragma unroll
+                for (int bt = 0; bt < 5; ++bt) cnt1 += __popcll(__ballot((cf >> bt) & 1)) << bt;
+            }
             int pos = cnt + pre;
             while (um) {
                 const int u = __builtin_ctz(um);
@@ -262,83 +305,98 @@ __global__ __launch_bounds__(256) void sgram_fill_kernel(const uint8_t* __restri
             }
             cnt += tot;
         }
+        c1r[r] = split ? cnt1 : cnt;
         __builtin_amdgcn_wave_barrier();
-        // stable counting sort by residue (l mod 16): counts, starts, ranks (16 ballots a batch)
-        int cntu = 0;   // lane u < 16: entries of residue u
-        for (int i0 = 0; i0 < cnt; i0 += 64) {
-            const int i = i0 + lane;
-            const int res = i < cnt ? (int)((nat[wv][i] >> 2) & 15u) : 16;
+        // per part: stable counting sort by residue (l mod 16) into grp (part 1 after part 0):
+        // counts, starts, ranks (16 ballots a batch)
+        for (int h = 0; h < np; ++h) {
+            const int base = h ? c1r[r] : 0, cn = h ? cnt - c1r[r] : c1r[r];
+            int cntu = 0;   // lane u < 16: entries of residue u
+            for (int i0 = 0; i0 < cn; i0 += 64) {
+                const int i = i0 + lane;
+                const int res = i < cn ? (int)((nat[wv][base + i] >> 2) & 15u) : 16;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int m = __popcll(__ballot(res == u));
-                if (lane == u) cntu += m;
+                for (int u = 0; u < 16; ++u) {
+                    const int m = __popcll(__ballot(res == u));
+                    if (lane == u) cntu += m;
+                }
             }
-        }
-        int start = cntu;   // exclusive prefix over lanes 0..15
+            int start = cntu;   // exclusive prefix over lanes 0..15
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int v = __shfl_up(start, o, 64);
-            if ((lane & 15) >= o) start += v;
-        }
-        start -= cntu;
-        if (lane < 16) {
-            rsb[wv][r][lane] = start;
-            rcb[wv][r][lane] = cntu;
-        }
-        int seen = 0;   // lane u < 16: entries of residue u already placed
-        for (int i0 = 0; i0 < cnt; i0 += 64) {
-            const int i = i0 + lane;
-            const uint32_t e = i < cnt ? nat[wv][i] : 0u;
-            const int res = i < cnt ? (int)((e >> 2) & 15u) : 16;
-            int dst = 0;
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const uint64_t mk = __ballot(res == u);
-                const int su = __shfl(start + seen, u, 64);
-                if (res == u) dst = su + __popcll(mk & lt);
-                if (lane == u) seen += __popcll(mk);
+            for (int o = 1; o < 16; o <<= 1) {
+                const int v = __shfl_up(start, o, 64);
+                if ((lane & 15) >= o) start += v;
             }
-            if (i < cnt) grp[wv][r][dst] = e;
+            start -= cntu;
+            start += base;
+            if (lane < 16) {
+                rsb[wv][r][h][lane] = start;
+                rcb[wv][r][h][lane] = cntu;
+            }
+            int seen = 0;   // lane u < 16: entries of residue u already placed
+            for (int i0 = 0; i0 < cn; i0 += 64) {
+                const int i = i0 + lane;
+                const uint32_t e = i < cn ? nat[wv][base + i] : 0u;
+                const int res = i < cn ? (int)((e >> 2) & 15u) : 16;
+                int dst = 0;
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const uint64_t mk = __ballot(res == u);
+                    const int su = __shfl(start + seen, u, 64);
+                    if (res == u) dst = su + __popcll(mk & lt);
+                    if (lane == u) seen += __popcll(mk);
+                }
+                if (i < cn) grp[wv][r][dst] = e;
+            }
         }
         cntr[r] = cnt;
         __builtin_amdgcn_wave_barrier();
     }
-    // greedy order, the SG_FILL_RW rows at once: lane = 16 g + u (row g, residue u)
+    // greedy order per part, the SG_FILL_RW rows at once: lane = 16 g + u (row g, residue u)
     const int g = lane >> 4, u = lane & 15;
-    int myc = 0, mys = 0, mycnt = 0;
-    uint32_t* myout = nullptr;
-    int64_t mywid = 0;
-#pragma unroll
-    for (int r = 0; r < SG_FILL_RW; ++r)
-        if (g == r) { mycnt = cntr[r]; myout = outr[r]; mywid = widr[r]; }
-    if (mycnt > 0) {
-        myc = rcb[wv][g][u];
-        mys = rsb[wv][g][u];
-    }
-    int T = 0;
-#pragma unroll
-    for (int r = 0; r < SG_FILL_RW; ++r) T = cntr[r] > T ? cntr[r] : T;
     const int q = (int)((p0 + g) & 15);
-    int taken = 0;
-    for (int t = 0; t < T; ++t) {
-        const int d = (q + t) & 15;
-        const int remd = __shfl(myc - taken, 16 * g + d, 64);
-        int key = ((myc - taken) << 4) | (15 - u);
+    for (int h = 0; h < np; ++h) {
+        int myc = 0, mys = 0, mycnt = 0;
+        uint32_t* myout = nullptr;
+        int T = 0;
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) key = max(key, __shfl_xor(key, o, 64));
-        const int sel = remd > 0 ? d : 15 - (key & 15);
-        const int at = __shfl(mys + taken, 16 * g + sel, 64);
-        if (t < mycnt) {
-            if (u == 0) myout[(int64_t)t * SG_SLICE] = grp[wv][g][at];
-            if (u == sel) ++taken;
+        for (int r = 0; r < SG_FILL_RW; ++r) {
+            const int cn = cntr[r] <= 0 ? 0 : (h ? cntr[r] - c1r[r] : c1r[r]);
+            if (g == r) {
+                mycnt = cn;
+                myout = outr[r] ? outr[r] + (h ? w1r[r] * SG_SLICE : 0) : nullptr;
+            }
+            T = cn > T ? cn : T;
+        }
+        if (mycnt > 0) {
+            myc = rcb[wv][g][h][u];
+            mys = rsb[wv][g][h][u];
+        }
+        int taken = 0;
+        for (int t = 0; t < T; ++t) {
+            const int d = (q + t) & 15;
+            const int remd = __shfl(myc - taken, 16 * g + d, 64);
+            int key = ((myc - taken) << 4) | (15 - u);
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) key = max(key, __shfl_xor(key, o, 64));
+            const int sel = remd > 0 ? d : 15 - (key & 15);
+            const int at = __shfl(mys + taken, 16 * g + sel, 64);
+            if (t < mycnt) {
+                if (u == 0) myout[(int64_t)t * SG_SLICE] = grp[wv][g][at];
+                if (u == sel) ++taken;
+            }
         }
     }
-    // padding: l = 0, code 0
+    // padding (code 0): the first part at l = 0, the second at l = Lh (inside its staged slab)
 #pragma unroll
     for (int r = 0; r < SG_FILL_RW; ++r) {
         if (!outr[r]) continue;
-        const int64_t from = cntr[r] < 0 ? -cntr[r] : cntr[r];
-        for (int64_t t = from + lane; t < widr[r]; t += 64) outr[r][t * SG_SLICE] = 1u;
+        const int tot = cntr[r] < 0 ? -cntr[r] : cntr[r];
+        for (int64_t t = c1r[r] + lane; t < w1r[r]; t += 64) outr[r][t * SG_SLICE] = 1u;
+        if (split) {
+            const uint32_t pad = (uint32_t)(Lh << 2) | 1u;
+            for (int64_t t = w1r[r] + (tot - c1r[r]) + lane; t < widr[r]; t += 64) outr[r][t * SG_SLICE] = pad;
+        }
     }
 }
 
@@ -357,13 +415,13 @@ __device__ __forceinline__ int64_t sg_slab_at(int64_t L, int64_t l, int r) {
 
 template <int R>
 __device__ __forceinline__ void sg_slice(const float* __restrict__ slab, int64_t L, const uint32_t* __restrict__ ep,
-                                         int64_t width, float (&acc)[R]) {
+                                         int64_t width, float (&acc)[R], int64_t lbase = 0) {
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
     constexpr int PL = R < 4 ? R : 4;
     auto fma_entry = [&](uint32_t e) {
         const float c = (float)((int)(e & 3u) - 1);
-        const int64_t l = e >> 2;
+        const int64_t l = (int64_t)(e >> 2) - lbase;   // the slab holds l in [lbase, lbase + L)
 #pragma unroll
         for (int pl = 0; pl < R / PL; ++pl) {
             const float* v = slab + (int64_t)pl * PL * L + l * PL;
@@ -396,26 +454,29 @@ __device__ __forceinline__ void sg_slice(const float* __restrict__ slab, int64_t
 // wv + 16, ...; with NSW > 0 (ceil(ns / 16) <= NSW) it keeps all of its results in registers and
 // the R output rows are assembled in LDS (the slab's space, k <= L, j-major) and stored over j
 // -- the sorted slices' rows are scattered over j, so direct stores would be 4-byte scatters
-template <int R, int NSW>
+template <int R, int NSW, bool SPLIT = false>
 __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __restrict__ W, const uint8_t* __restrict__ packed,
                                                          const float* __restrict__ qscale, const float* __restrict__ wcol,
                                                          int64_t k, int64_t L, const uint32_t* __restrict__ ell,
                                                          const int32_t* __restrict__ perm,
-                                                         const int64_t* __restrict__ slice_off, int64_t stride_ell,
-                                                         float* __restrict__ P) {
+                                                         const int64_t* __restrict__ slice_off,
+                                                         const int32_t* __restrict__ slice_w1, int64_t Lh,
+                                                         int64_t stride_ell, float* __restrict__ P) {
     extern __shared__ __attribute__((aligned(16))) float slab[];
     const int64_t b = blockIdx.y;
     const int64_t i0 = (int64_t)blockIdx.x * R;
     const float hs = 0.5f * qscale[b];
     const int64_t KL = k * L;
-    // stage: per plane, a thread loads 8 consecutive l of each of its PL rows (16-byte W and
-    // 2-byte code loads) and stores the 8 l-entries (PL floats each) in an order rotated by its
-    // lane (t mod 8): the 8 lanes of a ds_write_b128 group then hit 8 different bank groups
-    // instead of one (the entries of consecutive lanes lie 128 bytes apart)
+    const int64_t Ls = SPLIT ? Lh : L;   // l-values a slab holds (SPLIT: each part of the contraction)
+    // stage E for l in [la, lb): per plane, a thread loads 8 consecutive l of each of its PL rows
+    // (16-byte W and 2-byte code loads) and stores the 8 l-entries (PL floats each) in an order
+    // rotated by its lane (t mod 8): the 8 lanes of a ds_write_b128 group then hit 8 different
+    // bank groups instead of one (the entries of consecutive lanes lie 128 bytes apart)
     constexpr int PL = R < 4 ? R : 4;
+    auto stage = [&](int64_t la, int64_t lb) {
 #pragma unroll
     for (int pl = 0; pl < R / PL; ++pl) {
-        for (int64_t l0 = (int64_t)threadIdx.x * 8; l0 < L; l0 += SG_THREADS * 8) {
+        for (int64_t l0 = la + (int64_t)threadIdx.x * 8; l0 < lb; l0 += SG_THREADS * 8) {
             float e[PL][8];
 #pragma unroll
             for (int r = 0; r < PL; ++r) {
@@ -453,12 +514,14 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                float* dst = slab + (int64_t)pl * PL * L + (l0 + ((u + rot) & 7)) * PL;
+                float* dst = slab + (int64_t)pl * PL * Ls + (l0 - la + ((u + rot) & 7)) * PL;
                 if constexpr (PL == 4) *reinterpret_cast<float4*>(dst) = make_float4(e[0][u], e[1][u], e[2][u], e[3][u]);
                 else *reinterpret_cast<float2*>(dst) = make_float2(e[0][u], e[1][u]);
             }
         }
     }
+    };
+    stage(0, SPLIT ? Lh : L);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t ns = (k + SG_SLICE - 1) / SG_SLICE;
@@ -509,15 +572,35 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
         }
     } else if constexpr (NSW < 0) {
         // output block of its own after the slab (k x R, j-major): each slice's results go to
-        // LDS as soon as they are done (nothing held in registers), then stored over j
-        float* outb = slab + (int64_t)R * L;
+        // LDS as soon as they are done (nothing held in registers), then stored over j.
+        // SPLIT (l-split ELL, the 11008-long contractions): R = 4 rows of E fit the LDS only
+        // half a contraction at a time, so each slice's first part (l < Lh) is swept against
+        // the slab of l in [0, Lh), then the slab is restaged with l in [Lh, L) and the second
+        // parts are added: every workgroup still reads the ELL once, but half as many do it
+        // as with R = 2 rows over the whole contraction
+        float* outb = slab + (int64_t)R * Ls;
+        const int32_t* w1 = SPLIT ? slice_w1 + b * ns : nullptr;
         for (int64_t s = wv; s < ns; s += SG_WAVES) {
             float acc[R];
-            sg_slice<R>(slab, L, eb + so[s] * SG_SLICE, so[s + 1] - so[s], acc);
+            sg_slice<R>(slab, Ls, eb + so[s] * SG_SLICE, SPLIT ? w1[s] : so[s + 1] - so[s], acc);
             const int64_t p = s * SG_SLICE + lane;
             if (p < k) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) outb[(int64_t)pm[p] * R + r] = acc[r];
+            }
+        }
+        if constexpr (SPLIT) {
+            __syncthreads();   // every wave is done with the first part's slab
+            stage(Lh, L);
+            __syncthreads();
+            for (int64_t s = wv; s < ns; s += SG_WAVES) {
+                float acc[R];
+                sg_slice<R>(slab, Ls, eb + (so[s] + w1[s]) * SG_SLICE, so[s + 1] - so[s] - w1[s], acc, Lh);
+                const int64_t p = s * SG_SLICE + lane;
+                if (p < k) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) outb[(int64_t)pm[p] * R + r] += acc[r];
+                }
             }
         }
         __syncthreads();
@@ -950,28 +1033,35 @@ int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t col
 }
 
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
-                   int32_t* perm, int64_t* slice_off, int64_t* total, const void* W, const float* qscale,
-                   const float* wcol, double* corr_ws, double* corr_out, void* stream) {
+                   int32_t* perm, int64_t* slice_off, int64_t* total, int64_t Lh, int32_t* row_nnz1,
+                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, double* corr_ws,
+                   double* corr_out, void* stream) {
     CQ_REQUIRE(packed && row_nnz && perm && slice_off && total, "cq_sgram_count: null argument");
     CQ_REQUIRE(bits == 2, "cq_sgram_count: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0, "cq_sgram_count: bad shape");
     CQ_REQUIRE(!W || (qscale && corr_ws && corr_out), "cq_sgram_count: the norm correction needs qscale, corr_ws, corr_out");
+    CQ_REQUIRE(Lh >= L || (Lh > 0 && Lh % 64 == 0 && 2 * Lh >= L && row_nnz1 && slice_w1),
+               "cq_sgram_count: an l-split needs Lh % 64 == 0, Lh >= L / 2, row_nnz1 and slice_w1");
+    const bool split = Lh < L;
     hipStream_t s = as_stream(stream);
     sgram_count_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, s>>>(
-        packed, k, L, row_nnz, reinterpret_cast<const _Float16*>(W), qscale, wcol, corr_ws);
+        packed, k, L, row_nnz, reinterpret_cast<const _Float16*>(W), qscale, wcol, corr_ws, split ? Lh : L,
+        split ? row_nnz1 : nullptr);
     sgram_slices_kernel<<<(unsigned)batch, 256, 0, s>>>(row_nnz, k, perm, slice_off, total, W ? corr_ws : nullptr,
-                                                        corr_out);
+                                                        corr_out, split ? row_nnz1 : nullptr, slice_w1);
     return check_launch("cq_sgram_count");
 }
 
 int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
-                  const int32_t* perm, const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream) {
+                  const int32_t* perm, const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh,
+                  int64_t stride_ell, uint32_t* ell, void* stream) {
     CQ_REQUIRE(packed && row_nnz && perm && slice_off && ell, "cq_sgram_fill: null argument");
     CQ_REQUIRE(bits == 2, "cq_sgram_fill: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0 && L < (1ll << 29),
                "cq_sgram_fill: bad shape");
+    CQ_REQUIRE(Lh >= L || (Lh > 0 && Lh % 64 == 0 && 2 * Lh >= L && slice_w1), "cq_sgram_fill: bad l-split");
     sgram_fill_kernel<<<dim3((unsigned)ceil_div(k, 4 * SG_FILL_RW), (unsigned)batch), 256, 0, as_stream(stream)>>>(
-        packed, k, L, row_nnz, perm, slice_off, stride_ell, ell);
+        packed, k, L, row_nnz, perm, slice_off, slice_w1, Lh < L ? Lh : L, stride_ell, ell);
     return check_launch("cq_sgram_fill");
 }
 
@@ -981,18 +1071,34 @@ int cq_sgram_rows(int64_t L) {
     return 0;
 }
 
+int64_t cq_sgram_split(int64_t k, int64_t L) {
+    // two rows of E fit the LDS but not four: stage four rows half a contraction at a time when
+    // the half-slab and the k x 4 output block fit (config 3's and config 4's 11008 contractions)
+    if (cq_sgram_rows(L) != 2 || L % 64) return L;
+    const int64_t Lh = ceil_div(L / 2, (int64_t)64) * 64;
+    return ((size_t)Lh * 4 + (size_t)k * 4) * sizeof(float) <= 150 * 1024 ? Lh : L;
+}
+
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
                   int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
-                  const int64_t* slice_off, int64_t stride_ell, float* P, void* stream) {
+                  const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh, int64_t stride_ell, float* P,
+                  void* stream) {
     CQ_REQUIRE(W && packed && qscale && ell && perm && slice_off && P, "cq_sgram_spmm: null argument");
     CQ_REQUIRE(dtype == CQ_F16, "cq_sgram_spmm: fp16 W only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L % 64 == 0, "cq_sgram_spmm: bad shape");
+    hipStream_t s = as_stream(stream);
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
+    if (Lh < L) {   // l-split ELL (cq_sgram_split): R = 4 rows, two slabs of Lh values
+        CQ_REQUIRE(Lh == cq_sgram_split(k, L) && slice_w1, "cq_sgram_spmm: Lh must be cq_sgram_split(k, L)");
+        const size_t lds = ((size_t)Lh * 4 + (size_t)k * 4) * sizeof(float);
+        sgram_spmm_kernel<4, -1, true><<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), SG_THREADS, lds, s>>>(
+            Wh, packed, qscale, wcol, k, L, ell, perm, slice_off, slice_w1, Lh, stride_ell, P);
+        return check_launch("cq_sgram_spmm");
+    }
     const int R = cq_sgram_rows(L);
     CQ_REQUIRE(R > 0, "cq_sgram_spmm: rows of %lld values do not fit the LDS", (long long)L);
     size_t lds = (size_t)L * R * sizeof(float);
-    hipStream_t s = as_stream(stream);
     const dim3 grid((unsigned)ceil_div(k, R), (unsigned)batch);
-    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const int64_t nsw = ceil_div(ceil_div(k, SG_SLICE), SG_WAVES);  // slices per wave
     // the register-held form needs k <= L (the output block reuses the slab's LDS) and fits the
     // 128-VGPR budget of 16 waves per CU only at R = 8 (4 slices per wave): at R = 4 / 2 its 8 /
@@ -1002,7 +1108,7 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     const bool ldsout = !held && R < 8 && lds + (size_t)k * R * sizeof(float) <= 150 * 1024;
     if (ldsout) lds += (size_t)k * R * sizeof(float);
 #define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
-                                                                             perm, slice_off, stride_ell, P)
+                                                                             perm, slice_off, nullptr, L, stride_ell, P)
     if (R == 8) {
         if (held) CQ_SP(8, 4); else CQ_SP(8, 0);
     } else if (R == 4) {

@@ -51,6 +51,19 @@ def run_interleaved(gens, device, ready_first: bool = True):
     each resume blocking on that generator's own stream."""
     if len(gens) == 1:
         return [run_to_end(gens[0])]
+    # concurrent batches fill the chip together: a small batch's split-fp16 products need no
+    # split-K here (_lib.AUTO_SPLIT_K; its partial sums and epilogue launches only add traffic:
+    # config-4 rank share 0.159 -> 0.136 s, profiles/r05f_share*.log)
+    from . import _lib
+    auto_split = _lib.AUTO_SPLIT_K
+    _lib.AUTO_SPLIT_K = False
+    try:
+        return _run_interleaved(gens, device, ready_first)
+    finally:
+        _lib.AUTO_SPLIT_K = auto_split
+
+
+def _run_interleaved(gens, device, ready_first):
     caller = torch.cuda.current_stream(device)
     streams = _part_streams(device, len(gens))
     for s in streams:

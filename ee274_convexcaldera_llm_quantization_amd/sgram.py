@@ -18,6 +18,9 @@ import torch
 from . import _lib as K
 from . import scratch
 
+# l-split ELL for the long contractions (cq_sgram_split); False: the unsplit R = 2 layout (A/B)
+L_SPLIT = True
+
 # above this fraction of nonzero codes (padded sliced-ELL entries / (m n)) the dense Gram is
 # cheaper (the sparse product's cost grows with the entries, the dense Gram's does not)
 MAX_DENSITY = 0.03
@@ -78,6 +81,11 @@ class SparseGram:
         self.perm = torch.empty(B * m, dtype=torch.int32, device=dev)
         self.slice_off = torch.empty(B * (self.ns + 1), dtype=torch.int64, device=dev)
         self.total = torch.empty(B, dtype=torch.int64, device=dev)
+        # l-split ELL for the long contractions (cq_sgram_split: n = 11008 at k = 4096): four rows
+        # of E staged half a contraction at a time instead of two over all of it
+        self.Lh = K.sgram_split(m, n) if L_SPLIT else n
+        self.row_nnz1 = torch.empty(B * m, dtype=torch.int32, device=dev) if self.Lh < n else None
+        self.slice_w1 = torch.empty(B * self.ns, dtype=torch.int32, device=dev) if self.Lh < n else None
         self.density = None
         self.stats = {"sparse": 0, "dense": 0}
         self._corr_ws = None
@@ -93,7 +101,8 @@ class SparseGram:
                 self._corr_ws = torch.empty(self.B * self.m, dtype=torch.float64, device=W.device)
             self.ysq_corr = torch.empty(self.B, dtype=torch.float64, device=W.device)
             corr = dict(W=W, qscale=qscale, wcol=wcol, corr_ws=self._corr_ws, corr_out=self.ysq_corr)
-        K.sgram_count(packed, self.m, self.n, self.row_nnz, self.perm, self.slice_off, self.total, **corr)
+        K.sgram_count(packed, self.m, self.n, self.row_nnz, self.perm, self.slice_off, self.total, Lh=self.Lh,
+                      row_nnz1=self.row_nnz1, slice_w1=self.slice_w1, **corr)
         mx = int(self.total.max().item())
         self.density = mx / float(self.m * self.n)
         return mx
@@ -115,9 +124,11 @@ class SparseGram:
         # fixed capacity per matrix (a stable scratch shape across LR steps)
         stride = -(-int(max(MAX_DENSITY, self.density) * m * n) // 4096) * 4096
         ell = scratch.get("sgram.ell", (B * stride,), torch.int32, dev)
-        K.sgram_fill(packed, m, n, self.row_nnz, self.perm, self.slice_off, ell, stride)
+        K.sgram_fill(packed, m, n, self.row_nnz, self.perm, self.slice_off, ell, stride, Lh=self.Lh,
+                     slice_w1=self.slice_w1)
         P = scratch.get("sgram.P", (B, m, m), torch.float32, dev)
-        K.sgram_spmm(Ws, packed, qscale, w, ell, self.perm, self.slice_off, stride, P)
+        K.sgram_spmm(Ws, packed, qscale, w, ell, self.perm, self.slice_off, stride, P, Lh=self.Lh,
+                     slice_w1=self.slice_w1)
         K.sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, gscale, ginv, G32=G32)
         self.stats["sparse"] += 1
         return True

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CQ_ABI_VERSION 2
+#define CQ_ABI_VERSION 3
 
 #define CQ_OK 0
 #define CQ_EINVAL (-1)   /* bad argument (shape, bits, null pointer) */
@@ -369,25 +369,36 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  *                     nonzero codes of wcol[l] (s^2 - 2 s c W[j, l]) (fp64, s = qscale[b], wcol NULL
  *                     = 1; corr_ws: batch x k doubles): ||(W - s c) diag(ycol)||^2 - ||W diag(ycol)||^2
  *                     for wcol = ycol^2, the ||Y||_F^2 of alg.py:211 without a pass over Y;
+ *                     l-split (Lh < L, from cq_sgram_split): also row_nnz1 (batch x k, the
+ *                     entries with l < Lh) and slice_w1 (batch x ceil(k/64), int32): a slice holds
+ *                     its rows' first-part entries in its first slice_w1 64-entry rows, the rest
+ *                     after them (each part padded to its widest row); Lh >= L: one part
+ *                     (row_nnz1 / slice_w1 may be NULL);
  *   cq_sgram_fill:    the ELL entries (uint32: l << 2 | code + 1) of matrix b at ell + b stride_ell
- *                     (row_nnz, perm, slice_off from cq_sgram_count);
+ *                     (row_nnz, perm, slice_off, slice_w1, Lh as given to cq_sgram_count);
  *   cq_sgram_rows:    rows of E a workgroup stages for contraction length L (0: too long);
+ *   cq_sgram_split:   the l-split point Lh for k x L (L: no split): where two rows of E fit the
+ *                     LDS but four do not, four are staged half a contraction at a time;
  *   cq_sgram_spmm:    P (batch x k x k fp32) from W (fp16, batch x k x L), the codes, qscale[b] = s
- *                     and wcol (L, may be NULL = 1);
+ *                     and wcol (L, may be NULL = 1), over the ELL of cq_sgram_fill (same Lh);
  *   cq_sgram_combine: G = A - s (P + P^T) with A (batch x k x k fp32, upper triangle read) =
  *                     W diag(w) W^T, written as the K-blocked split halves Gh/Gl with
  *                     cq_gemm_x3 sym_out's scale rule (scale_out[b] from bound[b] >= max|G|,
  *                     inv_out[b] = 1 / (scale_out[b] out_scale)); G32 (full fp32 G) optional.
  * k % 64 == 0, L % 64 == 0. */
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
-                   int32_t* perm, int64_t* slice_off, int64_t* total, const void* W, const float* qscale,
-                   const float* wcol, double* corr_ws, double* corr_out, void* stream);
+                   int32_t* perm, int64_t* slice_off, int64_t* total, int64_t Lh, int32_t* row_nnz1,
+                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, double* corr_ws,
+                   double* corr_out, void* stream);
 int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
-                  const int32_t* perm, const int64_t* slice_off, int64_t stride_ell, uint32_t* ell, void* stream);
+                  const int32_t* perm, const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh,
+                  int64_t stride_ell, uint32_t* ell, void* stream);
 int cq_sgram_rows(int64_t L);
+int64_t cq_sgram_split(int64_t k, int64_t L);
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
                   int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
-                  const int64_t* slice_off, int64_t stride_ell, float* P, void* stream);
+                  const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh, int64_t stride_ell, float* P,
+                  void* stream);
 int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_t batch, int64_t k,
                      const double* bound, float out_scale, uint16_t* Gh, uint16_t* Gl, float* scale_out,
                      float* inv_out, float* G32, void* stream);

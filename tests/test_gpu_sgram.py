@@ -21,7 +21,8 @@ def _unblock(h, k):
 
 
 @pytest.mark.parametrize("B,m,n,weighted", [(3, 256, 512, False), (2, 512, 512, True), (2, 256, 4608, False),
-                                            (2, 128, 6400, True), (2, 64, 12800, False)])
+                                            (2, 128, 6400, True), (2, 64, 12800, False), (2, 256, 11008, False),
+                                            (1, 4096, 11008, True)])
 def test_sparse_gram_matches_fp64(B, m, n, weighted):
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     from ee274_convexcaldera_llm_quantization_amd import sgram
@@ -95,16 +96,17 @@ def test_sparse_gram_matches_fp64(B, m, n, weighted):
     assert err32 < 1.5 * errd + 2e-7 and errs < 1.5 * errd + 2e-7
 
 
-def _expected_ell_rows(codes, perm, row_nnz):
+def _expected_ell_rows(codes, perm, row_nnz, lo=0, hi=None):
     """The sliced-ELL entry order (cq_sgram.hip, sgram_fill_kernel) restated on the host: per
-    sorted position p (row j = perm[p]) the nonzero codes (l << 2 | code + 1), grouped by
-    residue l mod 16 in increasing l; rows of at most 256 entries take residue (p + t) mod 16 at
-    step t while it has entries left, else the residue with the most left (ties: the smaller);
-    longer rows the residues in the order p, p + 1, ... (mod 16)."""
+    sorted position p (row j = perm[p]) the nonzero codes (l << 2 | code + 1) with l in [lo, hi)
+    (one part of an l-split row; default all), grouped by residue l mod 16 in increasing l;
+    rows of at most 256 entries in total take residue (p + t) mod 16 at step t while it has
+    entries left, else the residue with the most left (ties: the smaller); longer rows the
+    residues in the order p, p + 1, ... (mod 16)."""
     out = []
     for p, j in enumerate(perm):
         row = codes[j]
-        ls = np.nonzero(row != 0)[0]
+        ls = [l for l in np.nonzero(row != 0)[0] if lo <= l < (len(row) if hi is None else hi)]
         ent = {u: [int((l << 2) | (row[l] + 1)) for l in ls if l % 16 == u] for u in range(16)}
         q = p & 15
         seq = []
@@ -125,11 +127,14 @@ def _expected_ell_rows(codes, perm, row_nnz):
     return out
 
 
-@pytest.mark.parametrize("k,L,dens", [(200, 1024, 0.03), (64, 4096, 0.004)])
+@pytest.mark.parametrize("k,L,dens", [(200, 1024, 0.03), (64, 4096, 0.004), (200, 10240, 0.01), (128, 11008, 0.012)])
 def test_sparse_gram_ell_order(k, L, dens):
     """The ELL fill (sgram_count + sgram_fill) against the host restatement of its entry order:
     counts, row sort, per-row entry sequence (bank-group rotation, greedy fallback, rows past
-    256 entries in residue-rotated order) and padding, entry for entry."""
+    256 entries in residue-rotated order) and padding, entry for entry.  Contractions past
+    9600 (L = 10240, 11008) take the l-split layout (cq_sgram_split): per slice the first parts
+    (l < Lh) in its first slice_w1 rows, padded with l = 0, then the second parts padded with
+    l = Lh, each part ordered as above on its own entries."""
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     rng = np.random.default_rng(k + L)
     B = 2
@@ -145,24 +150,36 @@ def test_sparse_gram_ell_order(k, L, dens):
     perm = torch.empty(B * k, dtype=torch.int32, device=dev)
     slice_off = torch.empty(B * (ns + 1), dtype=torch.int64, device=dev)
     total = torch.empty(B, dtype=torch.int64, device=dev)
-    K.sgram_count(pk, k, L, row_nnz, perm, slice_off, total)
+    Lh = K.sgram_split(k, L)
+    assert (Lh < L) == (L > 9600)
+    nz1 = torch.empty(B * k, dtype=torch.int32, device=dev)
+    sw1 = torch.empty(B * ns, dtype=torch.int32, device=dev)
+    K.sgram_count(pk, k, L, row_nnz, perm, slice_off, total, Lh=Lh, row_nnz1=nz1, slice_w1=sw1)
     stride = int(total.max().item()) + 64
     ell = torch.full((B * stride,), -7, dtype=torch.int32, device=dev)
-    K.sgram_fill(pk, k, L, row_nnz, perm, slice_off, ell, stride)
+    K.sgram_fill(pk, k, L, row_nnz, perm, slice_off, ell, stride, Lh=Lh, slice_w1=sw1)
     torch.cuda.synchronize()
     nz, pm, so = row_nnz.cpu().numpy().reshape(B, k), perm.cpu().numpy().reshape(B, k), slice_off.cpu().numpy()
+    w1 = sw1.cpu().numpy().reshape(B, ns)
     el = ell.cpu().numpy().view(np.uint32).reshape(B, stride)
     for b in range(B):
         assert (nz[b] == (codes[b] != 0).sum(1)).all()
         assert sorted(pm[b].tolist()) == list(range(k))
-        exp = _expected_ell_rows(codes[b], pm[b], nz[b])
+        parts = [(0, Lh, 1)] + ([(Lh, L, (Lh << 2) | 1)] if Lh < L else [])
+        exps = [_expected_ell_rows(codes[b], pm[b], nz[b], lo, hi) for lo, hi, _ in parts]
         sob = so[b * (ns + 1):(b + 1) * (ns + 1)]
         for p in range(k):
             s = p // 64
             width = int(sob[s + 1] - sob[s])
-            got = [int(el[b, (sob[s] + t) * 64 + p % 64]) for t in range(width)]
-            want = exp[p] + [1] * (width - len(exp[p]))
-            assert got == want, (b, p, got[:8], want[:8])
+            cut = int(w1[b, s]) if Lh < L else width
+            if Lh < L:   # the slice's part widths: its widest row's count in each part
+                rows = pm[b][64 * s:64 * s + 64]
+                c1 = [int((codes[b][j, :Lh] != 0).sum()) for j in rows]
+                assert cut == max(c1) and width - cut == max(int(nz[b][j]) - c for j, c in zip(rows, c1))
+            for (lo, hi, pad), exp, (t0, t1) in zip(parts, exps, [(0, cut), (cut, width)]):
+                got = [int(el[b, (sob[s] + t) * 64 + p % 64]) for t in range(t0, t1)]
+                want = exp[p] + [pad] * (t1 - t0 - len(exp[p]))
+                assert got == want, (b, p, lo, got[:8], want[:8])
 
 
 @pytest.mark.parametrize("m,n,weighted", [(1024, 2048, False), (1024, 2048, True), (2048, 1024, False),

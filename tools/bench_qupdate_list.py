@@ -4,7 +4,8 @@ the single-recompute list path (scale_hint given: pass 2 + qp_codes_kernel), HIP
 call; the packed codes and scales of both must be identical.  Run under
 `rocprofv3 --kernel-trace --stats` for the per-kernel split.
 
-  python tools/bench_qupdate_list.py [B] [reps]"""
+  python tools/bench_qupdate_list.py [B] [reps] [--lib path/to/libcaldera_hip.so]
+(--lib: another build of the library, e.g. tools/probes/build_rev.sh HEAD base, for an A/B on one box)"""
 import os
 import sys
 
@@ -15,11 +16,17 @@ import torch  # noqa: E402
 import ee274_convexcaldera_llm_quantization_amd._lib as K  # noqa: E402
 
 dev = "cuda:0"
+lib = None
+if "--lib" in sys.argv:
+    i = sys.argv.index("--lib")
+    lib = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 m = n = 4096
 r = 128
-K.load()
+K.load() if lib is None else K.load(lib)
+print("library:", lib or K.LIB_PATH)
 g = torch.Generator(device=dev).manual_seed(0)
 W = (torch.randn(B, m, n, device=dev, generator=g) * 0.5).half()
 L = torch.linalg.qr(torch.randn(B, m, r, device=dev, generator=g))[0].contiguous()

@@ -34,10 +34,13 @@ def main():
     ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--group", type=int, default=4)
     ap.add_argument("--rr", action="store_true", help="plain round-robin interleaving (overlap.run_interleaved)")
+    ap.add_argument("--no-splitk", action="store_true", help="_lib.AUTO_SPLIT_K = False (one-pass products)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     K.load()
+    if args.no_splitk:
+        K.AUTO_SPLIT_K = False
     qp = CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, update_order=["Q", "LR"], sigma_reg=1e-8)
     ep = EngineParams.from_caldera_params(qp)
     items = S.llama2_7b_matrices(32)
@@ -78,7 +81,7 @@ def main():
         if i >= args.warmup:
             ts.append(time.perf_counter() - t0)
     print(json.dumps({"world": args.world, "rank": args.rank, "matrices": len(mine), "max_batch": args.max_batch,
-                      "group": args.group, "rr": args.rr, "share_s": ts, "median_s": sorted(ts)[len(ts) // 2]}), flush=True)
+                      "group": args.group, "rr": args.rr, "no_splitk": args.no_splitk, "share_s": ts, "median_s": sorted(ts)[len(ts) // 2]}), flush=True)
 
 
 if __name__ == "__main__":

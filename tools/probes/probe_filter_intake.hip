@@ -29,6 +29,24 @@ __device__ __forceinline__ f16x8 frag(const _Float16* img, int row, int chunk) {
     return *reinterpret_cast<const f16x8*>(img + row * BK + (chunk ^ swz(row)) * 8);
 }
 
+__device__ __forceinline__ void issue(const _Float16* Ah, const _Float16* Al, const _Float16* Bh, const _Float16* Bl,
+                                      int64_t b, int64_t M, int64_t N, int64_t K, int wid, const uint32_t (&off)[PER_WAVE],
+                                      int64_t k0, _Float16* st, bool withB) {
+#pragma unroll
+    for (int u = 0; u < PER_WAVE; ++u) {
+        const int I = wid * PER_WAVE + u;
+        const bool isA = I < 24;
+        if (!isA && !withB) continue;
+        const int part = isA ? (I >= 12) : (I >= 48);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+        const _Float16* base = isA ? (part ? Al : Ah) + b * M * K + (k0 >> 5) * (M * 32)
+                                   : (part ? Bl : Bh) + b * N * K + (k0 >> 5) * (N * 32);
+        _Float16* dst = st + (isA ? part * APART : 2 * APART + part * BPART) + (16 * sub) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[u]), (__attribute__((address_space(3))) void*)dst, 16,
+                                         0, 0);
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, const _Float16* Al, const _Float16* Bh,
                                                            const _Float16* Bl, int64_t M, int64_t N, int64_t K,
@@ -53,56 +71,60 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
         gr = gr < lim ? gr : lim - 1;
         off[u] = (uint32_t)(gr * 32 + c * 8);
     }
-    auto issue = [&](int64_t k0, _Float16* st, bool withB) {
-#pragma unroll
-        for (int u = 0; u < PER_WAVE; ++u) {
-            const int I = wid * PER_WAVE + u;
-            const bool isA = I < 24;
-            if (!isA && !withB) continue;
-            const int part = isA ? (I >= 12) : (I >= 48);
-            const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
-            const _Float16* base = isA ? (part ? Al : Ah) + b * M * K + (k0 >> 5) * (M * 32)
-                                       : (part ? Bl : Bh) + b * N * K + (k0 >> 5) * (N * 32);
-            _Float16* dst = st + (isA ? part * APART : 2 * APART + part * BPART) + (16 * sub) * BK;
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[u]),
-                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-        }
-    };
     f32x4v acc[6][4];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const int64_t nt = K / BK;
-    issue(0, smem, true);
-    f16x8 bh[4], bl[4], ah[6], al[6];
+    issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, 0, smem, true);
+    f16x8 bh3[4], bl3[4], a0h, a0l;   // mode 3: fragments read at the first step, reused
     for (int64_t t = 0; t < nt; ++t) {
+        f16x8 bh[4], bl[4];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + 1 < nt && MODE != 2) issue((t + 1) * BK, smem + ((t + 1) & 1) * STAGE, MODE != 1 || ((t + 1) & 1) == 0);
+        if (t + 1 < nt && MODE != 2)
+            issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE,
+                  MODE != 1 || ((t + 1) & 1) == 0);
         const _Float16* sA = smem + (t & 1) * STAGE;
         const _Float16* sB = sA + 2 * APART;
-        if (MODE != 3 || t == 0) {
+        if (MODE != 3) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 bh[j] = frag(sB, 64 * wn + 16 * j + l16, lq);
                 bl[j] = frag(sB + BPART, 64 * wn + 16 * j + l16, lq);
             }
+        } else {
+            if (t == 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bh3[j] = frag(sB, 64 * wn + 16 * j + l16, lq);
+                    bl3[j] = frag(sB + BPART, 64 * wn + 16 * j + l16, lq);
+                }
+                a0h = frag(sA, 96 * wm + l16, lq);
+                a0l = frag(sA + APART, 96 * wm + l16, lq);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { bh[j] = bh3[j]; bl[j] = bl3[j]; }
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            if (MODE != 3 || t == 0) {
-                ah[i] = frag(sA, 96 * wm + 16 * i + l16, lq);
-                al[i] = frag(sA + APART, 96 * wm + 16 * i + l16, lq);
+            f16x8 ah, al;
+            if (MODE != 3) {
+                ah = frag(sA, 96 * wm + 16 * i + l16, lq);
+                al = frag(sA + APART, 96 * wm + 16 * i + l16, lq);
+            } else {
+                ah = a0h;
+                al = a0l;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (MODE != 4) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al[i], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah, acc[i][j], 0, 0, 0);
                 }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
             }
         }
     }
