@@ -122,7 +122,7 @@ _SIGS = {
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
     "cq_q_update_workspace": (c_size, [c_i64, c_i64, c_i64, c_int]),
-    "cq_q_update_list_geometry": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "cq_q_update_list_geometry": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
@@ -784,8 +784,9 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
     # the hint only matters to the 2-bit packed path on fp16 W (the C side ignores it
-    # otherwise): only then is the list workspace (~2.25 B per element: half of the 8-element
-    # groups x 36 B) sized and cached (scratch.py)
+    # otherwise): only then is the list workspace (~0.36 B per element from 2^22 elements on:
+    # single candidates 8 B each for 1/6 of the 8-element groups, whole groups 36 B each for
+    # 1/48; smaller matrices 1/2 and 1/4) sized and cached (scratch.py)
     hint = (scale_hint is not None and r > 0 and bits == 2 and packed is not None and codes is None
             and W.dtype == torch.float16)
     if not hint:
@@ -802,13 +803,14 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         events[1].record()
 
 
-def q_update_list_geometry(m: int, n: int, r: int):
-    """(rows of W per list region, list capacity in 8-element groups per region) of the 2-bit
-    single-recompute Q update (cq_q_update_list_geometry), or None where it does not apply."""
-    rows, cap = ctypes.c_int64(0), ctypes.c_int64(0)
-    if load().cq_q_update_list_geometry(m, n, r, ctypes.byref(rows), ctypes.byref(cap)) != 0:
+def q_update_list_geometry(m: int, n: int, r: int, both: bool = False):
+    """(rows of W per list region, capacity of its single-candidate list[, capacity of its
+    list of groups with two or more candidates]) of the 2-bit single-recompute Q update
+    (cq_q_update_list_geometry), or None where it does not apply."""
+    rows, cap, capb = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    if load().cq_q_update_list_geometry(m, n, r, ctypes.byref(rows), ctypes.byref(cap), ctypes.byref(capb)) != 0:
         return None
-    return int(rows.value), int(cap.value)
+    return (int(rows.value), int(cap.value), int(capb.value)) if both else (int(rows.value), int(cap.value))
 
 
 def absmax(X: torch.Tensor) -> torch.Tensor:

@@ -157,7 +157,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         if (h > 0.f && h <= 0x1p127f) tb = abs_bits(QP_TAU * h);
     }
     const int64_t region = (b * panels + panel) * NW + wid;
-    int64_t gcur = 0;   // pass 2: groups this wave has listed
+    int64_t gcur = 0, gcurA = 0;   // pass 2: list-B groups / list-A entries this wave has listed
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -308,31 +308,46 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                 // one ballot: the list order, hence every later sum, is deterministic).  The
                 // stores are followed by a full drain at the chunk's end (compute() returns
                 // true), a wait that costs little next to a chunk's ~4 us of MFMA work.
-                uint32_t lm = 0u;
+                uint32_t lm = 0u, cm = 0u;   // |res| max, mask of the elements with |res| >= tau
                 float e8 = 0.f;
                 if (ewl) {
                     const float* wv = ewslot + 32 * (ch & 1) + 8 * lq;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        lm = max(lm, abs_bits(v[u]));
+                        const uint32_t ab = abs_bits(v[u]);
+                        lm = max(lm, ab);
+                        cm |= (uint32_t)(ab >= tb) << u;
                         e8 = __builtin_fmaf(v[u] * v[u], wv[u], e8);
                     }
                 } else {
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        lm = max(lm, abs_bits(v[u]));
+                        const uint32_t ab = abs_bits(v[u]);
+                        lm = max(lm, ab);
+                        cm |= (uint32_t)(ab >= tb) << u;
                         e8 = __builtin_fmaf(v[u], v[u], e8);
                     }
                 }
                 mx = max(mx, lm);
                 err += (double)e8;
-                const bool cand = lm >= tb;
-                const uint64_t mk = __ballot(cand);
-                if (mk) {
+                const bool one = cm != 0u && (cm & (cm - 1u)) == 0u, many = (cm & (cm - 1u)) != 0u;
+                const uint64_t mA = __ballot(one), mB = __ballot(many);
+                if (mA | mB) {
                     stored = true;
-                    if (cand) {
+                    if (one) {   // list A: the one candidate element and its residual
+                        const int64_t pos = gcurA + (int64_t)__builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0u));
+                        if (pos < q.capA) {
+                            const int u1 = __builtin_ctz(cm);
+                            float x1 = v[0];
+#pragma unroll
+                            for (int u = 1; u < 8; ++u) x1 = u1 == u ? v[u] : x1;
+                            q.la[region * q.capA + pos] = make_uint2((uint32_t)(e + u1), __float_as_uint(x1));
+                        }
+                    }
+                    if (many) {  // list B: the whole group
                         const int64_t pos = gcur + (int64_t)__builtin_amdgcn_mbcnt_hi(
-                            (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                            (uint32_t)(mB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mB, 0u));
                         if (pos < q.cap) {
                             float4* dv = q.gval + 2 * (region * q.cap + pos);
                             dv[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -340,7 +355,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                             q.gid[region * q.cap + pos] = (uint32_t)e;
                         }
                     }
-                    gcur += __builtin_popcountll(mk);
+                    gcurA += __builtin_popcountll(mA);
+                    gcur += __builtin_popcountll(mB);
                 }
                 continue;
             }
@@ -529,7 +545,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             // gcur == cap: every listed group got a slot (pos < cap) -- a full list, not an
             // overflow; past cap the count is clamped and the matrix falls back to pass 1
             q.cnt[region] = (uint32_t)(gcur <= q.cap ? gcur : q.cap);
-            if (gcur > q.cap) q.ovf[b] = 1u;
+            q.cntA[region] = (uint32_t)(gcurA <= q.capA ? gcurA : q.capA);
+            if (gcur > q.cap || gcurA > q.capA) q.ovf[b] = 1u;
         }
         __shared__ double red2[16];
         const double tsum = block_sum_f64(err, red2);
@@ -601,6 +618,28 @@ __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw
         const uint32_t* gid = q.gid + region * q.cap;
         const float4* gv = q.gval + 2 * region * q.cap;
         const int64_t base = r0 * n;
+        // list A (single candidates), then list B (whole groups): a fixed order
+        const int64_t cntA = q.cntA[region];
+        const uint2* la = q.la + region * q.capA;
+        for (int64_t i = tid; i < cntA; i += 256) {
+            const uint2 en = la[i];
+            const float x = __uint_as_float(en.y);
+            const float qd = x * ys;
+            const float rr = __builtin_fmaf(-qd, s, x);
+            const float c = rintf(__builtin_fmaf(rr, ys, qd) * 1.f);
+            if (c != 0.f) {
+                const int64_t loc = (int64_t)en.x - base;
+                const uint32_t sh = 8u * (uint32_t)((loc >> 2) & 3) + 6u - 2u * (uint32_t)(loc & 3);
+                atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
+                const float d = c * s - x;
+                if (q.ew) {
+                    const float w = q.ew[(int64_t)en.x % n];
+                    delta += (double)((d * d) * w) - (double)((x * x) * w);
+                } else {
+                    delta += (double)(d * d) - (double)(x * x);
+                }
+            }
+        }
         for (int64_t i = tid; i < cnt; i += 256) {
             const float4 v0 = gv[2 * i], v1 = gv[2 * i + 1];
             const float xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};

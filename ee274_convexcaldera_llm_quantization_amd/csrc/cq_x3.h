@@ -59,10 +59,17 @@ struct QUK {
     // whose lists cannot be complete (qp_fallback)
     const float* hint;           // [batch] previous Q scale (candidate threshold), or NULL
     uint32_t* ovf;               // [batch] a wave's list overflowed (zeroed before pass 2)
-    uint32_t* cnt;               // [batch * panels * waves] listed groups per wave region
+    // two lists per wave region: a lane group (8 elements) with exactly ONE |res| >= tau goes
+    // to list A as (element index, residual) -- 8 B; one with two or more to list B as (first
+    // element index, 8 residuals) -- 36 B.  ~95 % of the candidate groups are single (~12 % of
+    // all groups hold a candidate at 4096^2), so the lists take ~1/4 of whole-group records
+    uint32_t* cnt;               // [batch * panels * waves] list-B groups per wave region
     uint32_t* gid;               // [batch * panels * waves * cap] first element index of a group
-    float4* gval;                // [.. * cap * 2] the group's 8 residuals (any |res| >= tau)
-    int64_t cap;                 // groups per wave region
+    float4* gval;                // [.. * cap * 2] the group's 8 residuals (two or more |res| >= tau)
+    int64_t cap;                 // list-B groups per wave region
+    uint32_t* cntA;              // [batch * panels * waves] list-A entries per wave region
+    uint2* la;                   // [.. * capA] (element index, residual bits) of single candidates
+    int64_t capA;                // list-A entries per wave region
     double* part0;               // [batch * panels] pass-2 error partials (all codes zero)
     double* partF;               // [batch * panels * waves] code-kernel error corrections
     int only_fallback;           // pass 1: skip matrices that took the list path
@@ -70,11 +77,14 @@ struct QUK {
 };
 
 constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
-// list capacity: 1 / 2 of a wave region's 8-element groups.  Candidates (|res| >= 0.45 of the
-// absmax) are ~12 % of the groups at 4096^2 but ~31 % on a 320 x 544 matrix (the absmax of
-// fewer Gaussians sits lower); a region past it overflows and its matrix takes the second
-// recompute, so the margin is kept for small shapes (2.25 B of list per element)
-constexpr int QP_CAP_DIV = 2;
+// list capacities (fractions of a wave region's 8-element groups).  Candidate groups (any
+// |res| >= 0.45 of the absmax) are ~12 % at 4096^2 (11.5 % single, 0.6 % multiple; ~9 % at
+// 4096 x 11008) but ~31 % on a 320 x 544 matrix (the absmax of fewer Gaussians sits lower): a
+// region past a capacity overflows and its matrix takes the second recompute.  Matrices of at
+// least 2^22 elements get A 1/6 + B 1/48 (~0.36 B of list per element: 0.9 GB at the bench's
+// B = 256), smaller ones A 1/2 + B 1/4 (their lists are small anyway)
+constexpr int QP_CAPA_DIV_BIG = 6, QP_CAPB_DIV_BIG = 48, QP_CAPA_DIV_SMALL = 2, QP_CAPB_DIV_SMALL = 4;
+constexpr int64_t QP_BIG_NUMEL = 1ll << 22;
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
 constexpr int QP_KMAX = 256;              // row-panel Q update: largest r

@@ -675,6 +675,117 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
 }
 
 
+// ------------------------------------------------------------------ 256 x 256 tile variant
+// For the rank-256 products (config 5: the LPLR loop's Y Rw^T and L^T res, the normal-equation
+// multiplies, all with r = 256 as M or N), where the 192 x 384 tile leaves a third of every
+// tile idle (256 = 192 + 64 rows, or 256 of 384 columns).  Tile 256 x 256 x 32: 8 waves of
+// 128 x 64 (8 x 4 blocks of v_mfma_f32_16x16x32_f16, 128 accumulator VGPRs, two waves per
+// SIMD), the same LDS image (16-row x 64-B pieces, swizzled chunks), the same fragment reads
+// and MFMA order per block as xv_mainloop<false> (al x bh, ah x bl, ah x bh per K step), so a
+// block's sum is the same bits as the 192 x 384 kernel's; the same per-element bytes per flop
+// (2/256 + 2/256 vs 2/192 + 2/384).  Two 64 KB stages.  Plain products only (C = alpha A B^T
+// scale): M % 256 == 0, N % 256 == 0, no split-K / P / D / split output / colw.
+constexpr int XS_BM = 256, XS_BN = 256, XS_THREADS = 512;
+constexpr int XS_APART = XS_BM * XW_BK, XS_BPART = XS_BN * XW_BK;   // halves
+constexpr int XS_STAGE = 2 * XS_APART + 2 * XS_BPART;
+constexpr size_t XS_LDS_BYTES = (size_t)2 * XS_STAGE * sizeof(_Float16);  // 128 KB
+constexpr int XS_PER_WAVE = (2 * XS_BM / 16 + 2 * XS_BN / 16) / (XS_THREADS / 64);  // 8
+static_assert(XS_PER_WAVE == 8, "load split");
+
+__device__ __forceinline__ void xs_plan(const X3K& a, int64_t m0, int64_t n0, int wid, int lane,
+                                        uint32_t (&off)[XS_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XS_PER_WAVE; ++u) {
+        const int I = wid * XS_PER_WAVE + u;  // 0..63: Ah 0-15, Al 16-31, Bh 32-47, Bl 48-63
+        const bool isA = I < 32;
+        const int sub = I & 15;
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ xg_swz(row);
+        const int64_t gr = (isA ? m0 : n0) + row;
+        off[u] = (uint32_t)(isA ? (a.a_blocked ? gr * 32 + c * 8 : gr * a.lda + c * 8)
+                                : (a.b_blocked ? gr * 32 + c * 8 : gr * a.ldb + c * 8));
+    }
+}
+
+__device__ __forceinline__ void xs_issue(const X3K& a, int64_t b, int64_t k0, _Float16* stage, int wid,
+                                         const uint32_t (&off)[XS_PER_WAVE]) {
+#pragma unroll
+    for (int u = 0; u < XS_PER_WAVE; ++u) {
+        const int I = wid * XS_PER_WAVE + u;
+        const bool isA = I < 32;
+        const int part = (I >> 4) & 1;
+        const int sub = I & 15;
+        const _Float16* base = isA ? (part ? a.Al : a.Ah) + b * a.sa + (a.a_blocked ? (k0 >> 5) * (a.lda * 32) : k0)
+                                   : (part ? a.Bl : a.Bh) + b * a.sb + (a.b_blocked ? (k0 >> 5) * (a.ldb * 32) : k0);
+        _Float16* dst = stage + (isA ? part * XS_APART : 2 * XS_APART + part * XS_BPART) + (16 * sub) * XW_BK;
+        xw_load(base + off[u], dst);
+    }
+}
+
+__global__ __launch_bounds__(XS_THREADS, 1) void gemm_x3s_kernel(X3K a) {
+    extern __shared__ __attribute__((aligned(16))) char xs_smem_raw[];
+    _Float16* smem = reinterpret_cast<_Float16*>(xs_smem_raw);
+    const int64_t total = a.tiles_n * a.tiles_m * a.batch;
+    const int64_t orig = blockIdx.x;
+    const int64_t q = total / 8, r8 = total % 8, xcd = orig % 8;
+    const int64_t lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+    const int64_t tm = lin % a.tiles_m, tn = (lin / a.tiles_m) % a.tiles_n, b = lin / (a.tiles_n * a.tiles_m);
+    const int64_t m0 = tm * XS_BM, n0 = tn * XS_BN;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid & 1, wn = wid >> 1;  // rows 128 wm .. +128, cols 64 wn .. +64
+    const int l16 = lane & 15, lq = lane >> 4;
+    f32x4v acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    uint32_t off[XS_PER_WAVE];
+    xs_plan(a, m0, n0, wid, lane, off);
+    const int64_t nt = a.K / XW_BK;
+    xs_issue(a, b, 0, smem, wid, off);
+    for (int64_t t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage t landed everywhere; stage t-1 fully read
+        if (t + 1 < nt) xs_issue(a, b, (t + 1) * XW_BK, smem + ((t + 1) & 1) * XS_STAGE, wid, off);
+        const _Float16* sA = smem + (t & 1) * XS_STAGE;
+        const _Float16* sB = sA + 2 * XS_APART;
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 64 * wn + 16 * j + l16;
+            bh[j] = xg_frag(sB, row, lq);
+            bl[j] = xg_frag(sB + XS_BPART, row, lq);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = 128 * wm + 16 * i + l16;
+            const f16x8 ah = xg_frag(sA, row, lq);
+            const f16x8 al = xg_frag(sA + XS_APART, row, lq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    // C = alpha (acc scale), the same two roundings as gemm_x3v_kernel's epilogue
+    const float sc = a.inv_scale[b], al = a.alpha_v ? a.alpha_v[b] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int64_t row = m0 + 128 * wm + 16 * i + l16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t col = n0 + 64 * wn + 16 * j + 4 * lq;
+            *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) =
+                make_float4(al * (acc[i][j][0] * sc), al * (acc[i][j][1] * sc), al * (acc[i][j][2] * sc),
+                            al * (acc[i][j][3] * sc));
+        }
+    }
+}
+
 // Split-K epilogue: C = alpha (sum of the ksplit partials, in chunk order) + beta P + gamma D,
 // and the split halves of C, as gemm_x3v_kernel's epilogue does (inactive matrices: C = D).
 // One thread per 4 consecutive columns (N % 4 == 0).
@@ -1556,17 +1667,22 @@ static int64_t qu_tiles(int64_t m, int64_t n) {
     return std::max(ceil_div(n, XW_BM) * ceil_div(m, XW_BN), ceil_div(m, XW_BM) * ceil_div(n, XW_BN));
 }
 
-// the single-recompute 2-bit path's buffers (qp_launch_cand) for the larger of its two
-// geometries (rows per wave 32 or 48): overflow flags | counts | pass-2 partials |
-// corrections | group ids | group residuals (1 / QP_CAP_DIV of a region's 8-element groups)
+// the single-recompute 2-bit path's buffers (qp_launch_cand) for one of its geometries (rows
+// per wave, waves): overflow flags | list-B counts | pass-2 partials | corrections | list-A
+// counts | list-B group ids | list-B residuals | list-A entries
 static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int nw, int64_t* regions_out,
-                           int64_t* cap_out) {
-    const int64_t regions = ceil_div(m, (int64_t)rpw * nw) * nw, cap = ceil_div((int64_t)rpw * n / 8, QP_CAP_DIV);
+                           int64_t* cap_out, int64_t* capa_out = nullptr) {
+    const int64_t regions = ceil_div(m, (int64_t)rpw * nw) * nw, groups = (int64_t)rpw * n / 8;
+    const bool big = m * n >= QP_BIG_NUMEL;
+    const int64_t cap = ceil_div(groups, (int64_t)(big ? QP_CAPB_DIV_BIG : QP_CAPB_DIV_SMALL));
+    const int64_t capa = ceil_div(groups, (int64_t)(big ? QP_CAPA_DIV_BIG : QP_CAPA_DIV_SMALL));
     if (regions_out) *regions_out = regions;
     if (cap_out) *cap_out = cap;
+    if (capa_out) *capa_out = capa;
     return align_up((size_t)batch * 4, 256) + align_up((size_t)batch * regions * 4, 256) +
-           align_up((size_t)batch * regions * 8, 256) * 2 + align_up((size_t)batch * regions * cap * 4, 256) +
-           (size_t)batch * regions * cap * 32;
+           align_up((size_t)batch * regions * 8, 256) * 2 + align_up((size_t)batch * regions * 4, 256) +
+           align_up((size_t)batch * regions * cap * 4, 256) + align_up((size_t)batch * regions * cap * 32, 256) +
+           (size_t)batch * regions * capa * 8;
 }
 static size_t qu_cand_bytes(int64_t m, int64_t n, int64_t batch) {
     return std::max(qu_cand_geom(m, n, batch, qp_cand_rows(128), qp_cand_waves(128), nullptr, nullptr),
@@ -1583,12 +1699,15 @@ size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint)
            (with_hint ? qu_cand_bytes(m, n, batch) : 0);
 }
 
-int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out) {
+int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out,
+                              int64_t* capb_out) {
     CQ_REQUIRE(rows_out && cap_out, "cq_q_update_list_geometry: null argument");
     if (!(r > 0 && r % XW_BK == 0 && qp_cand_ok(m, n, (int)r)))
         return set_error(CQ_EINVAL, "cq_q_update_list_geometry: (m, n, r) do not take the list path");
     const int rpw = qp_cand_rows((int)r);
-    qu_cand_geom(m, n, 1, rpw, qp_cand_waves((int)r), nullptr, cap_out);
+    int64_t capb = 0;
+    qu_cand_geom(m, n, 1, rpw, qp_cand_waves((int)r), nullptr, &capb, cap_out);
+    if (capb_out) *capb_out = capb;
     *rows_out = rpw;
     return CQ_OK;
 }
@@ -1659,16 +1778,19 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     // pass 2 + candidate lists + code kernel, pass 1 only where a list cannot be complete
     if (pk && !known && scale_hint && bits == 2 && packed && !codes && dtype == CQ_F16 &&
         qp_cand_ok(m, n, (int)r)) {
-        int64_t regions = 0, cap = 0;
-        qu_cand_geom(m, n, batch, qp_cand_rows((int)r), qp_cand_waves((int)r), &regions, &cap);
+        int64_t regions = 0, cap = 0, capa = 0;
+        qu_cand_geom(m, n, batch, qp_cand_rows((int)r), qp_cand_waves((int)r), &regions, &cap, &capa);
         char* c = reinterpret_cast<char*>(q.part) + align_up((size_t)batch * tiles * sizeof(double), 256);
         q.ovf = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * 4, 256);
         q.cnt = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * 4, 256);
         q.part0 = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
         q.partF = reinterpret_cast<double*>(c); c += align_up((size_t)batch * regions * 8, 256);
+        q.cntA = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * 4, 256);
         q.gid = reinterpret_cast<uint32_t*>(c); c += align_up((size_t)batch * regions * cap * 4, 256);
-        q.gval = reinterpret_cast<float4*>(c);
+        q.gval = reinterpret_cast<float4*>(c); c += align_up((size_t)batch * regions * cap * 32, 256);
+        q.la = reinterpret_cast<uint2*>(c);
         q.cap = cap;
+        q.capA = capa;
         q.hint = scale_hint;
         q.fb_out = fallback_out;
         q.x.batch = batch;
@@ -1848,6 +1970,20 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
         total *= a.ksplit;
     }
     CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
+    // the 256 x 256 tile where the 192 x 384 one would leave over 15 % of its MFMA work idle
+    // (rank-256 products), for plain split products
+    const bool sq = !a.single && !g->b_exact && !a.tri && !a.sym_out && a.ksplit == 1 && !a.P && !a.D && !a.Oh &&
+                    !a.colw && !a.active && g->M % XS_BM == 0 && g->N % XS_BN == 0 && g->ldc % 4 == 0 &&
+                    g->stride_c % 4 == 0 && (reinterpret_cast<uintptr_t>(g->C) & 15) == 0 &&
+                    (double)(a.tiles_m * XW_BM) * (double)(a.tiles_n * XW_BN) > 1.15 * (double)g->M * (double)g->N;
+    if (sq) {
+        a.tiles_m = g->M / XS_BM;
+        a.tiles_n = g->N / XS_BN;
+        const int64_t tot = a.tiles_m * a.tiles_n * a.batch;
+        CQ_REQUIRE(tot < (1ll << 31), "cq_gemm_x3: grid too large");
+        gemm_x3s_kernel<<<(unsigned)tot, XS_THREADS, XS_LDS_BYTES, as_stream(stream)>>>(a);
+        return check_launch("cq_gemm_x3");
+    }
     if (a.single) gemm_x3v_kernel<1><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     else if (g->b_exact) gemm_x3v_kernel<2><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);
     else gemm_x3v_kernel<0><<<(unsigned)total, XW_THREADS, XW_LDS_BYTES, as_stream(stream)>>>(a);

@@ -437,8 +437,9 @@ int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t col
  * scale_hint (may be NULL; may alias scale_out): the previous Q update's scale per matrix.
  * With 2-bit packed codes and fp16 W, LR is then recomputed once: the
  * absmax pass also sums the all-zero-code error and lists every 8-element group holding a
- * |res| >= 0.45 scale_hint; the codes come from that list (a 2-bit code is nonzero only where
- * |res| > scale / 2).  A
+ * |res| >= 0.45 scale_hint (a group with one such element as that element's index and
+ * residual, 8 B; a group with more as its 8 residuals, 36 B); the codes come from those lists
+ * (a 2-bit code is nonzero only where |res| > scale / 2).  A
  * matrix whose list cannot be complete (scale < 0.9 scale_hint, list overflow, non-normal
  * scale) takes the second recompute; fallback_out[b] (may be NULL) reports it.  The
  * workspace is cq_q_update_workspace(m, n, batch, scale_hint != NULL) bytes.  Codes and
@@ -446,10 +447,12 @@ int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t col
  * another order (~1e-8 relative). */
 size_t cq_q_update_workspace(int64_t m, int64_t n, int64_t batch, int with_hint);
 /* Geometry of the single-recompute list path for rank r: rows of W per list region
- * (*rows_out) and list capacity in 8-element groups per region (*cap_out); a region with
- * more candidate groups than that overflows and its matrix takes the second recompute.
+ * (*rows_out), the capacity of its list of single-candidate groups (*cap_out) and of its list
+ * of groups with two or more candidates (*capb_out, may be NULL), per region; a region with
+ * more groups of either kind overflows and its matrix takes the second recompute.
  * Returns 0, or CQ_EINVAL when (m, n, r) do not take the list path. */
-int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out);
+int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out, int64_t* cap_out,
+                              int64_t* capb_out);
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
                    const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
                    const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,

@@ -495,6 +495,36 @@ def test_gemm_x3_matches_fp64(K, M, N, Kd):
     assert err < max(3 * err32, 1e-6), (err, err32)
 
 
+@pytest.mark.parametrize("M,N,Kd,blocked", [(256, 1024, 4096, True), (512, 256, 256, False), (256, 4096, 128, False)])
+def test_gemm_x3_square_tile_bit_identical(K, M, N, Kd, blocked):
+    """The 256 x 256 tile (gemm_x3s_kernel: rank-256 products, config 5's LPLR loop and normal
+    equations) against the 192 x 384 kernel on the same operands: an N a multiple of 384 but
+    not of 256 (N + 128) keeps the 192 x 384 tiling, whose first N columns must be the same
+    bits (same fragments, MFMA order per 16 x 16 block and epilogue roundings); and fp32-grade
+    against fp64."""
+    Bt = 2
+    g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g) * 0.1
+    Bm = torch.randn(Bt, N + 128, Kd, device=DEV, generator=g) * 5.0
+    assert (N + 128) % 384 == 0 and (N + 128) % 256 != 0
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 6, blocked=blocked)
+    Bh, Bl = K.split_f16(Bm.contiguous(), 2.0 ** 10, blocked=blocked)
+    inv = torch.full((Bt,), 2.0 ** -16, device=DEV)
+    C_wide = torch.full((Bt, M, N + 128), float("nan"), device=DEV)
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C_wide, a_blocked=blocked, b_blocked=blocked)
+    if blocked:   # the first N rows of B in the K-blocked layout [K/32][rows][32]
+        Bh_n = Bh.view(Bt, Kd // 32, N + 128, 32)[:, :, :N].contiguous().view(Bt, N, Kd)
+        Bl_n = Bl.view(Bt, Kd // 32, N + 128, 32)[:, :, :N].contiguous().view(Bt, N, Kd)
+    else:
+        Bh_n, Bl_n = Bh[:, :N].contiguous(), Bl[:, :N].contiguous()
+    C = torch.full((Bt, M, N), float("nan"), device=DEV)
+    K.gemm_x3(Ah, Al, Bh_n, Bl_n, inv, C, a_blocked=blocked, b_blocked=blocked)
+    assert torch.equal(C, C_wide[:, :, :N])
+    ref = torch.matmul(A.double(), Bm[:, :N].double().transpose(1, 2))
+    err = ((C.double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < 1e-6, err
+
+
 @pytest.mark.parametrize("M,N,Kd,blocked", [(192, 4096, 4096, True), (100, 1000, 32, False), (192, 400, 64, True),
                                             (250, 770, 96, False), (192, 384, 128, True)])
 def test_gemm_x3_single_product_matches_fp64(K, M, N, Kd, blocked):

@@ -33,25 +33,30 @@ def test_q_update_matches_round2_kernel(case):
 LIST_CASES = [c for c in C.CASES if c[5] == 2 and c[6] == torch.float16]
 
 
+@pytest.mark.parametrize("kind", ["single", "multi"])
 @pytest.mark.parametrize("extra", [-1, 0, 1], ids=["cap-1", "cap", "cap+1"])
-def test_q_update_list_at_capacity(extra):
+def test_q_update_list_at_capacity(extra, kind):
     """A list region holding exactly its capacity of candidate groups is complete (no
     fallback) and one more overflows (fallback to the second recompute); both give the
-    two-pass codes bit for bit.  Region 0 of matrix 0 gets cap + extra planted groups, region 1
-    a few, so a count one past the filled slots would read region 1's first entry."""
+    two-pass codes bit for bit.  Region 0 of matrix 0 gets cap + extra planted groups -- with
+    one candidate element each (list A) or two (list B) -- region 1 a few, so a count one past
+    the filled slots would read region 1's first entry."""
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     dev = torch.device("cuda:0")
     B, n, r = 2, 64, 32
-    rows, cap = K.q_update_list_geometry(8 * 48, n, r)
+    rows, cap_a, cap_b = K.q_update_list_geometry(8 * 48, n, r, both=True)
+    cap = cap_a if kind == "single" else cap_b
     m = 8 * rows                          # 8 wave regions (the first panel)
     g = torch.Generator().manual_seed(4242)
     W = torch.randn(B, m, n, generator=g) * 0.01
     groups = [(i, 8 * c) for i in range(rows) for c in range(n // 8)]   # (row, first column) of region 0
     assert len(groups) >= cap + 1
     pick = torch.randperm(len(groups), generator=g)[: cap + extra].tolist()
-    for t, j in enumerate(pick):          # one element >= 0.5 per planted group; the first is the absmax
+    for t, j in enumerate(pick):          # candidate elements >= 0.5 per planted group; the first is the absmax
         i, c0 = groups[j]
         W[0, i, c0 + t % 8] = 1.0 if t == 0 else (0.5 + 0.4 * torch.rand((), generator=g)) * (1 if t % 3 else -1)
+        if kind == "multi":
+            W[0, i, c0 + (t + 3) % 8] = (0.5 + 0.4 * torch.rand((), generator=g)) * (-1 if t % 2 else 1)
     for t in range(5):                    # region 1
         W[0, rows + 3 * t, 8 * t % n] = 0.7
     W[1, 5, 9] = 1.0
