@@ -71,6 +71,7 @@ class X3Args(ctypes.Structure):
         ("split_ws", c_vp),
         ("b_exact", c_int),
         ("colw", c_vp),
+        ("absmax_out", c_vp),
     ]
 
 
@@ -131,6 +132,7 @@ _SIGS = {
                                c_vp, c_vp, c_vp, c_vp]),
     "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_sgram_rows": (c_int, [c_i64]),
+    "cq_pow2_from_absmax": (c_int, [c_vp, c_i64, c_int, c_vp]),
     "cq_sgram_split": (c_i64, [c_i64, c_i64]),
     "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                               c_vp, c_vp]),
@@ -657,6 +659,18 @@ def pow2_scale(X: torch.Tensor, log2_target: int = 14, out=None):
     return out
 
 
+def pow2_from_absmax(bits: torch.Tensor, log2_target: int = 14) -> torch.Tensor:
+    """In place: (B,) bits of max|X[b]| (as written by gemm_x3 absmax_out, or a positive fp32
+    bound such as a quantiser's scale) -> the fp32 power-of-two split scales pow2_scale would
+    give for X (cq_pow2_from_absmax).  Returns the tensor viewed as fp32."""
+    _require_hip(bits)
+    assert bits.element_size() == 4 and bits.is_contiguous()
+    out = bits.view(torch.float32)
+    _check(load().cq_pow2_from_absmax(_p(out), bits.numel(), int(log2_target), _stream(bits.device)),
+           "cq_pow2_from_absmax")
+    return out
+
+
 def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False):
     """fp16 halves of X * scale (scale: float or (B,) tensor), same shape as X; blocked: the
     K-blocked operand layout over X's last dimension (storage size unchanged)."""
@@ -681,7 +695,7 @@ AUTO_SPLIT_K = True
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
-            single=False, ksplit=None, b_exact=False, colw=None):
+            single=False, ksplit=None, b_exact=False, colw=None, absmax_out=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
@@ -690,7 +704,9 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     C may then be None.  lda / M (a_blocked only): A holds lda >= M rows of which the first M
     are used (C has M rows).  b_exact: B is exactly fp16 (Bl = 0, e.g. W's halves written
     under a split scale >= 1); Bl is not read and may be None.  colw (N,) fp32: the product
-    term of column j scaled by colw[j] (before beta P + gamma D)."""
+    term of column j scaled by colw[j] (before beta P + gamma D).  absmax_out (B,) int32/uint32/fp32
+    (plain products): zeroed here, receives the bits of max|C[b]| (pow2_from_absmax turns them
+    into the next split's scale without a pass over C)."""
     assert Bl is not None or b_exact or single
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, MA, Kd = Ah.shape
@@ -730,6 +746,10 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     if colw is not None:
         assert colw.dtype == torch.float32 and colw.is_contiguous() and colw.numel() == N
         g.colw = colw.data_ptr()
+    if absmax_out is not None:
+        assert absmax_out.numel() == Bt and absmax_out.element_size() == 4 and absmax_out.is_contiguous()
+        absmax_out.zero_()
+        g.absmax_out = absmax_out.data_ptr()
     # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
     # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups.
     # The chunked sum has another fp32 summation order than the one-pass product, so a matrix

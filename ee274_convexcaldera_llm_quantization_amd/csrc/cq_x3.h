@@ -36,6 +36,7 @@ struct X3K {
     int ksplit;                // > 1: K cut into ksplit chunks, fp32 partials in part (split-K)
     float* part;               // [ksplit][batch][M][N]
     const float* colw = nullptr;  // [N] (or NULL): the product term scaled per C column
+    uint32_t* absmax_out = nullptr;  // [batch] (or NULL, plain products): atomic max of |C| bits
 };
 
 using f16x8g = __attribute__((ext_vector_type(8))) _Float16;

@@ -601,6 +601,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
     const float be_ = !live ? 0.f : a.beta_v ? a.beta_v[b] : 0.f;
     const float ga_ = !live ? 1.f : a.gamma_v ? a.gamma_v[b] : 0.f;
     bool ovf = false;
+    uint32_t amx = 0u;   // |C| max bits (absmax_out)
     // lane = C row (A row), registers r = 4 consecutive C columns: 16-byte fp32 and 8-byte
     // fp16 accesses (host guarantees N % 4 == 0 and 16-byte aligned rows)
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -635,6 +636,8 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
                     v[0] += ga_ * dv.x; v[1] += ga_ * dv.y; v[2] += ga_ * dv.z; v[3] += ga_ * dv.w;
                 }
                 *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) = make_float4(v[0], v[1], v[2], v[3]);
+                if (a.absmax_out)
+                    amx = max(amx, max(max(abs_bits(v[0]), abs_bits(v[1])), max(abs_bits(v[2]), abs_bits(v[3]))));
                 if (a.Oh) {
                     _Float16 h[4], l[4];
 #pragma unroll
@@ -658,6 +661,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
                     if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + c];
                     if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + c];
                     a.C[b * a.sc + row * a.ldc + c] = w;
+                    amx = max(amx, abs_bits(w));
                     if (a.Oh) {
                         const float hs = w * a.out_scale;
                         const _Float16 h = (_Float16)hs;
@@ -672,6 +676,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
         }
     }
     if (ovf) atomicOr(a.overflow + b, 1);
+    if (a.absmax_out) {
+        amx = wave_max_u32(amx);
+        if (lane == 0 && amx) atomicMax(a.absmax_out + b, amx);
+    }
 }
 
 
@@ -773,16 +781,22 @@ __global__ __launch_bounds__(XS_THREADS, 1) void gemm_x3s_kernel(X3K a) {
     }
     // C = alpha (acc scale), the same two roundings as gemm_x3v_kernel's epilogue
     const float sc = a.inv_scale[b], al = a.alpha_v ? a.alpha_v[b] : 1.f;
+    uint32_t mx = 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int64_t row = m0 + 128 * wm + 16 * i + l16;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t col = n0 + 64 * wn + 16 * j + 4 * lq;
-            *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) =
-                make_float4(al * (acc[i][j][0] * sc), al * (acc[i][j][1] * sc), al * (acc[i][j][2] * sc),
-                            al * (acc[i][j][3] * sc));
+            const float4 v = make_float4(al * (acc[i][j][0] * sc), al * (acc[i][j][1] * sc), al * (acc[i][j][2] * sc),
+                                         al * (acc[i][j][3] * sc));
+            *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) = v;
+            mx = max(mx, max(max(abs_bits(v.x), abs_bits(v.y)), max(abs_bits(v.z), abs_bits(v.w))));
         }
+    }
+    if (a.absmax_out) {
+        mx = wave_max_u32(mx);
+        if (lane == 0 && mx) atomicMax(a.absmax_out + b, mx);
     }
 }
 
@@ -793,7 +807,9 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
     const int64_t nq = a.N / 4;
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t b = blockIdx.y;
-    if (t >= a.M * nq) return;
+    const bool in = t < a.M * nq;
+    uint32_t amx = 0u;
+    if (in) {
     const int64_t row = t / nq, col = 4 * (t % nq);
     const bool live = !a.active || a.active[b];
     const float al_ = !live ? 0.f : a.alpha_v ? a.alpha_v[b] : 1.f;
@@ -812,6 +828,7 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
         if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + col + r];
         if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + col + r];
         a.C[b * a.sc + row * a.ldc + col + r] = w;
+        amx = max(amx, abs_bits(w));
         if (a.Oh) {
             const float hs = w * a.out_scale;
             const _Float16 h = (_Float16)hs;
@@ -823,6 +840,11 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
         }
     }
     if (ovf) atomicOr(a.overflow + b, 1);
+    }
+    if (a.absmax_out) {   // (every lane reaches the wave reduction)
+        amx = wave_max_u32(amx);
+        if ((threadIdx.x & 63) == 0 && amx) atomicMax(a.absmax_out + b, amx);
+    }
 }
 
 // ------------------------------------------------------------------ fused Q update
@@ -1630,6 +1652,13 @@ int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target,
     return check_launch("cq_pow2_scale");
 }
 
+int cq_pow2_from_absmax(float* scale_inout, int64_t batch, int log2_target, void* stream) {
+    CQ_REQUIRE(scale_inout && batch > 0, "cq_pow2_from_absmax: bad args");
+    CQ_REQUIRE(log2_target > -100 && log2_target < 100, "cq_pow2_from_absmax: bad target");
+    pow2_scale_kernel<<<(unsigned)ceil_div(batch, 256), 256, 0, as_stream(stream)>>>(scale_inout, batch, log2_target);
+    return check_launch("cq_pow2_from_absmax");
+}
+
 int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scale_v, float scale, uint16_t* hi,
                  uint16_t* lo, int64_t blocked_ncols, void* stream) {
     CQ_REQUIRE(X && hi && lo, "cq_split_f16: null pointer");
@@ -1937,6 +1966,8 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
                "cq_gemm_x3: tri needs a square plain product");
     a.single = g->single;
     a.colw = g->colw;
+    a.absmax_out = g->absmax_out;
+    CQ_REQUIRE(!g->absmax_out || (!g->sym_out && !g->tri), "cq_gemm_x3: absmax_out needs a plain product");
     CQ_REQUIRE(!g->colw || (!g->sym_out && !g->tri), "cq_gemm_x3: colw needs a plain product");
     // single + sym_out: the Gram of an exactly-fp16 operand (lo = 0; A = W W^T of the sparse-code
     // Gram, sgram.py): the split products add exact zeros, so one product gives the same bits

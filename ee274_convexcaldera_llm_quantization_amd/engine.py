@@ -294,6 +294,7 @@ class CalderaEngine:
         self.sparse_gram = True      # G from the sparse 2-bit codes where it applies (sgram.py)
         self.r_from_codes = True     # with it, R = U^T W - s U^T c and ||Y||^2 without a residual pass
         self.lplr_trace = None       # list -> per-LPLR-iteration errors are appended (diagnostics)
+        self._s_bm = None            # split scale of the last Y Rw^T product (lplr_rhs -> lplr_L_from)
         for meth in (params.method_Q, params.method_LR):
             if meth not in ("uniform", "nf4", "nf2", "bbint4", "bbint2"):
                 raise NotImplementedError(f"Quantization method '{meth}' not supported yet.")
@@ -763,11 +764,14 @@ class CalderaEngine:
             return K.scale_rc(R, colscale=wts.ycol)
         return R
 
-    def lplr_rhs(self, R, Ysrc, wts: _Weights, Bm, halves=None):
+    def lplr_rhs(self, R, Ysrc, wts: _Weights, Bm, halves=None, r_bound=None):
         """The L step's normal-equation pieces for the current R: Bm = Y Rw^T (m x r, into Bm)
         and Mr = Rw Rw^T (r x r, fp64 Gram).  halves (unweighted Y): Y's K-blocked split-fp16
         halves from cq_residual_split; the product then runs on split-fp16 MFMAs (fp32-grade,
-        3 fp16 products) instead of the fp32 MFMA GEMM."""
+        3 fp16 products) instead of the fp32 MFMA GEMM, and leaves the split scale of Bm for
+        the next product in self._s_bm (from the product's own |Bm| max, no pass over Bm).
+        r_bound (B,) fp32: max|Rw| when known (a quantised R is bounded by its quantiser's scale,
+        attained by its largest code), so its split needs no pass over Rw either."""
         Rw = self._lplr_rw(R, wts)
         B_, m, n = Ysrc.shape
         r = R.shape[1]
@@ -775,10 +779,12 @@ class CalderaEngine:
         if ev is not None:
             ev[0].record()
         if halves is not None:
-            sR = K.pow2_scale(Rw, 14)
+            sR = K.pow2_from_absmax(r_bound.clone()) if r_bound is not None and Rw is R else K.pow2_scale(Rw, 14)
             rh, rl = K.split_f16(Rw, sR, hi=halves["rwh"], lo=halves["rwl"], blocked=True)
+            amx = torch.empty(B_, dtype=torch.float32, device=Rw.device)
             K.gemm_x3(halves["yh"], halves["yl"], rh, rl, 1.0 / (halves["ys"] * sR), Bm, a_blocked=True,
-                      b_blocked=True)
+                      b_blocked=True, absmax_out=amx)
+            self._s_bm = K.pow2_from_absmax(amx)
         else:
             K.gemm(Ysrc, Rw, tb=True, C=Bm)                # m x r
         if ev is not None:
@@ -786,14 +792,16 @@ class CalderaEngine:
         return Bm, K.gram_f64(Rw, Rw, ta=True, tb=True)     # r x r
 
     @staticmethod
-    def _mm_x3(A, B_nk, C, tB=False):
+    def _mm_x3(A, B_nk, C, tB=False, sA=None, sB=None, scale_out=False):
         """C = A B_nk^T (tB: A B_nk, B_nk then given as K x N) on split-fp16 MFMAs (three fp16
         products, fp32 accumulation; per-matrix power-of-two scales): the LPLR loop's
         normal-equation GEMMs (m x r x r, r x r x n), fp32-grade at a fraction of the fp32 MFMA
-        time.  A (B, M, K), C (B, M, N) fp32."""
-        sA = K.pow2_scale(A, 14)
+        time.  A (B, M, K), C (B, M, N) fp32.  sA / sB: the operands' split scales when already
+        known (pow2_scale's value, e.g. from the producing product's |C| max); scale_out: also
+        return C's split scale for the next product (C, sC)."""
+        sA = K.pow2_scale(A, 14) if sA is None else sA
         ah, al = K.split_f16(A, sA)
-        sB = K.pow2_scale(B_nk, 14)
+        sB = K.pow2_scale(B_nk, 14) if sB is None else sB
         if tB:
             Bt, kk, nn = B_nk.shape
             bh = torch.empty((Bt, nn, kk), dtype=torch.float16, device=A.device)
@@ -801,7 +809,11 @@ class CalderaEngine:
             K.transpose_split(B_nk, hi=bh, lo=bl, scale=sB)
         else:
             bh, bl = K.split_f16(B_nk, sB)
-        return K.gemm_x3(ah, al, bh, bl, 1.0 / (sA * sB), C)
+        if not scale_out:
+            return K.gemm_x3(ah, al, bh, bl, 1.0 / (sA * sB), C)
+        amx = torch.empty(A.shape[0], dtype=torch.float32, device=A.device)
+        K.gemm_x3(ah, al, bh, bl, 1.0 / (sA * sB), C, absmax_out=amx)
+        return C, K.pow2_from_absmax(amx)
 
     def lplr_L_from(self, Bm, Mr, n, L, x3=False):
         """L = Bm Mr^{-1} through the whitening Wr Wr^T = Mr^{-1} (rank-revealing at gelsy's
@@ -809,8 +821,10 @@ class CalderaEngine:
         split-fp16 MFMAs."""
         Wr, _ = self._solve_normal(Mr, n)
         if x3:
-            T1 = self._mm_x3(Bm, Wr, torch.empty_like(L), tB=True)  # (Y Rw^T) Wr
-            self._mm_x3(T1, Wr, L)                                   # ... Wr^T
+            sW = K.pow2_scale(Wr, 14)  # (r x r: small)
+            sBm, self._s_bm = self._s_bm, None
+            T1, sT1 = self._mm_x3(Bm, Wr, torch.empty_like(L), tB=True, sA=sBm, sB=sW, scale_out=True)  # (Y Rw^T) Wr
+            self._mm_x3(T1, Wr, L, sA=sT1, sB=sW)                                                    # ... Wr^T
             return L
         T1 = K.gemm(Bm, Wr, C=torch.empty_like(L))          # (Y Rw^T) Wr
         K.gemm(T1, Wr, tb=True, C=L)                       # ... Wr^T
@@ -825,10 +839,11 @@ class CalderaEngine:
         Bm, Mr = self.lplr_rhs(R, Ysrc, wts, torch.empty_like(L) if tmp_mr is None else tmp_mr)
         return self.lplr_L_from(Bm, Mr, R.shape[-1], L)
 
-    def lplr_R_step(self, L, res, R, tmp_rn=None, Ml=None, halves=None):
+    def lplr_R_step(self, L, res, R, tmp_rn=None, Ml=None, halves=None, l_bound=None):
         """R step of the LPLR loop (alg.py:175-177), before quantisation:
         R = lstsq(L, res) = (L^T L)^{-1} L^T res (unweighted, as the reference).
-        L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output.  Returns (R, L^T L)."""
+        L (B, m, r) dequantised, res (B, m, n), R (B, r, n) output.  Returns (R, L^T L).
+        l_bound (B,) fp32: max|L| when known (the quantiser's scale)."""
         m = L.shape[1]
         if tmp_rn is None:
             tmp_rn = torch.empty_like(R)
@@ -840,11 +855,14 @@ class CalderaEngine:
         ev = LPLR_PROBE.start("L^T_res", 2.0 * B_ * m * n * r, 4.0 * B_ * (m * n + n * r + m * r))
         if ev is not None:
             ev[0].record()
+        sCt = None
         if halves is not None:  # L^T res on split-fp16 MFMAs: A = L^T halves, B = res^T halves
-            sL = K.pow2_scale(L, 14)
+            sL = K.pow2_from_absmax(l_bound.clone()) if l_bound is not None else K.pow2_scale(L, 14)
             K.transpose_split(L, hi=halves["lth"], lo=halves["ltl"], scale=sL, blocked=True)
+            amx = torch.empty(B_, dtype=torch.float32, device=L.device)
             K.gemm_x3(halves["lth"], halves["ltl"], halves["yth"], halves["ytl"], 1.0 / (sL * halves["ys"]),
-                      tmp_rn, a_blocked=True, b_blocked=True)
+                      tmp_rn, a_blocked=True, b_blocked=True, absmax_out=amx)
+            sCt = K.pow2_from_absmax(amx)
             Ct = tmp_rn
         else:
             Ct = K.gemm(L, res, ta=True, C=tmp_rn)         # r x n
@@ -852,8 +870,10 @@ class CalderaEngine:
             ev[1].record()
         if halves is not None and r % 32 == 0:  # the two r x r x n GEMMs on split-fp16 MFMAs
             Wlt = K.transpose_split(Wl, out=torch.empty_like(Wl))[0]
-            T2 = self._mm_x3(Wlt, Ct, torch.empty_like(tmp_rn), tB=True)   # Wl^T Ct
-            self._mm_x3(Wl, T2, R, tB=True)                                 # Wl T2
+            sWl = K.pow2_scale(Wl, 14)  # (r x r: small; Wl^T has the same maximum)
+            T2, sT2 = self._mm_x3(Wlt, Ct, torch.empty_like(tmp_rn), tB=True, sA=sWl, sB=sCt,
+                                  scale_out=True)                                  # Wl^T Ct
+            self._mm_x3(Wl, T2, R, tB=True, sA=sWl, sB=sT2)                        # Wl T2
             return R, Ml
         T2 = K.gemm(Wl, Ct, ta=True, C=torch.empty_like(tmp_rn))
         K.gemm(Wl, T2, C=R)
@@ -917,7 +937,7 @@ class CalderaEngine:
                 qL = K.quantize_uniform(L.view(B, m * r), m * r, p.L_bits, codes=True, deq=True)
                 L = qL["deq"].view(B, m, r)
             # --- R = lstsq(L, res) = (L^T L)^{-1} L^T res   (alg.py:175-177, unweighted)
-            _, Ml = self.lplr_R_step(L, res, Rn, tmp_rn, halves=halves)
+            _, Ml = self.lplr_R_step(L, res, Rn, tmp_rn, halves=halves, l_bound=None if cb else qL["scale"].view(B))
             if cb:
                 itemsR, deqR = self._quantize_whole(Rn.view(B, r * n), p.method_LR, p.R_bits)
                 R = deqR.view(B, r, n)
@@ -925,7 +945,7 @@ class CalderaEngine:
                 qR = K.quantize_uniform(Rn.view(B, r * n), r * n, p.R_bits, codes=True, deq=True)
                 R = qR["deq"].view(B, r, n)
             # --- the next L step's normal equations; error ||(res - L R) H_sqrt||_F  (alg.py:182)
-            Bm, Mr = self.lplr_rhs(R, Ysrc, wts, Bm, halves)
+            Bm, Mr = self.lplr_rhs(R, Ysrc, wts, Bm, halves, r_bound=None if cb else qR["scale"].view(B))
             if fused_err:
                 err = (ysq - 2.0 * K.batched_dot(L, Bm) + K.batched_dot(Ml, Mr)).clamp_min(0.0)
             elif aware:  # dense H (or the A/B switch lplr_fused_err off): the error GEMM

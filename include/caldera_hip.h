@@ -270,6 +270,10 @@ int cq_sym_split_f16(const float* G, int64_t n, int64_t batch, int upper_only, i
 /* scale_out[b] = 2^(log2_target - e) with max|X[b]| in [2^(e-1), 2^e) (1 for all-zero X[b]). */
 int cq_pow2_scale(const float* X, int64_t n_per, int64_t batch, int log2_target, float* scale_out,
                   void* stream);
+/* In place: scale_inout[b] holds the bits of a bound on max|X[b]| (cq_gemm_x3's absmax_out, or a
+ * positive fp32 such as a quantiser's scale) on entry and the power-of-two split scale
+ * cq_pow2_scale would give for that maximum on exit (no pass over X). */
+int cq_pow2_from_absmax(float* scale_inout, int64_t batch, int log2_target, void* stream);
 /* hi/lo[b] = split of X[b] (n_per values) scaled by scale_v[b] (or scale if scale_v NULL).
  * blocked_ncols > 0: X[b] is (n_per / ncols) x ncols and the halves are written K-blocked
  * (element (r, c) at (c / 32) * rows * 32 + r * 32 + c % 32; ncols % 32 == 0). */
@@ -329,6 +333,9 @@ typedef struct cq_x3_args {
                                       C column j is scaled by colw[j] before beta P + gamma D
                                       (R = (U^T W) diag(ycol) - s (U^T c) diag(ycol) from W's
                                       exact halves)                                        */
+    uint32_t* absmax_out;          /* [batch] or NULL (plain products only): atomic max of the
+                                      bits of |C[b]| into absmax_out[b] (zeroed by the caller):
+                                      the next product's split scale without a pass over C */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

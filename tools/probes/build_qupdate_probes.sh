@@ -1,0 +1,33 @@
+#!/bin/bash
+# Probe builds of the 2-bit list-path Q update (test infrastructure, never the product library):
+# each variant removes one part of pass 2's work from a temporary copy of the sources and builds
+# tools/probes/lib_qu_<variant>.so, for tools/bench_qupdate_list.py --lib (codes are wrong on purpose)
+#   no_r    the R^T stage loaded for the first chunk only (later chunks reuse it)
+#   no_w    the W ring filled in the prologue only
+#   no_epi  no pass-2 epilogue (residual, max, error, lists): the products are folded into the max
+#   mfma1   one MFMA per block and K step instead of three
+set -e
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
+for v in no_r no_w no_epi mfma1; do
+  T=$(mktemp -d); mkdir -p $T/a/csrc $T/include
+  cp $ROOT/ee274_convexcaldera_llm_quantization_amd/csrc/* $T/a/csrc/; cp $ROOT/include/caldera_hip.h $T/include/
+  f=$T/a/csrc/cq_qupdate.hip
+  case $v in
+    no_r)  sed -i 's/^\(\s*\)qp_issue_r<NW, RROW>(Rhb, Rlb, (ch + 1) \* QP_BN/\1if (false) qp_issue_r<NW, RROW>(Rhb, Rlb, (ch + 1) * QP_BN/' $f ;;
+    no_w)  sed -i 's/^\(\s*\)if (wlive) issue_w(ch + QP_WD - 1/\1if (false) issue_w(ch + QP_WD - 1/' $f ;;
+    no_epi) sed -i 's/^\(\s*\)if constexpr (PASS == 2) {$/\1if constexpr (PASS == 2) { mx = max(mx, __float_as_uint(v[0] + v[1] + v[2] + v[3] + v[4] + v[5] + v[6] + v[7]) \& 0x7fffffffu); continue;/' $f ;;
+    mfma1) sed -i 's/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl\[ks\]\[c\], lh\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/; s/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh\[ks\]\[c\], ll\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/' $f ;;
+  esac
+  if cmp -s $f $ROOT/ee274_convexcaldera_llm_quantization_amd/csrc/cq_qupdate.hip; then echo "probe $v: patch did not apply"; exit 1; fi
+  F="-O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt"
+  objs=""
+  for s in $T/a/csrc/*.hip; do
+    extra=""; [ "$(basename $s)" = cq_qupdate.hip ] && extra="-fno-slp-vectorize"
+    /opt/rocm/bin/hipcc $F $extra -c -o ${s%.hip}.o $s &
+    objs="$objs ${s%.hip}.o"
+  done
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/tools/probes/lib_qu_$v.so $objs
+  rm -rf $T
+  echo built tools/probes/lib_qu_$v.so
+done
