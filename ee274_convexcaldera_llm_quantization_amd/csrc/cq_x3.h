@@ -82,9 +82,10 @@ constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scal
 // |res| >= 0.45 of the absmax) are ~12 % at 4096^2 (11.5 % single, 0.6 % multiple; ~9 % at
 // 4096 x 11008) but ~31 % on a 320 x 544 matrix (the absmax of fewer Gaussians sits lower): a
 // region past a capacity overflows and its matrix takes the second recompute.  Matrices of at
-// least 2^22 elements get A 1/6 + B 1/48 (~0.36 B of list per element: 0.9 GB at the bench's
-// B = 256), smaller ones A 1/2 + B 1/4 (their lists are small anyway)
-constexpr int QP_CAPA_DIV_BIG = 6, QP_CAPB_DIV_BIG = 48, QP_CAPA_DIV_SMALL = 2, QP_CAPB_DIV_SMALL = 4;
+// least 2^22 elements get A 1/7 (14.3 % of the groups: ~11 standard deviations above the 11.5 %
+// a 4096^2 region of 16384 groups holds) + B 1/96 (1.0 %, 1.7x the 0.6 %): ~0.21 B of list per
+// element, 0.87 GB at the bench's B = 256; smaller ones A 1/2 + B 1/4 (1.6 B per element)
+constexpr int QP_CAPA_DIV_BIG = 7, QP_CAPB_DIV_BIG = 96, QP_CAPA_DIV_SMALL = 2, QP_CAPB_DIV_SMALL = 4;
 constexpr int64_t QP_BIG_NUMEL = 1ll << 22;
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk
