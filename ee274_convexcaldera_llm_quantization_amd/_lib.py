@@ -804,9 +804,9 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
         halves = [Lh, Ll, Rth, Rtl]
     lib = load()
     # the hint only matters to the 2-bit packed path on fp16 W (the C side ignores it
-    # otherwise): only then is the list workspace (~0.21 B per element from 2^22 elements on:
-    # single candidates 8 B each for 1/7 of the 8-element groups, whole groups 36 B each for
-    # 1/96; smaller matrices 1/2 and 1/4) sized and cached (scratch.py)
+    # otherwise): only then is the list workspace (~0.22 B per element from 2^22 elements on:
+    # single candidates 8 B each for 15.5 % of the 8-element groups, whole groups 36 B each for
+    # 1.5 %; smaller matrices 50 % and 25 %) sized and cached (scratch.py)
     hint = (scale_hint is not None and r > 0 and bits == 2 and packed is not None and codes is None
             and W.dtype == torch.float16)
     if not hint:

@@ -78,14 +78,18 @@ struct QUK {
 };
 
 constexpr float QP_TAU = 0.45f;           // candidate threshold / previous scale (2 tau <= s needed)
-// list capacities (fractions of a wave region's 8-element groups).  Candidate groups (any
-// |res| >= 0.45 of the absmax) are ~12 % at 4096^2 (11.5 % single, 0.6 % multiple; ~9 % at
-// 4096 x 11008) but ~31 % on a 320 x 544 matrix (the absmax of fewer Gaussians sits lower): a
-// region past a capacity overflows and its matrix takes the second recompute.  Matrices of at
-// least 2^22 elements get A 1/7 (14.3 % of the groups: ~11 standard deviations above the 11.5 %
-// a 4096^2 region of 16384 groups holds) + B 1/96 (1.0 %, 1.7x the 0.6 %): ~0.21 B of list per
-// element, 0.87 GB at the bench's B = 256; smaller ones A 1/2 + B 1/4 (1.6 B per element)
-constexpr int QP_CAPA_DIV_BIG = 7, QP_CAPB_DIV_BIG = 96, QP_CAPA_DIV_SMALL = 2, QP_CAPB_DIV_SMALL = 4;
+// list capacities, in thousandths of a wave region's 8-element groups.  Measured on the bench
+// batches (tools/list_density.py, profiles/r05n_list_density_*.log): the first hinted update
+// has the densest lists -- single-candidate groups 7.8 % on average at 4096^2 but up to 13.4 %
+// in one 32-row region (the L R part of the residual is not uniform over rows), groups with two
+// or more 0.32 % on average, up to 1.07 %; later updates ~5.3 % / 0.14 %; 4096 x 11008 and
+// 11008 x 4096 lower.  A region past a capacity overflows and its matrix takes the second
+// recompute (correct, slower).  Matrices of at least 2^22 elements get A 15.5 % (1.16x the
+// densest region) + B 1.5 % (1.4x): 1.78 B of list per group, ~0.22 B per element, 0.99 GB of workspace at
+// the bench's B = 256; smaller ones A 50 % + B 25 % (their candidates are denser, ~31 % of the
+// groups at 320 x 544, and their lists small anyway)
+constexpr int QP_CAPA_PERMILLE_BIG = 155, QP_CAPB_PERMILLE_BIG = 15, QP_CAPA_PERMILLE_SMALL = 500,
+              QP_CAPB_PERMILLE_SMALL = 250;
 constexpr int64_t QP_BIG_NUMEL = 1ll << 22;
 
 constexpr int QP_BN = 32;                 // row-panel Q update: columns per chunk

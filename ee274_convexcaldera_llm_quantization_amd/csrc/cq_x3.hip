@@ -1703,8 +1703,8 @@ static size_t qu_cand_geom(int64_t m, int64_t n, int64_t batch, int rpw, int nw,
                            int64_t* cap_out, int64_t* capa_out = nullptr) {
     const int64_t regions = ceil_div(m, (int64_t)rpw * nw) * nw, groups = (int64_t)rpw * n / 8;
     const bool big = m * n >= QP_BIG_NUMEL;
-    const int64_t cap = ceil_div(groups, (int64_t)(big ? QP_CAPB_DIV_BIG : QP_CAPB_DIV_SMALL));
-    const int64_t capa = ceil_div(groups, (int64_t)(big ? QP_CAPA_DIV_BIG : QP_CAPA_DIV_SMALL));
+    const int64_t cap = ceil_div(groups * (big ? QP_CAPB_PERMILLE_BIG : QP_CAPB_PERMILLE_SMALL), (int64_t)1000);
+    const int64_t capa = ceil_div(groups * (big ? QP_CAPA_PERMILLE_BIG : QP_CAPA_PERMILLE_SMALL), (int64_t)1000);
     if (regions_out) *regions_out = regions;
     if (cap_out) *cap_out = cap;
     if (capa_out) *capa_out = capa;

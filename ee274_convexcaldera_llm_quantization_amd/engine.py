@@ -523,7 +523,7 @@ class CalderaEngine:
                     sparse_g = lite = True
             if sparse_g and not tall and self._sg_A is None:  # once per run: A = W diag(w) W^T
                 self._sg_A = scratch.get("sgram.A", (B, m, m), torch.float32, dev)
-                self._sg = sgram.SparseGram(B, m, n, dev)
+                self._sg = sgram.SparseGram(B, m, n, dev, split=not weighted)
                 self._sg_w = (wts.ycol * wts.ycol).contiguous() if weighted else None
                 sv._alloc(dev)
                 if lite:

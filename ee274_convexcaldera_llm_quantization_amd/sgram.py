@@ -74,7 +74,7 @@ def gram_A(Ws: torch.Tensor, ycol, ycol_max: float, wmax: torch.Tensor, A: torch
 class SparseGram:
     """Per-batch workspace of the sparse Gram (row counts, ELL, P)."""
 
-    def __init__(self, B: int, m: int, n: int, dev):
+    def __init__(self, B: int, m: int, n: int, dev, split: bool = True):
         self.B, self.m, self.n = B, m, n
         self.ns = -(-m // 64)
         self.row_nnz = torch.empty(B * m, dtype=torch.int32, device=dev)
@@ -82,8 +82,11 @@ class SparseGram:
         self.slice_off = torch.empty(B * (self.ns + 1), dtype=torch.int64, device=dev)
         self.total = torch.empty(B, dtype=torch.int64, device=dev)
         # l-split ELL for the long contractions (cq_sgram_split: n = 11008 at k = 4096): four rows
-        # of E staged half a contraction at a time instead of two over all of it
-        self.Lh = K.sgram_split(m, n) if L_SPLIT else n
+        # of E staged half a contraction at a time instead of two over all of it.  split=False
+        # (the engine's column-weighted Grams): the unsplit layout, whose SpMM measured faster
+        # there (config 3: 32.9 vs 34.7 ms per B = 192 launch; unweighted config 4t: 10.97 vs
+        # 10.53 ms per B = 64, profiles/r05i_kt3*, r05n_kt4t_*)
+        self.Lh = K.sgram_split(m, n) if (L_SPLIT and split) else n
         self.row_nnz1 = torch.empty(B * m, dtype=torch.int32, device=dev) if self.Lh < n else None
         self.slice_w1 = torch.empty(B * self.ns, dtype=torch.int32, device=dev) if self.Lh < n else None
         self.density = None

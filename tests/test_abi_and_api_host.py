@@ -44,6 +44,17 @@ def test_gemm_args_struct_matches_header():
     assert [f for f, _ in K.X3Args._fields_] == _struct_fields("cq_x3_args")
 
 
+def test_q_update_list_workspace_fits_1gb():
+    """The 2-bit list workspace of the bench batch (B = 256 x 4096^2, rank 128) stays within
+    1 GB; the region capacities are the measured-density fractions of csrc/cq_x3.h."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    lib = K.load()
+    assert lib.cq_q_update_workspace(4096, 4096, 256, 1) <= 1_000_000_000
+    rows, capA, capB = K.q_update_list_geometry(4096, 4096, 128, both=True)
+    groups = rows * 4096 // 8
+    assert capA >= 0.155 * groups and capB >= 0.015 * groups
+
+
 def test_caldera_params_defaults_match_reference():
     from src.caldera.utils.dataclasses import CalderaParams, CalderaDecomposition, QuantInfo
     p = CalderaParams()
