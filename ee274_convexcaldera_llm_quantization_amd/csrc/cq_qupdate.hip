@@ -85,6 +85,15 @@ __device__ __forceinline__ bool qp_fallback(const QUK& q, int64_t b, float s) {
     return q.ovf[b] != 0u || !div_fast_ok(s) || !(2.f * tau <= s);
 }
 
+// max(m, |a|, |b|) in one v_max3_f32 with |.| source modifiers (fmaxf would first canonicalise
+// each |x| by a v_max_f32 of its own).  A NaN operand is dropped, not propagated: pass 2
+// catches NaN residuals through its error sum instead.
+__device__ __forceinline__ float qp_max3_abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
 // RB row-blocks of 16 rows per wave; K = r <= 32 KSMAX.  FAST (pass 1): the scale is a
 // finite normal number and |res| <= scale, so x / s and c / k take the branch-free correctly
 // rounded division (div_fast; same results as IEEE division), and 2-bit dequantisation is
@@ -151,13 +160,18 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     double err = 0.0;
     // pass 2: candidate threshold (|res| >= tau as order-preserving bits; an invalid hint keeps
     // only non-finite values and the matrix falls back) and this wave's list region
-    uint32_t tb = 0x7f800000u;
+    float tau = __builtin_inff();
+    float mxf = 0.f;   // pass 2: max |res| (non-negative floats order as their bits)
     if (PASS == 2) {
         const float h = q.hint[b];
-        if (h > 0.f && h <= 0x1p127f) tb = abs_bits(QP_TAU * h);
+        if (h > 0.f && h <= 0x1p127f) tau = QP_TAU * h;
     }
     const int64_t region = (b * panels + panel) * NW + wid;
-    int64_t gcur = 0, gcurA = 0;   // pass 2: list-B groups / list-A entries this wave has listed
+    int gcur = 0, gcurA = 0;   // pass 2: list-B groups / list-A entries this wave has listed
+    uint2* const laR = PASS == 2 ? q.la + region * q.capA : nullptr;
+    float4* const gvR = PASS == 2 ? q.gval + 2 * region * q.cap : nullptr;
+    uint32_t* const gidR = PASS == 2 ? q.gid + region * q.cap : nullptr;
+    const int capA = PASS == 2 ? (int)q.capA : 0, capB = PASS == 2 ? (int)q.cap : 0;
     // A-row t (MFMA row) of 16-column block c <-> chunk column 8 (t / 4) + 4 c + t % 4: the
     // lane (l16, lq) then owns chunk columns 8 lq .. 8 lq + 7 of W row l16 (per row block)
     const int acol0 = 8 * (l16 >> 2) + (l16 & 3);   // + 4 c
@@ -232,15 +246,18 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     auto resid = [&](const uint4 (&wc)[RB][WV], const f32x4v (&acc)[RB][2], int rb, float (&v)[8]) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            float w;
             if (DT == CQ_F16) {
+                // one fma: the product times the power-of-two scale is exact, so w - acc sc
+                // rounded once is the same number as the multiply then subtract of the fp32
+                // path (v_fma_mix_f32 reads the f16 half of W's register directly)
                 const uint32_t pr = (&wc[rb][0].x)[u >> 1];
-                w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
+                const float w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
+                v[u] = __builtin_fmaf(-acc[rb][u >> 2][u & 3], sc, w);
             } else {
-                w = __uint_as_float((&wc[rb][u >> 2].x)[u & 3]);
+                const float w = __uint_as_float((&wc[rb][u >> 2].x)[u & 3]);
+                const float pv = acc[rb][u >> 2][u & 3] * sc;
+                v[u] = w - pv;
             }
-            const float pv = acc[rb][u >> 2][u & 3] * sc;
-            v[u] = w - pv;
         }
     };
     auto vmax = [&](const float (&v)[8], uint32_t cur) {
@@ -303,56 +320,62 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             }
             if constexpr (PASS == 2) {
                 // absmax; the error every element has with code 0 (d = 0 - x; fp32 over the
-                // lane's 8 elements, fp64 across); and, where any of the lane's 8 elements has
-                // |res| >= tau, the whole group of 8 residuals to this wave's list (slot from
-                // one ballot: the list order, hence every later sum, is deterministic).  The
-                // stores are followed by a full drain at the chunk's end (compute() returns
-                // true), a wait that costs little next to a chunk's ~4 us of MFMA work.
-                uint32_t lm = 0u, cm = 0u;   // |res| max, mask of the elements with |res| >= tau
+                // lane's 8 elements, fp64 across); and the candidates |res| >= tau, as lane
+                // masks (v_cmp with the |.| modifier).  A lane group with exactly one candidate
+                // goes to list A (its element index and residual), one with two or more to
+                // list B (the whole group); the count runs bit-sliced on the masks (scalar
+                // instructions), the slot of a lane comes from one ballot per list, so the list
+                // order, hence every later sum, is deterministic.  The stores are followed by a
+                // full drain at the chunk's end (compute() returns true).
+                // (the per-element tests as 64-lane masks from the start: kept as lane booleans
+                // the compiler materialises the count's and/or chain in VALU registers)
+                uint64_t c[8];
                 float e8 = 0.f;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c[u] = __ballot(__builtin_fabsf(v[u]) >= tau);
+#pragma unroll
+                for (int u = 0; u < 8; u += 2) mxf = qp_max3_abs(mxf, v[u], v[u + 1]);
                 if (ewl) {
                     const float* wv = ewslot + 32 * (ch & 1) + 8 * lq;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const uint32_t ab = abs_bits(v[u]);
-                        lm = max(lm, ab);
-                        cm |= (uint32_t)(ab >= tb) << u;
-                        e8 = __builtin_fmaf(v[u] * v[u], wv[u], e8);
-                    }
+                    for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u] * v[u], wv[u], e8);
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const uint32_t ab = abs_bits(v[u]);
-                        lm = max(lm, ab);
-                        cm |= (uint32_t)(ab >= tb) << u;
-                        e8 = __builtin_fmaf(v[u], v[u], e8);
-                    }
+                    for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u], v[u], e8);
                 }
-                mx = max(mx, lm);
                 err += (double)e8;
-                const bool one = cm != 0u && (cm & (cm - 1u)) == 0u, many = (cm & (cm - 1u)) != 0u;
-                const uint64_t mA = __ballot(one), mB = __ballot(many);
+                uint64_t any = c[0], two = 0;
+#pragma unroll
+                for (int u = 1; u < 8; ++u) {
+                    two |= any & c[u];
+                    any |= c[u];
+                }
+                const uint64_t mA = any & ~two, mB = two;
                 if (mA | mB) {
                     stored = true;
-                    if (one) {   // list A: the one candidate element and its residual
-                        const int64_t pos = gcurA + (int64_t)__builtin_amdgcn_mbcnt_hi(
+                    if (__builtin_amdgcn_inverse_ballot_w64(mA)) {   // list A: the one candidate's index and residual
+                        const int pos = gcurA + (int)__builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0u));
-                        if (pos < q.capA) {
-                            const int u1 = __builtin_ctz(cm);
-                            float x1 = v[0];
-#pragma unroll
-                            for (int u = 1; u < 8; ++u) x1 = u1 == u ? v[u] : x1;
-                            q.la[region * q.capA + pos] = make_uint2((uint32_t)(e + u1), __float_as_uint(x1));
+                        if (pos < capA) {
+                            // its position u1 bit by bit from the masks, its residual by a
+                            // three-level select on those bits
+                            const bool b0 = __builtin_amdgcn_inverse_ballot_w64(c[1] | c[3] | c[5] | c[7]);
+                            const bool b1 = __builtin_amdgcn_inverse_ballot_w64(c[2] | c[3] | c[6] | c[7]);
+                            const bool b2 = __builtin_amdgcn_inverse_ballot_w64(c[4] | c[5] | c[6] | c[7]);
+                            const uint32_t u1 = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
+                            const float p0 = b0 ? v[1] : v[0], p1 = b0 ? v[3] : v[2];
+                            const float p2 = b0 ? v[5] : v[4], p3 = b0 ? v[7] : v[6];
+                            const float x1 = b2 ? (b1 ? p3 : p2) : (b1 ? p1 : p0);
+                            laR[pos] = make_uint2((uint32_t)e + u1, __float_as_uint(x1));
                         }
                     }
-                    if (many) {  // list B: the whole group
-                        const int64_t pos = gcur + (int64_t)__builtin_amdgcn_mbcnt_hi(
+                    if (__builtin_amdgcn_inverse_ballot_w64(mB)) {  // list B: the whole group
+                        const int pos = gcur + (int)__builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(mB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mB, 0u));
-                        if (pos < q.cap) {
-                            float4* dv = q.gval + 2 * (region * q.cap + pos);
-                            dv[0] = make_float4(v[0], v[1], v[2], v[3]);
-                            dv[1] = make_float4(v[4], v[5], v[6], v[7]);
-                            q.gid[region * q.cap + pos] = (uint32_t)e;
+                        if (pos < capB) {
+                            gvR[2 * pos] = make_float4(v[0], v[1], v[2], v[3]);
+                            gvR[2 * pos + 1] = make_float4(v[4], v[5], v[6], v[7]);
+                            gidR[pos] = (uint32_t)e;
                         }
                     }
                     gcurA += __builtin_popcountll(mA);
@@ -536,6 +559,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
             }
         }
     }
+    if (PASS == 2) mx = __float_as_uint(mxf);
     if (PASS == 0 || PASS == 2) {
         mx = wave_max_u32(mx);
         if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
@@ -544,13 +568,21 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         if (lane == 0) {
             // gcur == cap: every listed group got a slot (pos < cap) -- a full list, not an
             // overflow; past cap the count is clamped and the matrix falls back to pass 1
-            q.cnt[region] = (uint32_t)(gcur <= q.cap ? gcur : q.cap);
-            q.cntA[region] = (uint32_t)(gcurA <= q.capA ? gcurA : q.capA);
-            if (gcur > q.cap || gcurA > q.capA) q.ovf[b] = 1u;
+            q.cnt[region] = (uint32_t)(gcur <= capB ? gcur : capB);
+            q.cntA[region] = (uint32_t)(gcurA <= capA ? gcurA : capA);
+            if (gcur > capB || gcurA > capA) q.ovf[b] = 1u;
         }
         __shared__ double red2[16];
         const double tsum = block_sum_f64(err, red2);
-        if (tid == 0) q.part0[b * panels + panel] = tsum;
+        if (tid == 0) {
+            q.part0[b * panels + panel] = tsum;
+            // a NaN residual (the float max above skips it; the error sum does not): the
+            // matrix takes pass 1 with a NaN absmax, as the two-pass form would
+            if (tsum != tsum) {
+                q.ovf[b] = 1u;
+                atomicMax(q.absmax + b, 0x7fffffffu);
+            }
+        }
     } else if (PASS == 1 && q.part) {
         __shared__ double red[16];
         const double tsum = block_sum_f64(err, red);

@@ -6,9 +6,14 @@
 #   no_w    the W ring filled in the prologue only
 #   no_epi  no pass-2 epilogue (residual, max, error, lists): the products are folded into the max
 #   mfma1   one MFMA per block and K step instead of three
+#   drain   the counted end-of-chunk wait even after list stores (timing only: with stores in
+#           flight the count does not prove the next stage landed)
+#   nostore the candidate lists classified but not stored
+#   prio    s_setprio 1 for the second half of the waves (static priority)
+# (variants to build: the arguments, default all)
 set -e
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-for v in no_r no_w no_epi mfma1; do
+for v in ${@:-no_r no_w no_epi mfma1 drain nostore prio}; do
   T=$(mktemp -d); mkdir -p $T/a/csrc $T/include
   cp $ROOT/ee274_convexcaldera_llm_quantization_amd/csrc/* $T/a/csrc/; cp $ROOT/include/caldera_hip.h $T/include/
   f=$T/a/csrc/cq_qupdate.hip
@@ -17,6 +22,9 @@ for v in no_r no_w no_epi mfma1; do
     no_w)  sed -i 's/^\(\s*\)if (wlive) issue_w(ch + QP_WD - 1/\1if (false) issue_w(ch + QP_WD - 1/' $f ;;
     no_epi) sed -i 's/^\(\s*\)if constexpr (PASS == 2) {$/\1if constexpr (PASS == 2) { mx = max(mx, __float_as_uint(v[0] + v[1] + v[2] + v[3] + v[4] + v[5] + v[6] + v[7]) \& 0x7fffffffu); continue;/' $f ;;
     mfma1) sed -i 's/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl\[ks\]\[c\], lh\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/; s/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh\[ks\]\[c\], ll\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/' $f ;;
+    drain) sed -i 's/^\(\s*\)if (!stored \&\& wlive) wait_vm(/\1if (wlive) wait_vm(/' $f ;;
+    nostore) sed -i 's/^\(\s*\)laR\[pos\] = make_uint2/\1if (q.m < 0) laR[pos] = make_uint2/; s/^\(\s*\)gvR\[2 \* pos\] = /\1if (q.m < 0) gvR[2 * pos] = /; s/^\(\s*\)gvR\[2 \* pos + 1\] = /\1if (q.m < 0) gvR[2 * pos + 1] = /; s/^\(\s*\)gidR\[pos\] = /\1if (q.m < 0) gidR[pos] = /' $f ;;
+    prio) sed -i 's/^\(\s*\)int sw = 0;   \/\/ slot of chunk ch/\1if (wid >= NW \/ 2) __builtin_amdgcn_s_setprio(1);\n\1int sw = 0;/' $f ;;
   esac
   if cmp -s $f $ROOT/ee274_convexcaldera_llm_quantization_amd/csrc/cq_qupdate.hip; then echo "probe $v: patch did not apply"; exit 1; fi
   F="-O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt"
