@@ -503,6 +503,10 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
         for (int c = 0; c < QP_WD - 1 && c < nchunks; ++c) issue_w(c, c);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        // static priority for the youngest wave of each SIMD (waves NW - 4 .. NW - 1, dispatched
+        // last: the arbitration losers of every chunk), set once (MI355X_MICROARCH.md, static
+        // priority): list pass 2 4.35 -> 4.21 ms per B = 256 call, profiles/r05r_kt_*
+        if (wid >= NW - 4) __builtin_amdgcn_s_setprio(1);
         int sw = 0;   // slot of chunk ch
         for (int64_t ch = 0; ch < nchunks; ++ch) {
             if (ch + 1 < nchunks) {

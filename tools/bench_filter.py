@@ -3,6 +3,7 @@ the Chebyshev filter step (blocked A/B, recurrence epilogue, blocked split outpu
 upper-triangle Gram Y Y^T, and the fused Q update.  Run once per kernel variant:
     CQ_X3_KERNEL=w2 python tools/bench_filter.py 128     # 2-stage ring (BK 32)
     python tools/bench_filter.py 128                     # default kernel
+    python tools/bench_filter.py 256 --lib tools/probes/lib_x.so   # another build (A/B on one box)
 Prints ms per launch and the filter's algorithmic GB/s."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -10,7 +11,12 @@ import torch
 import ee274_convexcaldera_llm_quantization_amd._lib as K
 
 dev = "cuda:0"
-K.load()
+_lib = None
+if "--lib" in sys.argv:
+    _i = sys.argv.index("--lib")
+    _lib = sys.argv[_i + 1]
+    del sys.argv[_i:_i + 2]
+K.load() if _lib is None else K.load(_lib)
 
 
 CLOCK = bool(os.environ.get("CQ_X3_CLOCK"))
@@ -34,7 +40,7 @@ def bench(fn, n=10):
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 k, p, xs = 4096, 192, 2.0 ** 6
-tag = os.environ.get("CQ_X3_KERNEL", "default")
+tag = os.environ.get("CQ_X3_KERNEL", os.path.basename(_lib) if _lib else "default")
 g = torch.Generator(device=dev).manual_seed(0)
 Gh = torch.empty(B, k, k, device=dev, dtype=torch.float16)
 Gl = torch.empty_like(Gh)

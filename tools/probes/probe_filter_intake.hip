@@ -9,7 +9,12 @@
 //   mode 2  no loads after the first stage (intake 0: fragment reads + MFMAs + barriers)
 //   mode 3  loads as mode 0, fragments read from LDS once (no per-step fragment reads)
 //   mode 4  loads and fragment reads as mode 0, one MFMA per block and step instead of three
-// Results are numerically meaningless for modes 1-4 (stale LDS / reused fragments).
+//   mode 5  X^T's (A's) LDS-DMA loads skipped after the first stage (G's every step)
+//   mode 6  G's (B's) LDS-DMA loads skipped after the first stage (X^T's every step)
+//   mode 7  X^T's fragments loaded by each wave straight into registers (global_load, L2/L1-
+//           served): row block i's fragments of step t + 1 are loaded into the registers of
+//           step t's right after its MFMAs; only G through the LDS-DMA ring
+// Results are numerically meaningless for modes 1-6 (stale LDS / reused fragments).
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -o probe_filter_intake probe_filter_intake.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -31,12 +36,13 @@ __device__ __forceinline__ f16x8 frag(const _Float16* img, int row, int chunk) {
 
 __device__ __forceinline__ void issue(const _Float16* Ah, const _Float16* Al, const _Float16* Bh, const _Float16* Bl,
                                       int64_t b, int64_t M, int64_t N, int64_t K, int wid, const uint32_t (&off)[PER_WAVE],
-                                      int64_t k0, _Float16* st, bool withB) {
+                                      int64_t k0, _Float16* st, bool withB, bool withA = true) {
 #pragma unroll
     for (int u = 0; u < PER_WAVE; ++u) {
         const int I = wid * PER_WAVE + u;
         const bool isA = I < 24;
         if (!isA && !withB) continue;
+        if (isA && !withA) continue;
         const int part = isA ? (I >= 12) : (I >= 48);
         const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
         const _Float16* base = isA ? (part ? Al : Ah) + b * M * K + (k0 >> 5) * (M * 32)
@@ -79,6 +85,16 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
     const int64_t nt = K / BK;
     issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, 0, smem, true);
     f16x8 bh3[4], bl3[4], a0h, a0l;   // mode 3: fragments read at the first step, reused
+    // mode 7: this wave's X^T fragments (96 rows x 32, hi and lo) of the current and the next step
+    f16x8 ra[6][2];
+    auto load_a = [&](int64_t k0, int i) {
+        const int64_t o = b * M * K + (k0 >> 5) * (M * 32) + (96 * wm + 16 * i + l16) * 32 + 8 * lq;
+        ra[i][0] = *reinterpret_cast<const f16x8*>(Ah + o);
+        ra[i][1] = *reinterpret_cast<const f16x8*>(Al + o);
+    };
+    if (MODE == 7)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) load_a(0, i);
     for (int64_t t = 0; t < nt; ++t) {
         f16x8 bh[4], bl[4];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -86,7 +102,7 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
         __builtin_amdgcn_s_barrier();
         if (t + 1 < nt && MODE != 2)
             issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE,
-                  MODE != 1 || ((t + 1) & 1) == 0);
+                  (MODE != 1 || ((t + 1) & 1) == 0) && MODE != 6, MODE != 5 && MODE != 7);
         const _Float16* sA = smem + (t & 1) * STAGE;
         const _Float16* sB = sA + 2 * APART;
         if (MODE != 3) {
@@ -111,7 +127,10 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             f16x8 ah, al;
-            if (MODE != 3) {
+            if (MODE == 7) {
+                ah = ra[i][0];
+                al = ra[i][1];
+            } else if (MODE != 3) {
                 ah = frag(sA, 96 * wm + 16 * i + l16, lq);
                 al = frag(sA + APART, 96 * wm + 16 * i + l16, lq);
             } else {
@@ -126,6 +145,7 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
                 }
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
             }
+            if (MODE == 7 && t + 1 < nt) load_a((t + 1) * BK, i);
         }
     }
 #pragma unroll
@@ -163,17 +183,24 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const unsigned grid = (unsigned)(B * tiles_n);
-    const char* names[5] = {"full split product", "G loads skipped on odd K steps (intake -1/3)",
+    const char* names[8] = {"full split product", "G loads skipped on odd K steps (intake -1/3)",
                             "no loads after the first stage", "fragments read once (no per-step LDS reads)",
-                            "one MFMA per block and step (loads + reads as full)"};
-    for (int mode = 0; mode < 5; ++mode) {
+                            "one MFMA per block and step (loads + reads as full)",
+                            "X^T loads skipped after the first stage (G every step)",
+                            "G loads skipped after the first stage (X^T every step)",
+                            "X^T fragments into registers one step ahead, G by LDS-DMA"};
+    for (int mode = 0; mode < 8; ++mode) {
         auto launch = [&]() {
             switch (mode) {
                 case 0: probe_kernel<0><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 case 1: probe_kernel<1><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 case 2: probe_kernel<2><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 case 3: probe_kernel<3><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
-                default: probe_kernel<4><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 5: probe_kernel<5><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 6: probe_kernel<6><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 7: probe_kernel<7><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 4: probe_kernel<4><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                default: break;
             }
         };
         for (int w = 0; w < 3; ++w) launch();
