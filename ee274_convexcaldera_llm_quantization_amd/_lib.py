@@ -178,7 +178,7 @@ def load(path: str = LIB_PATH):
         if fn is None:
             raise RuntimeError(f"{path} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.cq_abi_version() != 3 and not other:
+    if lib.cq_abi_version() != 4 and not other:
         raise RuntimeError("libcaldera_hip.so ABI version mismatch")
     _lib = lib
     return lib
@@ -500,15 +500,16 @@ def gram_f64(A, B, *, ta=False, tb=False, out=None):
 
 def spd_whiten(S: torch.Tensor, rcond2: float = 1e-30):
     """S (B, p, p) fp64 SPD (overwritten) -> (Wt32, Wt64, info) with Wt^T S Wt = I on the
-    independent columns; pivots <= rcond2 * max diag are dropped (info = their count)."""
+    independent columns; pivots <= rcond2 * max diag are dropped (info = their count).
+    Wt64 is S itself: the kernel leaves the fp64 Wt there (its Wt64 argument is scratch)."""
     _require_hip(S)
     B, p, _ = S.shape
     Wt32 = torch.empty((B, p, p), dtype=torch.float32, device=S.device)
-    Wt64 = torch.empty((B, p, p), dtype=torch.float64, device=S.device)
+    scr = torch.empty((B, p, p), dtype=torch.float64, device=S.device)
     info = torch.empty(B, dtype=torch.int32, device=S.device)
-    _check(load().cq_spd_whiten_rcond(_p(S), p, B, float(rcond2), _p(Wt32), _p(Wt64), _p(info),
+    _check(load().cq_spd_whiten_rcond(_p(S), p, B, float(rcond2), _p(Wt32), _p(scr), _p(info),
                                       _stream(S.device)), "cq_spd_whiten_rcond")
-    return Wt32, Wt64, info
+    return Wt32, S, info
 
 
 def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want64=False, want_vectors=True):

@@ -848,12 +848,11 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
     CQ_REQUIRE(S && p > 0 && batch > 0 && info && Wt64, "cq_spd_whiten: bad args (Wt64 is required scratch)");
     CQ_REQUIRE(rcond2 >= 0.0, "cq_spd_whiten: rcond2 must be >= 0");
     hipStream_t s = as_stream(stream);
-    // E is built in Wt64; the final fp64 Wt is staged in S and copied to Wt64.
+    // E is built in Wt64 (scratch); the final fp64 Wt is left in S (ABI 4: no device copy to
+    // Wt64 -- the copy was 0.46 ms per B = 256, p = 192 call, ~18 ms per config-2 step)
     const size_t wlm = (size_t)(p + 2 * 32 * 33 + 32) * sizeof(double);
     CQ_REQUIRE(wlm <= 64 * 1024, "cq_spd_whiten: p too large");
     spd_whiten_mfma_kernel<<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
-    if (hipMemcpyAsync(Wt64, S, (size_t)batch * p * p * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
-        return set_error(CQ_EHIP, "cq_spd_whiten: copy failed");
     return check_launch("cq_spd_whiten");
 }
 

@@ -1089,16 +1089,26 @@ __global__ __launch_bounds__(XW_THREADS, 1) void q_update_v_kernel(QUK q) {
 // elements per thread per step (32-byte fp16 loads, one 32-bit store of 16 two-bit codes),
 // no LDS and no MFMA, so many workgroups per CU keep HBM busy.  Same arithmetic as pass 1 of
 // the fused kernels with res = W.  n % 16 == 0; per-block fp64 error partials in part.
-template <int DT, int BITS, bool FAST>
+template <int DT, int BITS, bool FAST, bool EW>
 __device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t MN, int64_t e, const uint4 (&wr)[4],
                                               const float4 (&ewv)[4], float s, float ys, float yk, double& err) {
+    // EW: error column weights (loaded with the group's W); without them the squared errors
+    // are not multiplied by 1 (the same sums).  The 2-bit fast path dequantises as c s (k = 1:
+    // (c / 1) s is exactly c s) and packs each 8 codes by FMAs on integral floats (below 2^16,
+    // exact), as pass 1 of the fused Q update does: ~10 VALU instructions per element instead of
+    // ~20, which made this HBM stream VALU-bound (0.60 of HBM at B = 256)
     constexpr float kq = (float)((1 << (BITS - 1)) - 1);
     uint32_t pk[4] = {0u, 0u, 0u, 0u};
+    constexpr bool PK2 = BITS == 2 && FAST;
+    // 2-bit: element 8 h + 4 j' + r has weight 2^(8 j' + 6 - 2 r) in the h-th 16 bits
+    constexpr float wt[4] = {64.f, 16.f, 4.f, 1.f};
+    float a2[2] = {0.f, 0.f};
+    if (PK2) a2[0] = a2[1] = (64.f + 16.f + 4.f + 1.f) * 257.f;   // the +1 offsets of 8 codes
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         int cq[4];
+        float cf[4];
         float e4[4];
-        const float4 wv = ewv[j];   // error column weights (1 without), loaded with the group's W
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float v;
@@ -1108,13 +1118,28 @@ __device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t M
             } else {
                 v = __uint_as_float((&wr[j].x)[r]);
             }
-            const float c = FAST ? rintf(div_fast(v, s, ys) * kq) : quant_code(v, s, kq);
-            const float d = (FAST ? div_fast(c, kq, yk) * s : dequant(c, kq, s)) - v;
-            e4[r] = (d * d) * (&wv.x)[r];
-            cq[r] = (int)c;
+            float c, dq;
+            if (FAST && BITS == 2) {
+                c = rintf(div_fast(v, s, ys));
+                dq = c * s;
+            } else if (FAST) {
+                c = rintf(div_fast(v, s, ys) * kq);
+                dq = div_fast(c, kq, yk) * s;
+            } else {
+                c = quant_code(v, s, kq);
+                dq = dequant(c, kq, s);
+            }
+            const float d = dq - v;
+            e4[r] = EW ? (d * d) * (&ewv[j].x)[r] : d * d;
+            cf[r] = c;
+            if (!PK2) cq[r] = (int)c;
         }
         err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
-        if (BITS == 2) {
+        if (PK2) {
+            const float wj = (j & 1) ? 256.f : 1.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a2[j >> 1] = __builtin_fmaf(cf[r], wt[r] * wj, a2[j >> 1]);
+        } else if (BITS == 2) {
             pk[0] |= (((uint32_t)(cq[0] + 1) << 6) | ((uint32_t)(cq[1] + 1) << 4) | ((uint32_t)(cq[2] + 1) << 2) |
                       (uint32_t)(cq[3] + 1)) << (8 * j);
         } else if (BITS == 4) {
@@ -1128,11 +1153,17 @@ __device__ __forceinline__ void qstream_group(const QUK& q, int64_t b, int64_t M
             *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(q.codes) + b * MN + e + 4 * j) =
                 make_short4((short)cq[0], (short)cq[1], (short)cq[2], (short)cq[3]);
         }
-        if (BITS <= 4 && q.codes)
+        if (BITS <= 4 && q.codes) {
+            if (PK2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cq[r] = (int)cf[r];
+            }
             *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(q.codes) + b * MN + e + 4 * j) =
                 (uint32_t)(uint8_t)(int8_t)cq[0] | ((uint32_t)(uint8_t)(int8_t)cq[1] << 8) |
                 ((uint32_t)(uint8_t)(int8_t)cq[2] << 16) | ((uint32_t)(uint8_t)(int8_t)cq[3] << 24);
+        }
     }
+    if (PK2) pk[0] = (uint32_t)a2[0] | ((uint32_t)a2[1] << 16);
     if (BITS == 2 && q.packed) *reinterpret_cast<uint32_t*>(q.packed + (b * MN + e) / 4) = pk[0];
     if (BITS == 4 && q.packed) *reinterpret_cast<uint2*>(q.packed + (b * MN + e) / 2) = make_uint2(pk[0], pk[1]);
     if (BITS == 8 && q.codes)
@@ -1183,7 +1214,7 @@ __device__ __forceinline__ void qstream_load(const QUK& q, int64_t b, int64_t MN
 // 32-bit store of 16 two-bit codes), no LDS and no MFMA, so many workgroups per CU keep HBM
 // busy.  Same arithmetic as pass 1 of the fused kernels with res = W.  n % 16 == 0;
 // per-block fp64 error partials in part.
-template <int DT, int BITS>
+template <int DT, int BITS, bool EW>
 __global__ __launch_bounds__(256) void quant_w_stream_kernel(QUK q) {
     constexpr float kq = (float)((1 << (BITS - 1)) - 1);
     const int64_t b = blockIdx.y;
@@ -1196,18 +1227,26 @@ __global__ __launch_bounds__(256) void quant_w_stream_kernel(QUK q) {
     int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     // a grid stride that is a multiple of the row length (the launcher picks one when there are
     // error weights) keeps each thread on the same 16 columns: their weights are loaded once
-    const bool ewfix = q.ew && ((stride * 16) % q.n) == 0;
+    const bool ewfix = EW && ((stride * 16) % q.n) == 0;
     if (div_fast_ok(s)) {  // uniform: the common case, branch-free correctly rounded division
         uint4 nx[4];  // the next group's W (and weights), loaded while this one is quantised
         float4 nw[4];
-        if (g < ng) qstream_load<DT>(q, b, MN, g * 16, nx, nw);
-        if (ewfix) {
+        if (g < ng) qstream_load<DT>(q, b, MN, g * 16, nx, nw, EW);
+        if (!EW) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nw[u] = make_float4(1.f, 1.f, 1.f, 1.f);   // unused
+        }
+        if (ewfix || !EW) {
+            // columns fixed per thread (or no weights): W two groups ahead (~100 KB of loads in
+            // flight per CU at 6 waves per SIMD)
+            uint4 nx2[4];
+            if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx2);
             for (; g < ng; g += stride) {
                 uint4 cur[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) cur[u] = nx[u];
-                if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx);
-                qstream_group<DT, BITS, true>(q, b, MN, g * 16, cur, nw, s, ys, yk, err);
+                for (int u = 0; u < 4; ++u) { cur[u] = nx[u]; nx[u] = nx2[u]; }
+                if (g + 2 * stride < ng) qstream_load<DT>(q, b, MN, (g + 2 * stride) * 16, nx2);
+                qstream_group<DT, BITS, true, EW>(q, b, MN, g * 16, cur, nw, s, ys, yk, err);
             }
         }
         for (; g < ng; g += stride) {
@@ -1216,14 +1255,18 @@ __global__ __launch_bounds__(256) void quant_w_stream_kernel(QUK q) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) { cur[u] = nx[u]; cw[u] = nw[u]; }
             if (g + stride < ng) qstream_load<DT>(q, b, MN, (g + stride) * 16, nx, nw);
-            qstream_group<DT, BITS, true>(q, b, MN, g * 16, cur, cw, s, ys, yk, err);
+            qstream_group<DT, BITS, true, EW>(q, b, MN, g * 16, cur, cw, s, ys, yk, err);
         }
     } else {  // non-finite / subnormal scale: IEEE divisions
         for (; g < ng; g += stride) {
             uint4 w0[4];
             float4 ew0[4];
-            qstream_load<DT>(q, b, MN, g * 16, w0, ew0);
-            qstream_group<DT, BITS, false>(q, b, MN, g * 16, w0, ew0, s, ys, yk, err);
+            qstream_load<DT>(q, b, MN, g * 16, w0, ew0, EW);
+            if (!EW) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ew0[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+            }
+            qstream_group<DT, BITS, false, EW>(q, b, MN, g * 16, w0, ew0, s, ys, yk, err);
         }
     }
     if (q.part) {
@@ -1847,7 +1890,8 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
         }
         CQ_REQUIRE(batch < 65536, "cq_q_update_x3: batch too large");
         const dim3 sg((unsigned)gx, (unsigned)batch);
-#define CQ_QS(DT, B) quant_w_stream_kernel<DT, B><<<sg, 256, 0, s>>>(q)
+#define CQ_QS(DT, B) do { if (q.ew) quant_w_stream_kernel<DT, B, true><<<sg, 256, 0, s>>>(q); \
+                             else quant_w_stream_kernel<DT, B, false><<<sg, 256, 0, s>>>(q); } while (0)
         if (dtype == CQ_F16) {
             switch (bits) { case 2: CQ_QS(CQ_F16, 2); break; case 4: CQ_QS(CQ_F16, 4); break;
                             case 8: CQ_QS(CQ_F16, 8); break; default: CQ_QS(CQ_F16, 16); }

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CQ_ABI_VERSION 3
+#define CQ_ABI_VERSION 4
 
 #define CQ_OK 0
 #define CQ_EINVAL (-1)   /* bad argument (shape, bits, null pointer) */
@@ -205,7 +205,9 @@ int cq_gram_f64(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, 
 
 /* SPD whitening by symmetric Gaussian elimination (Cholesky-equivalent):
  * for each b, finds upper-triangular Wt (p x p) with Wt^T S Wt = I, written as fp32
- * (Wt32) and/or fp64 (Wt64).  S is overwritten.  A pivot <= rcond2 * max_j S_jj (or not
+ * (Wt32, may be NULL) and as fp64 over S itself (S is overwritten by Wt).  Wt64 (p x p fp64
+ * per matrix) is required scratch; its content is undefined on return (ABI 4: through ABI 3
+ * the fp64 Wt was also copied there).  A pivot <= rcond2 * max_j S_jj (or not
  * positive) marks a column dependent on the previous ones: it is dropped (its Wt column is
  * 0), so Wt Wt^T is a generalised inverse and (A^T A) x = A^T y solved through it gives the
  * basic least-squares solution — torch.linalg.lstsq's gelsy semantics (rcond = eps * max(m,

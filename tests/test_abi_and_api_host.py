@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(K.EXPORTS), set(names) ^ set(K.EXPORTS)
-    assert lib.cq_abi_version() == 3
+    assert lib.cq_abi_version() == 4
     assert isinstance(lib.cq_last_error(), bytes)
 
 

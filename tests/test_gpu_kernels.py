@@ -1016,19 +1016,23 @@ def test_gram_sym_split_output(K, n, kd):
         assert tol <= 2.0 ** -22 * float(Gr.abs().max())  # still fp32-grade
 
 
+@pytest.mark.parametrize("weighted", [True, False])
 @pytest.mark.parametrize("n", [1040, 1024, 4096])
 @pytest.mark.parametrize("bits", [2, 4, 8, 16])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
-def test_q_update_known_absmax_stream(K, bits, dtype, n):
+def test_q_update_known_absmax_stream(K, bits, dtype, n, weighted):
     """First Q step with max|W| known (streaming kernel, one pass) == the two-pass fused
-    update: identical codes and scale, error equal to fp64 summation order.  n = 1024 / 4096:
-    the grid stride is a whole number of rows (each thread's error weights loaded once);
-    n = 1040: it is not (weights loaded per group)."""
+    update: identical codes, packed codes and scale, error equal to fp64 summation order.
+    n = 1024 / 4096: the grid stride is a whole number of rows (each thread's error weights
+    loaded once); n = 1040: it is not (weights loaded per group).  Unweighted: the kernel's
+    no-weights instantiation (2-bit codes packed by FMAs, W two groups ahead)."""
     g = torch.Generator(device=DEV).manual_seed(5)
     B, m = 3, 192
     W = (torch.randn(B, m, n, device=DEV, generator=g) * 0.02).to(dtype)
     W[1, 7, 33] = 0.5  # a planted maximum
     ew = torch.rand(n, device=DEV, generator=g) + 0.5
+    if not weighted:
+        ew = None
     packed = bits <= 4
     outs = []
     for amax in (None, K.absmax(W)):
