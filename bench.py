@@ -490,6 +490,8 @@ def main():
                     help="per LR update, '+'-separated filter degrees of extra outer iterations after "
                          "convergence, updates separated by ',' (e.g. '6' or '6+4,4')")
     ap.add_argument("--no-l-split", action="store_true", help="sparse Gram without the l-split ELL (A/B)")
+    ap.add_argument("--no-transposed-output", action="store_true",
+                    help="solver products without the C^T epilogue output (transpose passes instead; A/B)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: api's choice)")
     ap.add_argument("--dry-run", action="store_true",
@@ -527,6 +529,8 @@ def main():
     if args.no_l_split:
         from ee274_convexcaldera_llm_quantization_amd import sgram
         sgram.L_SPLIT = False
+    if args.no_transposed_output:
+        solver.TRANSPOSED_OUT = False
     qp = make_params(wl)
     ep = EngineParams.from_caldera_params(qp)
     B = args.batch or wl["batch"]

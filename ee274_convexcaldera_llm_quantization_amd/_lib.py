@@ -72,6 +72,8 @@ class X3Args(ctypes.Structure):
         ("b_exact", c_int),
         ("colw", c_vp),
         ("absmax_out", c_vp),
+        ("Ct", c_vp),
+        ("stride_ct", c_i64),
     ]
 
 
@@ -696,7 +698,7 @@ AUTO_SPLIT_K = True
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
             out_h=None, out_l=None, out_scale=1.0, overflow=None, tri=False, b_blocked=False, active=None,
             a_blocked=False, o_blocked=False, sym_bound=None, scale_out=None, inv_out=None, lda=None, M=None,
-            single=False, ksplit=None, b_exact=False, colw=None, absmax_out=None):
+            single=False, ksplit=None, b_exact=False, colw=None, absmax_out=None, Ct=None):
     """C (B, M, N) = alpha * A B^T * inv_scale + beta P + gamma D with A = Ah + Al (B, M, K) and
     B = Bh + Bl (B, N, K) fp16 halves (b_blocked: in the K-blocked layout of sym_split_f16,
     same storage size); optional fp16 split of C into out_h/out_l.
@@ -707,7 +709,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     under a split scale >= 1); Bl is not read and may be None.  colw (N,) fp32: the product
     term of column j scaled by colw[j] (before beta P + gamma D).  absmax_out (B,) int32/uint32/fp32
     (plain products): zeroed here, receives the bits of max|C[b]| (pow2_from_absmax turns them
-    into the next split's scale without a pass over C)."""
+    into the next split's scale without a pass over C).  Ct (B, N, M) fp32: C^T as well (not
+    with tri / sym_out; C required)."""
     assert Bl is not None or b_exact or single
     _require_hip(Ah, Al, Bh, Bl, C)
     Bt, MA, Kd = Ah.shape
@@ -751,6 +754,10 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
         assert absmax_out.numel() == Bt and absmax_out.element_size() == 4 and absmax_out.is_contiguous()
         absmax_out.zero_()
         g.absmax_out = absmax_out.data_ptr()
+    if Ct is not None:
+        _require_hip(Ct)
+        assert C is not None and not tri and Ct.dtype == torch.float32 and Ct.is_contiguous() and Ct.shape == (Bt, N, M)
+        g.Ct, g.stride_ct = Ct.data_ptr(), N * M
     # split-K where the batch has fewer output tiles than the chip has CUs (one caldera() call:
     # the filter's 192 x 4096 product is 11 tiles): chunks of >= 8 K steps, ~512 workgroups.
     # The chunked sum has another fp32 summation order than the one-pass product, so a matrix

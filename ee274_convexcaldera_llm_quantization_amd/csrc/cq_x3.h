@@ -37,6 +37,7 @@ struct X3K {
     float* part;               // [ksplit][batch][M][N]
     const float* colw = nullptr;  // [N] (or NULL): the product term scaled per C column
     uint32_t* absmax_out = nullptr;  // [batch] (or NULL, plain products): atomic max of |C| bits
+    float* Ct = nullptr; int64_t sct = 0;  // C^T too (N x M, row stride M), batch stride sct
 };
 
 using f16x8g = __attribute__((ext_vector_type(8))) _Float16;

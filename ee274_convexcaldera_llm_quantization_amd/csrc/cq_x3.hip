@@ -636,6 +636,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
                     v[0] += ga_ * dv.x; v[1] += ga_ * dv.y; v[2] += ga_ * dv.z; v[3] += ga_ * dv.w;
                 }
                 *reinterpret_cast<float4*>(a.C + b * a.sc + row * a.ldc + col) = make_float4(v[0], v[1], v[2], v[3]);
+                if (a.Ct) {   // C^T: lanes l16 (consecutive rows) make 64-byte runs per column
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) a.Ct[b * a.sct + (col + r) * a.M + row] = v[r];
+                }
                 if (a.absmax_out)
                     amx = max(amx, max(max(abs_bits(v[0]), abs_bits(v[1])), max(abs_bits(v[2]), abs_bits(v[3]))));
                 if (a.Oh) {
@@ -661,6 +665,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
                     if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + c];
                     if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + c];
                     a.C[b * a.sc + row * a.ldc + c] = w;
+                    if (a.Ct) a.Ct[b * a.sct + c * a.M + row] = w;
                     amx = max(amx, abs_bits(w));
                     if (a.Oh) {
                         const float hs = w * a.out_scale;
@@ -828,6 +833,7 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
         if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + col + r];
         if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + col + r];
         a.C[b * a.sc + row * a.ldc + col + r] = w;
+        if (a.Ct) a.Ct[b * a.sct + (col + r) * a.M + row] = w;
         amx = max(amx, abs_bits(w));
         if (a.Oh) {
             const float hs = w * a.out_scale;
@@ -2011,6 +2017,9 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     a.single = g->single;
     a.colw = g->colw;
     a.absmax_out = g->absmax_out;
+    a.Ct = g->Ct;
+    a.sct = g->stride_ct;
+    CQ_REQUIRE(!g->Ct || (!g->sym_out && !g->tri && g->C), "cq_gemm_x3: Ct needs a non-symmetric product with C");
     CQ_REQUIRE(!g->absmax_out || (!g->sym_out && !g->tri), "cq_gemm_x3: absmax_out needs a plain product");
     CQ_REQUIRE(!g->colw || (!g->sym_out && !g->tri), "cq_gemm_x3: colw needs a plain product");
     // single + sym_out: the Gram of an exactly-fp16 operand (lo = 0; A = W W^T of the sparse-code
@@ -2047,7 +2056,7 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
     CQ_REQUIRE(total < (1ll << 31), "cq_gemm_x3: grid too large");
     // the 256 x 256 tile where the 192 x 384 one would leave over 15 % of its MFMA work idle
     // (rank-256 products), for plain split products
-    const bool sq = !a.single && !g->b_exact && !a.tri && !a.sym_out && a.ksplit == 1 && !a.P && !a.D && !a.Oh &&
+    const bool sq = !a.single && !g->b_exact && !a.tri && !a.sym_out && a.ksplit == 1 && !a.P && !a.D && !a.Oh && !a.Ct &&
                     !a.colw && !a.active && g->M % XS_BM == 0 && g->N % XS_BN == 0 && g->ldc % 4 == 0 &&
                     g->stride_c % 4 == 0 && (reinterpret_cast<uintptr_t>(g->C) & 15) == 0 &&
                     (double)(a.tiles_m * XW_BM) * (double)(a.tiles_n * XW_BN) > 1.15 * (double)g->M * (double)g->N;

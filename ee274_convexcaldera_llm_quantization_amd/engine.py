@@ -29,6 +29,7 @@ from .overlap import run_to_end
 from . import scratch
 from . import sgram
 from .solver import GRAM_PROBE, LPLR_PROBE, QUANT_PROBE, X3_SCALE, RandSVD, RankRSolver
+from . import solver as _solver
 
 
 @dataclass
@@ -701,9 +702,11 @@ class CalderaEngine:
             cv = scratch.get("lr.utc", (B, r, m), torch.float32, L.device)
             K.codes_matmul(st.Qc, m, n, X, r, cv, trans=True)
             Lt = torch.empty((B, r, m), dtype=torch.float32, device=L.device)
+            lc = L.is_contiguous() and _solver.TRANSPOSED_OUT   # L^T's product also writes L (Ct): no transpose pass
             K.gemm_x3(xh, xl, self._wth, self._wtl, 1.0 / (self._ysw * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
-                      lda=p, M=r, D=cv, gamma_v=-st.Qs, b_exact=self._wtl is None)
-            K.transpose_split(Lt, out=L)
+                      lda=p, M=r, D=cv, gamma_v=-st.Qs, b_exact=self._wtl is None, Ct=L if lc else None)
+            if not lc:
+                K.transpose_split(Lt, out=L)
             return
         if self._yrh is None or isinstance(sv, RandSVD) or sv.direct:
             K.gemm(Ysrc, V, C=L)
@@ -713,9 +716,11 @@ class CalderaEngine:
         r = L.shape[2]
         xh, xl = sv.split_block_t(X)
         Lt = torch.empty((B, r, L.shape[1]), dtype=torch.float32, device=L.device)
+        lc = L.is_contiguous() and _solver.TRANSPOSED_OUT
         K.gemm_x3(xh, xl, self._yrh, self._yrl, 1.0 / (self._ys * X3_SCALE), Lt, a_blocked=True, b_blocked=True,
-                  lda=p, M=r)
-        K.transpose_split(Lt, out=L)
+                  lda=p, M=r, Ct=L if lc else None)
+        if not lc:
+            K.transpose_split(Lt, out=L)
 
     def _ut_w(self, sv, R, st, ycol):
         """R~ = U^T Y = (U^T W) diag(ycol) - s (U^T c) diag(ycol) (m <= n, 2-bit Q = s c): the first

@@ -38,6 +38,12 @@ from . import scratch
 from .overlap import run_to_end
 
 
+
+# the filter's last step and the Rayleigh-Ritz product write X's k x p layout from their epilogue
+# (gemm_x3 Ct) instead of a transpose_split pass; False: the transpose passes (A/B, bench.py
+# --no-transposed-output)
+TRANSPOSED_OUT = True
+
 class _EventProbe:
     """HIP-event timing of the dominant kernel (the G X filter GEMM) on the stream it is
     launched on; used by bench.py inside its timed region (roofline.achieved).  The event
@@ -318,8 +324,9 @@ class RankRSolver:
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
             K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
             K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked,
-                      a_blocked=True, single=single and self._x3f)
-            K.transpose_split(self._xt[0], out=Z)
+                      a_blocked=True, single=single and self._x3f, Ct=Z if TRANSPOSED_OUT else None)
+            if not TRANSPOSED_OUT:
+                K.transpose_split(self._xt[0], out=Z)
         else:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
@@ -432,12 +439,15 @@ class RankRSolver:
         # the probe (bench.py's roofline) times the split-fp16 steps only: a single-product
         # step moves 2k^2 + 18pk bytes per matrix, not the 4k^2 + 20pk counted here
         probe = EVENT_PROBE.start if not single else (lambda *a: None)
+        # the last step also writes its result in X's own k x p layout (Ct): no transpose pass
+        out = self._free(X)
+        ct = out if TRANSPOSED_OUT else None
         last = deg == 1
         ev = probe(fl, nb, kn)
         K.gemm_x3(xh[0], xl[0], self._Gh, self._Gl, self._ginv, xt[1], D=xt[0], alpha_v=coef[0, 0],
                   gamma_v=coef[0, 2], out_h=None if last else xh[1], out_l=None if last else xl[1],
                   out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked, active=self._active,
-                  a_blocked=True, o_blocked=True, single=single)
+                  a_blocked=True, o_blocked=True, single=single, Ct=ct if last else None)
         EVENT_PROBE.stop(ev)
         self.stats.matvecs += 1
         prev, cur = 0, 1
@@ -448,12 +458,13 @@ class RankRSolver:
                       alpha_v=coef[i, 0], beta_v=coef[i, 1], gamma_v=coef[i, 2],
                       out_h=None if last else xh[prev], out_l=None if last else xl[prev],
                       out_scale=X3_SCALE, overflow=self._ovf, b_blocked=self._g_blocked,
-                      active=self._active, a_blocked=True, o_blocked=True, single=single)
+                      active=self._active, a_blocked=True, o_blocked=True, single=single,
+                      Ct=ct if last else None)
             EVENT_PROBE.stop(ev)
             self.stats.matvecs += 1
             prev, cur = cur, prev
-        out = self._free(X)
-        K.transpose_split(xt[cur], out=out)
+        if ct is None:
+            K.transpose_split(xt[cur], out=out)
         return out
 
     # ------------------------------------------------------------------ main entry

@@ -338,6 +338,11 @@ typedef struct cq_x3_args {
     uint32_t* absmax_out;          /* [batch] or NULL (plain products only): atomic max of the
                                       bits of |C[b]| into absmax_out[b] (zeroed by the caller):
                                       the next product's split scale without a pass over C */
+    float* Ct;                     /* N x M fp32 (row stride M, batch stride stride_ct) or NULL
+                                      (not with tri / sym_out): C^T as well (ABI 4) -- the
+                                      solver's filter and Rayleigh-Ritz products hand their
+                                      result back in the k x p layout without a transpose pass */
+    int64_t stride_ct;
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);

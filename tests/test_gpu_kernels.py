@@ -1120,3 +1120,45 @@ def test_gemm_x3_split_k_matches_one_pass(K, single, Bt, M, N, Kd, ks):
         else:
             assert torch.equal(c1[b], D[b]) and torch.equal(c2[b], D[b]) and torch.equal(h1[b], h2[b])
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("ks", [1, 5])
+@pytest.mark.parametrize("Bt,M,N,Kd", [(3, 192, 4096, 1024), (2, 200, 520, 2048), (2, 136, 1002, 512)])
+def test_gemm_x3_transposed_output(K, Bt, M, N, Kd, ks):
+    """Ct (C^T written by the same epilogue: the solver's filter and Rayleigh-Ritz products hand
+    back X's k x p layout without a transpose pass) is C transposed bit for bit -- with the full
+    filter epilogue (P, D, alpha/beta/gamma, split output, an inactive matrix), one pass and
+    split-K, and a ragged N (the scalar epilogue path)."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + ks)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g)
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g)
+    Ah, Al = K.split_f16(A.contiguous(), 2.0 ** 10, blocked=True)
+    bb = N % 8 == 0   # a ragged N (1002) takes row-major B and the scalar epilogue
+    Bh, Bl = K.split_f16(Bm.contiguous(), 2.0 ** 8, blocked=bb)
+    inv = torch.full((Bt,), 2.0 ** -18, device=DEV)
+    P = torch.randn(Bt, M, N, device=DEV, generator=g)
+    D = torch.randn(Bt, M, N, device=DEV, generator=g)
+    al = torch.rand(Bt, device=DEV, generator=g) * 1e-2
+    be = torch.rand(Bt, device=DEV, generator=g)
+    ga = torch.rand(Bt, device=DEV, generator=g)
+    active = torch.ones(Bt, dtype=torch.int32, device=DEV)
+    active[-1] = 0
+    outs = []
+    for with_t in (False, True):
+        C = torch.full((Bt, M, N), float("nan"), device=DEV)
+        Ct = torch.full((Bt, N, M), float("nan"), device=DEV) if with_t else None
+        oh = torch.empty((Bt, M, N), dtype=torch.float16, device=DEV)
+        ol = torch.empty_like(oh)
+        ovf = torch.zeros(Bt, dtype=torch.int32, device=DEV)
+        K.gemm_x3(Ah, Al, Bh, Bl, inv, C, P=P, D=D, alpha_v=al, beta_v=be, gamma_v=ga, out_h=oh, out_l=ol,
+                  out_scale=64.0, overflow=ovf, active=active, a_blocked=True, b_blocked=bb,
+                  o_blocked=N % 32 == 0, ksplit=ks if N % 4 == 0 else 1, Ct=Ct)
+        outs.append((C, oh, ol, Ct))
+    (c0, h0, l0, _), (c1, h1, l1, t1) = outs
+    assert torch.equal(c0, c1) and torch.equal(h0, h1) and torch.equal(l0, l1)
+    assert torch.equal(t1, c1.transpose(1, 2))
+    # plain product (no epilogue terms) on the same operands
+    C = torch.empty((Bt, M, N), device=DEV)
+    Ct = torch.empty((Bt, N, M), device=DEV)
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C, a_blocked=True, b_blocked=bb, Ct=Ct, ksplit=1)
+    assert torch.equal(Ct, C.transpose(1, 2))

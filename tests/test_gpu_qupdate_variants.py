@@ -139,3 +139,34 @@ def test_q_update_single_recompute_matches_two_pass(case, weighted):
                     assert abs(e[i].item() - e0[i].item()) <= 1e-12 * e0[i].item(), (name, i)
                 else:
                     assert abs(e[i].item() - e0[i].item()) <= 1e-7 * e0[i].item(), (name, i, e[i].item(), e0[i].item())
+
+
+def test_q_update_list_path_nan_residual_falls_back():
+    """A NaN residual (a NaN in W) on the single-recompute path: pass 2's |res| max skips NaN
+    (v_max3 with |.| modifiers), so the matrix is sent to pass 1 through its NaN error sum,
+    with a NaN absmax, as the two-pass form has it: same packed codes, a NaN scale and error
+    for that matrix, the other matrices of the batch untouched and on the list path."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    tag, B, m, n, r, bits, dt = LIST_CASES[0]
+    dev = torch.device("cuda:0")
+    W, L, R = C.make(B, m, n, r, dt, seed=99)
+    W, L, R = W.to(dev), L.to(dev), R.to(dev)
+    W[0, 5, 17] = float("nan")
+
+    def call(hint):
+        packed = torch.empty(B, m * n // 4, dtype=torch.uint8, device=dev)
+        err = torch.empty(B, dtype=torch.float64, device=dev)
+        scale = torch.empty(B, device=dev)
+        fb = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        K.q_update_x3(W, L, R, 2, packed=packed, scale=scale, err_out=err, scale_hint=hint, fallback_out=fb)
+        torch.cuda.synchronize()
+        return packed.cpu(), scale.cpu(), err.cpu(), fb.cpu()
+
+    p0, s0, e0, _ = call(None)
+    assert torch.isnan(s0[0]) and torch.isnan(e0[0])
+    hint = torch.where(torch.isnan(s0), torch.ones_like(s0), s0).to(dev)
+    p, s, e, fb = call(hint)
+    assert fb.tolist() == [1] + [0] * (B - 1)
+    assert torch.equal(p, p0)
+    assert torch.isnan(s[0]) and torch.isnan(e[0])
+    assert torch.equal(s[1:], s0[1:])

@@ -41,9 +41,10 @@ for spec in sys.argv[3:]:
     st = eng.solver.stats
     rels = [v for k, v in par.items() if k.startswith("seed") and isinstance(v, float)]
     fc = par.get("final_codes_summary", {})
+    fx = par.get("final_codes_vs_exact_lr", {})
     print(f"{spec:44s} {B / el:7.1f} matrices/s {1000 * el:8.1f} ms  matvecs {st.matvecs:4d} outer {st.outer:3d}  "
           f"stalls {st.stalls}  rel(seeds) max {max(rels):.2e} median {sorted(rels)[len(rels) // 2]:.2e}  "
           f"codes bit-exact {fc.get('bit_exact')}/{fc.get('matrices')} near-tie flips {fc.get('flips_at_near_ties')} "
-          f"unexplained rows {fc.get('rows_unexplained')}", flush=True)
+          f"unexplained rows {fc.get('rows_unexplained')}  vs exact LR {fx.get('bit_exact')}/{fx.get('matrices')}", flush=True)
     del decs, eng
     torch.cuda.empty_cache()
