@@ -626,281 +626,6 @@ __global__ __launch_bounds__(NW * 64, 1) void q_update_p_kernel(QUK q, const uin
 }
 
 
-// list path geometry at K <= 128 (see qp_launch_cand)
-constexpr int QP_CAND_NW_SMALL = 12;
-constexpr int QP_CAND_ROWS_SMALL = QP_CAND_NW_SMALL * 32;   // rows per panel at K <= 128
-constexpr bool QP_PC = false;  // pass 2 at K <= 128 by the producer/consumer kernel: measured slower (below)
-
-// ------------------------------------------------------------------ pass 2, producer / consumer
-// The list-path pass 2 at K <= 128 with the roles split between the 12 waves of a workgroup
-// (VERDICT r04 #4): waves 0-7 (two per SIMD) only multiply -- each holds the L fragments of 3
-// row blocks (48 of the panel's 384 rows) and computes their L R chunk on split-fp16 MFMAs from
-// the shared R^T stage, writing the fp32 products to an LDS hand-off buffer -- and waves 8-11
-// (one per SIMD) only run the epilogue: each takes 96 rows (three list regions of 32 rows) of
-// the PREVIOUS chunk's products from the other hand-off buffer, its W straight from HBM into
-// registers (two chunks ahead; no W ring in LDS), and forms the residual, |res| max, the error
-// with code 0 and the two candidate lists exactly as qp_body's pass 2 does.  One barrier per
-// chunk; the multiply of chunk ch and the epilogue of chunk ch - 1 run side by side on every
-// SIMD instead of in lockstep.  The MFMA order per accumulator (K steps; al x lh, ah x ll,
-// ah x lh) and the per-element arithmetic are qp_body's, and a region's list entries come in
-// the same (chunk, row block, lane) order: codes, scales and lists are bit-identical.
-constexpr int QPC_PROD = 8, QPC_NW = 12;   // producer waves, waves per workgroup
-constexpr int QPC_RB = 3;                  // producer row blocks: 8 x 48 = 384 rows per panel
-constexpr int QPC_CB = 6;                  // consumer row blocks: 4 x 96 = 384
-constexpr int QPC_ROWS = 384;
-constexpr int QPC_HS = 36;                 // hand-off row stride in floats (16-B aligned rows)
-constexpr int QPC_HBUF = QPC_ROWS * QPC_HS;
-constexpr size_t qpc_lds_bytes() { return (size_t)2 * qp_rstage(4) * 2 + (size_t)2 * QPC_HBUF * 4; }
-static_assert(qpc_lds_bytes() <= QP_LDS_MAX, "producer/consumer pass 2: LDS");
-static_assert(QPC_ROWS == QP_CAND_ROWS_SMALL, "the list regions are qp_launch_cand's (32 rows, 12 per panel)");
-
-template <bool EW>
-__global__ __launch_bounds__(QPC_NW * 64, 1) void q_update_pc_kernel(QUK q, const uint16_t* __restrict__ Lh,
-                                                                   const uint16_t* __restrict__ Ll,
-                                                                   const uint16_t* __restrict__ Rh,
-                                                                   const uint16_t* __restrict__ Rl, int K,
-                                                                   int panels) {
-    extern __shared__ __attribute__((aligned(16))) char qpc_smem_raw[];
-    constexpr int KSMAX = 4, RROW = 32 * KSMAX, RSTAGE = qp_rstage(KSMAX);
-    _Float16* rst = reinterpret_cast<_Float16*>(qpc_smem_raw);
-    float* hof = reinterpret_cast<float*>(qpc_smem_raw + (size_t)2 * RSTAGE * 2);
-    const int64_t m = q.m, n = q.n, MN = m * n;
-    const int64_t total = (int64_t)panels * q.x.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
-    const int64_t b = lin / panels, panel = lin % panels;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l16 = lane & 15, lq = lane >> 4;
-    const int KS = K / 32;
-    const int64_t nchunks = n / QP_BN;
-    const int64_t prow0 = panel * QPC_ROWS;
-    const float sc = q.x.inv_scale[b];
-    const uint16_t* Rhb = Rh + b * n * (int64_t)K;
-    const uint16_t* Rlb = Rl + b * n * (int64_t)K;
-    uint32_t mx = 0u;
-    double err = 0.0;
-    if (wid < QPC_PROD) {
-        // ---------------- producer: L R of rows prow0 + 48 wid + [0, 48), chunk by chunk
-        const uint16_t* Lhb = Lh + b * m * (int64_t)K;
-        const uint16_t* Llb = Ll + b * m * (int64_t)K;
-        f16x8g lh[QPC_RB][KSMAX], ll[QPC_RB][KSMAX];
-#pragma unroll
-        for (int rb = 0; rb < QPC_RB; ++rb) {
-            const int64_t row = prow0 + 48 * wid + 16 * rb + l16;
-#pragma unroll
-            for (int ks = 0; ks < KSMAX; ++ks) {
-                if (ks < KS && row < m) {
-                    const int64_t o = row * K + 32 * ks + 8 * lq;
-                    lh[rb][ks] = *reinterpret_cast<const f16x8g*>(Lhb + o);
-                    ll[rb][ks] = *reinterpret_cast<const f16x8g*>(Llb + o);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) { lh[rb][ks][e] = (_Float16)0.f; ll[rb][ks][e] = (_Float16)0.f; }
-                }
-            }
-        }
-        const int acol0 = 8 * (l16 >> 2) + (l16 & 3);
-        qp_issue_r<QPC_PROD, RROW>(Rhb, Rlb, 0, K, rst, wid, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (int64_t it = 0; it <= nchunks; ++it) {
-            if (it < nchunks) {
-                if (it + 1 < nchunks)
-                    qp_issue_r<QPC_PROD, RROW>(Rhb, Rlb, (it + 1) * QP_BN, K, rst + ((it + 1) & 1) * RSTAGE, wid, lane);
-                const _Float16* st = rst + (it & 1) * RSTAGE;
-                f32x4v acc[QPC_RB][2];
-#pragma unroll
-                for (int rb = 0; rb < QPC_RB; ++rb)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) acc[rb][c] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < KSMAX; ++ks) {
-                    if (ks < KS) {
-                        f16x8g fh[2], fl[2];
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            fh[c] = qp_frag<RROW>(st, 0, acol0 + 4 * c, 4 * ks + lq);
-                            fl[c] = qp_frag<RROW>(st, 1, acol0 + 4 * c, 4 * ks + lq);
-                        }
-#pragma unroll
-                        for (int rb = 0; rb < QPC_RB; ++rb)
-#pragma unroll
-                            for (int c = 0; c < 2; ++c) {
-                                acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
-                                acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ll[rb][ks], acc[rb][c], 0, 0, 0);
-                                acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
-                            }
-                    }
-                }
-                // acc[rb][c][i]: row 16 rb + l16 of the wave's 48, chunk column 8 lq + 4 c + i
-                float* ho = hof + (it & 1) * QPC_HBUF;
-#pragma unroll
-                for (int rb = 0; rb < QPC_RB; ++rb) {
-                    float* d = ho + (48 * wid + 16 * rb + l16) * QPC_HS + 8 * lq;
-                    *reinterpret_cast<f32x4v*>(d) = acc[rb][0];
-                    *reinterpret_cast<f32x4v*>(d + 4) = acc[rb][1];
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // R^T stage it + 1 landed
-            }
-            __syncthreads();
-        }
-    } else {
-        // ---------------- consumer: the epilogue of rows prow0 + 96 cw + [0, 96) (list regions
-        // 3 cw .. 3 cw + 2), one chunk behind the producers
-        const int cw = wid - QPC_PROD;
-        const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * MN;
-        float tau = __builtin_inff();
-        {
-            const float h = q.hint[b];
-            if (h > 0.f && h <= 0x1p127f) tau = QP_TAU * h;
-        }
-        float mxf = 0.f;
-        const int capA = (int)q.capA, capB = (int)q.cap;
-        const int64_t region0 = (b * panels + panel) * QPC_NW + 3 * cw;
-        int gcur[3] = {0, 0, 0}, gcurA[3] = {0, 0, 0};
-        // W of chunks ch .. ch + NR - 1 in a register ring (with error column weights one chunk
-        // less ahead: their registers would not fit beside a 3-deep ring)
-        constexpr int NR = EW ? 2 : 3;
-        uint4 wr[NR][QPC_CB];
-        float4 ewr[NR][2];
-        auto wrow = [&](int k) { const int64_t row = prow0 + 96 * cw + 16 * k + l16; return row < m ? row : m - 1; };
-        // (slots are compile-time constants: a runtime index would put the ring in scratch)
-        auto load_w = [&](int64_t ch, auto S) {
-            constexpr int slot = decltype(S)::value;
-#pragma unroll
-            for (int k = 0; k < QPC_CB; ++k)
-                wr[slot][k] = *reinterpret_cast<const uint4*>(Wh + wrow(k) * n + ch * QP_BN + 8 * lq);
-            if (EW) {
-                ewr[slot][0] = *reinterpret_cast<const float4*>(q.ew + ch * QP_BN + 8 * lq);
-                ewr[slot][1] = *reinterpret_cast<const float4*>(q.ew + ch * QP_BN + 8 * lq + 4);
-            }
-        };
-        // the epilogue of chunk ch (its products in hand-off buffer ch & 1, its W in ring slot S)
-        auto step = [&](int64_t ch, auto S) {
-            constexpr int slot = decltype(S)::value;
-            const float* hi = hof + (ch & 1) * QPC_HBUF;
-            const int64_t n0 = ch * QP_BN;
-#pragma unroll
-            for (int reg = 0; reg < 3; ++reg) {
-#pragma unroll
-                for (int rb = 0; rb < 2; ++rb) {
-                    const int k = 2 * reg + rb;
-                    const int64_t row = prow0 + 96 * cw + 16 * k + l16;
-                    if (row >= m) continue;   // m % 16 == 0: the whole 16-row block
-                    const float* src = hi + (96 * cw + 16 * k + l16) * QPC_HS + 8 * lq;
-                    const f32x4v a0 = *reinterpret_cast<const f32x4v*>(src);
-                    const f32x4v a1 = *reinterpret_cast<const f32x4v*>(src + 4);
-                    float v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const uint32_t pr = (&wr[slot][k].x)[u >> 1];
-                        const float w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
-                        const float pa = u < 4 ? a0[u] : a1[u - 4];
-                        v[u] = __builtin_fmaf(-pa, sc, w);
-                    }
-                    uint64_t c[8];
-                    float e8 = 0.f;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) c[u] = __ballot(__builtin_fabsf(v[u]) >= tau);
-#pragma unroll
-                    for (int u = 0; u < 8; u += 2) mxf = qp_max3_abs(mxf, v[u], v[u + 1]);
-                    if (EW) {
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u] * v[u], (&ewr[slot][u >> 2].x)[u & 3], e8);
-                    } else {
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u], v[u], e8);
-                    }
-                    err += (double)e8;
-                    uint64_t any = c[0], two = 0;
-#pragma unroll
-                    for (int u = 1; u < 8; ++u) {
-                        two |= any & c[u];
-                        any |= c[u];
-                    }
-                    const uint64_t mA = any & ~two, mB = two;
-                    if (mA | mB) {
-                        const int64_t region = region0 + reg;
-                        const int64_t e = row * n + n0 + 8 * lq;
-                        if (__builtin_amdgcn_inverse_ballot_w64(mA)) {
-                            const int pos = gcurA[reg] + (int)__builtin_amdgcn_mbcnt_hi(
-                                (uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0u));
-                            if (pos < capA) {
-                                const bool b0 = __builtin_amdgcn_inverse_ballot_w64(c[1] | c[3] | c[5] | c[7]);
-                                const bool b1 = __builtin_amdgcn_inverse_ballot_w64(c[2] | c[3] | c[6] | c[7]);
-                                const bool b2 = __builtin_amdgcn_inverse_ballot_w64(c[4] | c[5] | c[6] | c[7]);
-                                const uint32_t u1 = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
-                                const float p0 = b0 ? v[1] : v[0], p1 = b0 ? v[3] : v[2];
-                                const float p2 = b0 ? v[5] : v[4], p3 = b0 ? v[7] : v[6];
-                                const float x1 = b2 ? (b1 ? p3 : p2) : (b1 ? p1 : p0);
-                                q.la[region * q.capA + pos] = make_uint2((uint32_t)e + u1, __float_as_uint(x1));
-                            }
-                        }
-                        if (__builtin_amdgcn_inverse_ballot_w64(mB)) {
-                            const int pos = gcur[reg] + (int)__builtin_amdgcn_mbcnt_hi(
-                                (uint32_t)(mB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mB, 0u));
-                            if (pos < capB) {
-                                float4* gv = q.gval + 2 * (region * q.cap + pos);
-                                gv[0] = make_float4(v[0], v[1], v[2], v[3]);
-                                gv[1] = make_float4(v[4], v[5], v[6], v[7]);
-                                q.gid[region * q.cap + pos] = (uint32_t)e;
-                            }
-                        }
-                        gcurA[reg] += __builtin_popcountll(mA);
-                        gcur[reg] += __builtin_popcountll(mB);
-                    }
-                }
-            }
-            // W NR - 1 chunks ahead, issued after this chunk's list stores (a register load's
-            // wait then covers only what came before it)
-            if (ch + NR - 1 < nchunks) load_w(ch + NR - 1, std::integral_constant<int, (slot + NR - 1) % NR>{});
-            __syncthreads();
-        };
-        using S0 = std::integral_constant<int, 0>;
-        using S1 = std::integral_constant<int, 1>;
-        using S2 = std::integral_constant<int, 2 % NR>;
-        load_w(0, S0{});
-        if (NR == 3 && nchunks > 1) load_w(1, S1{});
-        // barriers: the producers' prologue (R^T stage 0 landed) and iteration 0 (chunk 0's
-        // products written); then one per chunk -- nchunks + 2 on both sides
-        __syncthreads();
-        __syncthreads();
-        // iterations 1 .. nchunks: chunk ch = it - 1 in slot ch % NR (one barrier each, as the
-        // producers)
-        int64_t ch = 0;
-        for (; ch + NR <= nchunks; ch += NR) {
-            step(ch, S0{});
-            step(ch + 1, S1{});
-            if (NR == 3) step(ch + 2, S2{});
-        }
-        if (ch < nchunks) step(ch++, S0{});
-        if (NR == 3 && ch < nchunks) step(ch++, S1{});
-        mx = __float_as_uint(mxf);
-        if (lane == 0) {
-#pragma unroll
-            for (int reg = 0; reg < 3; ++reg) {
-                const int64_t region = region0 + reg;
-                q.cnt[region] = (uint32_t)(gcur[reg] <= capB ? gcur[reg] : capB);
-                q.cntA[region] = (uint32_t)(gcurA[reg] <= capA ? gcurA[reg] : capA);
-                if (gcur[reg] > capB || gcurA[reg] > capA) q.ovf[b] = 1u;
-            }
-        }
-    }
-    mx = wave_max_u32(mx);
-    if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
-    __shared__ double red2[16];
-    const double tsum = block_sum_f64(err, red2);
-    if (tid == 0) {
-        q.part0[b * panels + panel] = tsum;
-        if (tsum != tsum) {   // a NaN residual: pass 1 with a NaN absmax (as qp_body)
-            q.ovf[b] = 1u;
-            atomicMax(q.absmax + b, 0x7fffffffu);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ list path: codes + error
 // One workgroup per wave region of pass 2 (rpw rows x n): the region's packed 2-bit codes are
 // built in LDS (all code 0 = offset-binary 01, then each nonzero code of a listed group flips
@@ -1007,6 +732,7 @@ __global__ void qp_finalize_cand_kernel(QUK q, int panels, int nw, float* scale,
 
 // list path geometry: K <= 128 runs 12 waves of 2 row blocks (three waves per SIMD at <= 168
 // VGPRs: the fragments are read per K step instead of up front), K <= 256 8 waves of 2
+constexpr int QP_CAND_NW_SMALL = 12;
 int qp_cand_rows(int K) { (void)K; return 32; }
 int qp_cand_waves(int K) { return K <= 128 ? QP_CAND_NW_SMALL : QP_WAVES; }
 
@@ -1032,14 +758,7 @@ int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uin
     q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, NWV, true><<<PS == 2 ? g : gf, NWV * 64,    \
         qp_lds_bytes(NWV, RBV, KSV, true), s>>>(                                           \
         q, Lh, Ll, Rth, Rtl, K, (int)panels)
-    if (small && QP_PC) {
-        if (q.ew) q_update_pc_kernel<true><<<g, QPC_NW * 64, qpc_lds_bytes(), s>>>(q, Lh, Ll, Rth, Rtl, K, (int)panels);
-        else q_update_pc_kernel<false><<<g, QPC_NW * 64, qpc_lds_bytes(), s>>>(q, Lh, Ll, Rth, Rtl, K, (int)panels);
-    } else if (small) {
-        CQ_QPC(2, 2, 4, QP_CAND_NW_SMALL);
-    } else {
-        CQ_QPC(2, 2, 8, QP_WAVES);
-    }
+    if (small) CQ_QPC(2, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(2, 2, 8, QP_WAVES);
     qp_codes_kernel<<<(unsigned)(panels * batch * nw), 256, lds, s>>>(q, (int)panels, nw, rpw);
     q.only_fallback = 1;
     if (small) CQ_QPC(1, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(1, 2, 8, QP_WAVES);
