@@ -493,7 +493,8 @@ def main():
     ap.add_argument("--no-transposed-output", action="store_true",
                     help="solver products without the C^T epilogue output (transpose passes instead; A/B)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="batch parts interleaved on separate HIP streams (default: api's choice)")
+                    help="batch parts interleaved on separate HIP streams (default: overlap.default_parts, "
+                         "2 from 32 matrices on)")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing test of the N-rank path: gloo on the CPU, a stub decomposer on tiny "
                          "matrices (no HIP device); the JSON line says dry_run")
@@ -523,7 +524,7 @@ def main():
 
     from ee274_convexcaldera_llm_quantization_amd import api, solver
     from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
-    from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
+    from ee274_convexcaldera_llm_quantization_amd.overlap import default_parts, run_interleaved
     import ee274_convexcaldera_llm_quantization_amd._lib as K
     K.load()
     if args.no_l_split:
@@ -541,22 +542,23 @@ def main():
     Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev, host=PINNED if rank == 0 else 0)
     h = make_h(wl)
     h = None if h is None else h.to(dev)
-    parts = max(1, args.streams or 1)
+    parts = max(1, args.streams or default_parts(B))
     tol_steps = tuple(float(x) for x in args.solver_tol_steps.split(",")) if args.solver_tol_steps else None
     refine_steps = (tuple(tuple(int(d) for d in x.split("+") if d) for x in args.solver_refine_steps.split(","))
                     if args.solver_refine_steps else None)
 
-    def step():
+    def step(nparts=None):
+        nparts = parts if nparts is None else nparts
         # the hot path: caldera() (alg.py:24-112) on B matrices resident in HBM, results
         # (packed Q codes + scale, L, R, dequantised Q, error history) left in HBM.  The
         # drop-in API layer adds only output placement (alg.py:81 copies W to the host); it is
         # timed separately below ("api_path").
-        engines = [CalderaEngine(ep) for _ in range(parts)]
+        engines = [CalderaEngine(ep) for _ in range(nparts)]
         for e in engines:
             e.solver_tol_steps = tol_steps
             if refine_steps is not None:
                 e.solver_refine_steps = refine_steps
-        bnd = [B * i // parts for i in range(parts + 1)]
+        bnd = [B * i // nparts for i in range(nparts + 1)]
         outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], h, True) for i, e in enumerate(engines)], dev)
         # no reference cycles: the previous step's buffers must be freed as soon as the
         # next step drops them, or the caching allocator grows and stalls on hipMalloc
@@ -586,7 +588,7 @@ def main():
         print(f"warmup done; reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     # time the dominant kernel (the G X filter GEMMs) with HIP events on its stream
     solver.EVENT_PROBE.enable(True)
-    solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * max(1, args.streams or 1))
+    solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * parts)
     solver.LPLR_PROBE.enable(wl["L_bits"] < 16, max_pairs=64)
     solver.GRAM_PROBE.enable(True, max_pairs=16 * args.steps * parts)
     gather_stats.update(ms=0.0, calls=0)
@@ -633,7 +635,10 @@ def main():
         "config": {"workload": wl["desc"], "name": args.workload,
                    "batch_per_gpu": B, "matrices_per_step": B * world, "parallelism": f"dp{world} (matrix-sharded)"},
     }
-    if probe["count"]:
+    solver_p = eng.solver.p if eng.solver is not None else None
+
+    def roofline_of(probe, launch_batch):
+        """The dominant kernel's roofline from a probe summary (HIP events on its stream)."""
         t = probe["avg_ms"] * 1e-3
         flops, nbytes = probe["flops_per_launch"], probe["bytes_per_launch"]
         x3 = probe["kernel"].startswith("gemm_x3")
@@ -643,12 +648,12 @@ def main():
         t_hbm = nbytes / (PEAK_HBM_GBS * 1e9)
         traffic = None  # HBM bytes per launch from the committed PMC pass of this same config
         pmc_path = os.path.join(ROOT, "bench_pmc_traffic.json")  # travels to the GPU box (profiles/ does not)
-        solver_p = eng.solver.p if eng.solver is not None else None
         if os.path.exists(pmc_path):
-            pm = json.load(open(pmc_path))
-            if (pm["config"]["batch"] == B // parts and pm["config"]["p"] == solver_p
-                    and pm["config"].get("workload", "cfg2") == args.workload and pm["kernel"] == probe["kernel"]):
-                traffic = pm["hbm_bytes_per_launch"]
+            pms = json.load(open(pmc_path))
+            for pm in (pms if isinstance(pms, list) else [pms]):
+                if (pm["config"]["batch"] == launch_batch and pm["config"]["p"] == solver_p
+                        and pm["config"].get("workload", "cfg2") == args.workload and pm["kernel"] == probe["kernel"]):
+                    traffic = pm["hbm_bytes_per_launch"]
         ach_tf = flops / t / 1e12
         ach_gb = nbytes / t / 1e9
         if t_hbm >= t_mfma:
@@ -660,8 +665,18 @@ def main():
         roof.update({"traffic": traffic, "kernel": probe["kernel"], "launches_timed": probe["count"],
                      "avg_launch_ms": probe["avg_ms"], "bytes_per_launch": nbytes,
                      "flops_per_launch_fp32_equiv": flops, "achieved_tflops_fp32_equiv": ach_tf,
-                     "mfma_frac": ach_tf / mfma_peak, "solver_block_p": solver_p})
-        result["roofline"] = roof
+                     "mfma_frac": ach_tf / mfma_peak, "solver_block_p": solver_p,
+                     "matrices_per_launch": launch_batch})
+        return roof
+
+    if probe["count"]:
+        result["roofline"] = roofline_of(probe, B // parts)
+        if parts > 1:
+            result["roofline"]["concurrency"] = (
+                f"{parts} interleaved batch parts on separate HIP streams: each launch shares the chip with the "
+                "other part's kernels (the one-CU-per-matrix eigensolves and whitening run beside it), so its "
+                "duration and this frac are per launch under that sharing; roofline_solo times the same kernel "
+                "with one part")
     # the quantise kernel (fused Q update, every pass of a call; SURVEY.md 8(d) bytes_Q per call):
     # "w" = first Q step (quantise W itself, pure HBM), "lr" = Q steps recomputing W - L R on
     # split-fp16 MFMAs (3 fp16 products per fp32-equivalent flop; one recompute on the 2-bit list path)
@@ -755,6 +770,18 @@ def main():
         result["cpu_baseline"] = cpu
         result.update(par)
     decs = eng = None
+    if parts > 1 and world == 1 and probe["count"]:
+        # the dominant kernel alone: one untimed step of the whole batch as one part (launches of
+        # B matrices, nothing beside them), HIP events as in the timed region
+        solver.EVENT_PROBE.enable(True)
+        step(1)
+        torch.cuda.synchronize()
+        solver.EVENT_PROBE.enable(False)
+        psolo = solver.EVENT_PROBE.summary()
+        if psolo["count"]:
+            result["roofline_solo"] = roofline_of(psolo, B)
+            result["roofline_solo"]["note"] = ("one untimed step of the same batch as one part (no concurrent "
+                                               "kernels): the kernel's own efficiency")
     if not args.no_api_path:
         # the drop-in API (caldera_batch: the reference's output placement, W copied to the host
         # as alg.py:81 does, dataclass assembly) on one extra step of the same resident batch

@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 
 from .engine import CalderaEngine, EngineParams
-from .overlap import run_interleaved
+from .overlap import default_parts, run_interleaved
 
 
 def _diag_of(H: torch.Tensor, n: int) -> torch.Tensor:
@@ -34,10 +34,11 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
     """Ws: list of (m, n) tensors or a (B, m, n) tensor.  H: None, (n,) diagonal, or (n, n).
 
     streams: number of parts the batch is split into, each decomposed by its own engine on
-    its own HIP stream and interleaved at host-sync points (overlap.py).  Default 1: on
-    MI355X concurrent parts measured slower (the one-CU p x p kernels need a whole CU's LDS
-    and stall behind the other part's GEMM tiles).  Results do not depend on it beyond the
-    solver tolerance."""
+    its own HIP stream and interleaved at host-sync points (overlap.py).  Default
+    `overlap.default_parts(B)`: 2 from 32 matrices on (one part's one-CU-per-matrix kernels and
+    read-backs overlap the other's products: +5-9 % on configs 2-5), else 1.  Results do not
+    depend on it beyond the solver tolerance (at large batches not at all: the parts take the
+    same kernels as the whole batch)."""
     if not torch.cuda.is_available():
         raise RuntimeError("caldera-mi355x: no HIP device available (this engine has no CPU path)")
     if decomposition_cls is None:
@@ -66,7 +67,7 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
     h = None if H is None else _diag_of(H.to(comp).float(), n)  # (n,) diagonal or (n, n) dense
     params = EngineParams.from_caldera_params(quant_params)
     if streams is None:
-        streams = 1
+        streams = default_parts(B)
     streams = max(1, min(int(streams), B))
     bounds = [B * i // streams for i in range(streams + 1)]
     engines = [CalderaEngine(params, **(engine_kwargs or {})) for _ in range(streams)]

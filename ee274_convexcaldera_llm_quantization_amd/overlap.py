@@ -26,6 +26,17 @@ def run_to_end(gen):
         return stop.value
 
 
+def default_parts(batch: int) -> int:
+    """How many interleaved parts a batch of `batch` same-shape matrices is split into by
+    default: 2 from 32 matrices on, else 1.  With ready-first interleaving and no split-K under
+    concurrency (round 5) two parts overlap one part's one-CU-per-matrix kernels (Jacobi,
+    whitening) and read-backs with the other's products: config 2 302.5 -> 316.5 matrices/s on
+    one box (`profiles/r05ab_bench_s*.log`; 4 parts 298.2), config 3 186.3 -> 202.7, config 4's
+    tall shape 180.1 -> 195.6, config 5 85.1 -> 89.0 (`profiles/r05ac_*`).  Small batches keep
+    one part: they rely on split-K, which interleaving turns off."""
+    return 2 if batch >= 32 else 1
+
+
 _STREAMS: dict = {}
 
 

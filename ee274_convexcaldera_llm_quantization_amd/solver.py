@@ -172,7 +172,8 @@ class RankRSolver:
                  tol: float = 1e-5, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 7, 6, 6, 6, 6),
                  seed: int = 0x5EED, jacobi_tol: float = 1e-7, filter_precision: str = "f16x3",
                  cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool = False,
-                 jacobi_tol_values: float = 1e-2, criterion: str = "product"):
+                 jacobi_tol_values: float = 1e-2, criterion: str = "product",
+                 jacobi_values_sweeps: int = 30):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -200,6 +201,9 @@ class RankRSolver:
         # errors ~1e-4 relative are ample for filter bounds): 243 -> 259 matrices/s
         self.jacobi_tol = jacobi_tol
         self.jacobi_tol_values = jacobi_tol_values
+        # sweep cap of the values-only eigensolves (cheap iterations: the Ritz values only set
+        # the next filter's bounds)
+        self.jacobi_values_sweeps = int(jacobi_values_sweeps)
         self.refine = ()   # extra full outer iterations after convergence (per call; engine.py)
         self.X = None      # warm-start Ritz block (B, k, p)
         self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
@@ -334,7 +338,8 @@ class RankRSolver:
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps
-            theta, _, _, sw = yield from self._eigh(T, self.jacobi_tol_values, want_vectors=False)
+            theta, _, _, sw = yield from self._eigh(T, self.jacobi_tol_values, want_vectors=False,
+                                                    max_sweeps=self.jacobi_values_sweeps)
             self._last_sw = sw
             return theta, X, None
         theta, V32, _, sw = yield from self._eigh(T, self.jacobi_tol)
@@ -345,7 +350,7 @@ class RankRSolver:
         K.gemm(Z, V32, C=Zo)
         return theta, Xo, Zo
 
-    def _eigh(self, T, tol, want_vectors=True):
+    def _eigh(self, T, tol, want_vectors=True, max_sweeps=None):
         """Rayleigh-Ritz eigensolve (descending).  p <= 192: one launch to convergence (A in
         one CU's LDS).  p > 192: block Jacobi in stages -- bj_first sweeps, then BJ_STEP at a
         time while matrices remain unconverged (one int read back per stage); bj_first follows
@@ -353,7 +358,7 @@ class RankRSolver:
         before each read-back, so batches interleaved on other streams (overlap.py) keep
         issuing while this one waits."""
         if not self.block_jacobi:
-            return K.jacobi_eigh(T, max_sweeps=JACOBI_MAX_SWEEPS, tol=tol, want_vectors=want_vectors)
+            return K.jacobi_eigh(T, max_sweeps=max_sweeps or JACOBI_MAX_SWEEPS, tol=tol, want_vectors=want_vectors)
         bj = K.BlockJacobi(T, tol, want_vectors)
         first = min(self.bj_first, JACOBI_MAX_SWEEPS)
         bj.launch(first, begin=True)
