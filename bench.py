@@ -280,7 +280,7 @@ def run_model(args):
     # solver kernels fill the chip, and two of them are interleaved at a time (HBM: ~1.2 GB of
     # scratch per 11008x4096 matrix)
     max_batch = args.model_batch or (16 if world >= 8 else 64)
-    group = 4 if max_batch <= 16 else 2
+    group = args.model_group or (4 if max_batch <= 16 else 2)
 
     def run_all(batches):
         res = []
@@ -309,7 +309,7 @@ def run_model(args):
         assert world == 1, "--emulate-world runs on one GPU"
         W_ = args.emulate_world
         mb_e = args.model_batch or (16 if W_ >= 8 else 64)
-        grp_e = 4 if mb_e <= 16 else 2
+        grp_e = args.model_group or (4 if mb_e <= 16 else 2)
 
         def run_all_e(batches):
             res = []
@@ -478,6 +478,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-api-path", action="store_true")
+    ap.add_argument("--model-group", type=int, default=None,
+                    help="model workload: same-shape batches interleaved at a time (default 4 for batches <= 16, "
+                         "else 2)")
     ap.add_argument("--model-batch", type=int, default=None,
                     help="--workload model: same-shape batch size (default 64 below 8 GPUs, 16 at 8)")
     ap.add_argument("--emulate-world", type=int, default=None,
