@@ -282,10 +282,18 @@ def run_model(args):
     max_batch = args.model_batch or (16 if world >= 8 else 64)
     group = args.model_group or (4 if max_batch <= 16 else 2)
 
+    def split_parts(grp, nparts):
+        """each same-shape batch of the group as nparts interleaved parts (engines in batch order)"""
+        out = []
+        for b in grp:
+            k = max(1, min(nparts, len(b)))
+            out += [b[len(b) * i // k:len(b) * (i + 1) // k] for i in range(k)]
+        return out
+
     def run_all(batches):
         res = []
         for g0 in range(0, len(batches), group):
-            grp = batches[g0:g0 + group]
+            grp = split_parts(batches[g0:g0 + group], args.model_parts)
             engines = [CalderaEngine(ep) for _ in grp]
             run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)], dev)
             res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"], d["R"],
@@ -314,7 +322,7 @@ def run_model(args):
         def run_all_e(batches):
             res = []
             for g0 in range(0, len(batches), grp_e):
-                grp = batches[g0:g0 + grp_e]
+                grp = split_parts(batches[g0:g0 + grp_e], args.model_parts)
                 engines = [CalderaEngine(ep) for _ in grp]
                 run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)],
                                 dev)
@@ -478,6 +486,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-api-path", action="store_true")
+    ap.add_argument("--model-parts", type=int, default=1,
+                    help="model workload: each same-shape batch as this many interleaved parts")
     ap.add_argument("--model-group", type=int, default=None,
                     help="model workload: same-shape batches interleaved at a time (default 4 for batches <= 16, "
                          "else 2)")
@@ -497,7 +507,7 @@ def main():
                     help="solver products without the C^T epilogue output (transpose passes instead; A/B)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch parts interleaved on separate HIP streams (default: overlap.default_parts, "
-                         "2 from 32 matrices on)")
+                         "2 from 16 matrices on)")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing test of the N-rank path: gloo on the CPU, a stub decomposer on tiny "
                          "matrices (no HIP device); the JSON line says dry_run")

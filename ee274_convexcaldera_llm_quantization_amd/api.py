@@ -35,8 +35,8 @@ def caldera_batch(quant_params, Ws, H=None, *, device="cuda", use_tqdm=False, sc
 
     streams: number of parts the batch is split into, each decomposed by its own engine on
     its own HIP stream and interleaved at host-sync points (overlap.py).  Default
-    `overlap.default_parts(B)`: 2 from 32 matrices on (one part's one-CU-per-matrix kernels and
-    read-backs overlap the other's products: +5-9 % on configs 2-5), else 1.  Results do not
+    `overlap.default_parts(B)`: 2 from 16 matrices on (one part's one-CU-per-matrix kernels and
+    read-backs overlap the other's products: +5-14 % on configs 2-5), else 1.  Results do not
     depend on it beyond the solver tolerance (at large batches not at all: the parts take the
     same kernels as the whole batch)."""
     if not torch.cuda.is_available():

@@ -28,13 +28,15 @@ def run_to_end(gen):
 
 def default_parts(batch: int) -> int:
     """How many interleaved parts a batch of `batch` same-shape matrices is split into by
-    default: 2 from 32 matrices on, else 1.  With ready-first interleaving and no split-K under
+    default: 2 from 16 matrices on, else 1.  With ready-first interleaving and no split-K under
     concurrency (round 5) two parts overlap one part's one-CU-per-matrix kernels (Jacobi,
-    whitening) and read-backs with the other's products: config 2 302.5 -> 316.5 matrices/s on
-    one box (`profiles/r05ab_bench_s*.log`; 4 parts 298.2), config 3 186.3 -> 202.7, config 4's
-    tall shape 180.1 -> 195.6, config 5 85.1 -> 89.0 (`profiles/r05ac_*`).  Small batches keep
-    one part: they rely on split-K, which interleaving turns off."""
-    return 2 if batch >= 32 else 1
+    whitening: a launch of B/2 matrices holds B/2 CUs) and read-backs with the other's products.
+    Config 2, one box: B = 256 302.5 -> 316.5 matrices/s (3 parts +0.6 %, 4 parts 298.2;
+    `profiles/r05ab_*`, `r05ag_*`), B = 32 211.9 -> 241.9, B = 16 157.2 -> 178.3, but B = 8
+    107.7 -> 105.5 and B = 4 67.3 -> 57.3 (`r05ah_*`: small batches rely on split-K, which
+    interleaving turns off); config 3 186.3 -> 202.7, config 4's tall shape 180.1 -> 195.6,
+    config 5 85.1 -> 89.0 (`r05ac_*`)."""
+    return 2 if batch >= 16 else 1
 
 
 _STREAMS: dict = {}
