@@ -730,243 +730,9 @@ __global__ void qp_finalize_cand_kernel(QUK q, int panels, int nw, float* scale,
     }
 }
 
-// ------------------------------------------------------------------ pass 2, software-pipelined
-// The list-path pass 2 at K <= 128 (12 waves of 2 row blocks, qp_body's geometry and regions)
-// with each wave's work skewed by one chunk: in the iteration of chunk ch a wave multiplies
-// chunk ch + 1 (its R^T stage issued two iterations ahead: three stages, so a 4-slot W ring)
-// and runs the epilogue of chunk ch on the products it kept from the previous iteration -- the
-// MFMAs and the epilogue's VALU / scalar work of one wave are independent and can overlap,
-// instead of all 12 waves multiplying, then all running the epilogue, between two barriers.
-// Same MFMA order per accumulator, the same per-element arithmetic and list order as qp_body:
-// codes, scales and lists are bit-identical.
-constexpr int QPP_WD = 4;   // W ring slots
-constexpr int QPP_NW = 12, QPP_RB = 2;
-__host__ __device__ constexpr size_t qpp_lds_bytes() {
-    return (size_t)(3 * qp_rstage(4) + QPP_WD * qp_wslot(QPP_NW, QPP_RB)) * 2 + 3 * 32 * 4;
-}
-static_assert(qpp_lds_bytes() <= QP_LDS_MAX, "pipelined pass 2: LDS");
-
-template <bool EW>
-__global__ __launch_bounds__(QPP_NW * 64, 1) void q_update_pipe_kernel(QUK q, const uint16_t* __restrict__ Lh,
-                                                                     const uint16_t* __restrict__ Ll,
-                                                                     const uint16_t* __restrict__ Rh,
-                                                                     const uint16_t* __restrict__ Rl, int K,
-                                                                     int panels) {
-    extern __shared__ __attribute__((aligned(16))) char qpp_smem_raw[];
-    constexpr int KSMAX = 4, RB = QPP_RB, NW = QPP_NW, RROW = 32 * KSMAX;
-    constexpr int RSTAGE = qp_rstage(KSMAX), WSLOT = qp_wslot(NW, RB);
-    _Float16* rst = reinterpret_cast<_Float16*>(qpp_smem_raw);
-    _Float16* wring = rst + 3 * RSTAGE;
-    float* ewslot = reinterpret_cast<float*>(wring + QPP_WD * WSLOT);
-    const int64_t m = q.m, n = q.n;
-    const int64_t total = (int64_t)panels * q.x.batch;
-    const int64_t orig = blockIdx.x;
-    const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
-    const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
-    const int64_t b = lin / panels, panel = lin % panels;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l16 = lane & 15, lq = lane >> 4;
-    const int KS = K / 32;
-    const int64_t nchunks = n / QP_BN;
-    const uint16_t* Lhb = Lh + b * m * (int64_t)K;
-    const uint16_t* Llb = Ll + b * m * (int64_t)K;
-    const uint16_t* Rhb = Rh + b * n * (int64_t)K;
-    const uint16_t* Rlb = Rl + b * n * (int64_t)K;
-    const _Float16* Wh = reinterpret_cast<const _Float16*>(q.W) + b * m * n;
-    const int64_t row0 = panel * (NW * 16 * RB) + wid * 16 * RB;
-    f16x8g lh[RB][KSMAX], ll[RB][KSMAX];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-        const int64_t row = row0 + 16 * rb + l16;
-#pragma unroll
-        for (int ks = 0; ks < KSMAX; ++ks) {
-            if (ks < KS && row < m) {
-                const int64_t o = row * K + 32 * ks + 8 * lq;
-                lh[rb][ks] = *reinterpret_cast<const f16x8g*>(Lhb + o);
-                ll[rb][ks] = *reinterpret_cast<const f16x8g*>(Llb + o);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) { lh[rb][ks][e] = (_Float16)0.f; ll[rb][ks][e] = (_Float16)0.f; }
-            }
-        }
-    }
-    const float sc = q.x.inv_scale[b];
-    float tau = __builtin_inff();
-    {
-        const float h = q.hint[b];
-        if (h > 0.f && h <= 0x1p127f) tau = QP_TAU * h;
-    }
-    float mxf = 0.f;
-    double err = 0.0;
-    const int64_t region = (b * panels + panel) * NW + wid;
-    int gcur = 0, gcurA = 0;
-    uint2* const laR = q.la + region * q.capA;
-    float4* const gvR = q.gval + 2 * region * q.cap;
-    uint32_t* const gidR = q.gid + region * q.cap;
-    const int capA = (int)q.capA, capB = (int)q.cap;
-    const int acol0 = 8 * (l16 >> 2) + (l16 & 3);
-    auto w_elem = [&](int rb, int64_t n0) {
-        const int64_t row = row0 + 16 * rb + l16;
-        return (row < m ? row : m - 1) * n + n0 + 8 * lq;
-    };
-    auto issue_r = [&](int64_t ch) {
-        qp_issue_r<NW, RROW>(Rhb, Rlb, ch * QP_BN, K, rst + (ch % 3) * RSTAGE, wid, lane);
-        if (EW && wid == 0 && lane < 8)
-            __builtin_amdgcn_global_load_lds((const void*)(q.ew + ch * QP_BN + 4 * lane),
-                                             (__attribute__((address_space(3))) void*)(ewslot + 32 * (ch % 3)), 16, 0, 0);
-    };
-    auto issue_w = [&](int64_t ch) {
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            _Float16* dst = wring + (ch % QPP_WD) * WSLOT + (wid * RB + rb) * 512;
-            __builtin_amdgcn_global_load_lds((const void*)(Wh + w_elem(rb, ch * QP_BN)),
-                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-        }
-    };
-    // the products of chunk ch (qp_body's MFMA order per accumulator)
-    auto mma = [&](int64_t ch, f32x4v (&acc)[RB][2]) {
-        const _Float16* st = rst + (ch % 3) * RSTAGE;
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) acc[rb][c] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < KSMAX; ++ks) {
-            if (ks < KS) {
-                f16x8g fh[2], fl[2];
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    fh[c] = qp_frag<RROW>(st, 0, acol0 + 4 * c, 4 * ks + lq);
-                    fl[c] = qp_frag<RROW>(st, 1, acol0 + 4 * c, 4 * ks + lq);
-                }
-#pragma unroll
-                for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
-                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ll[rb][ks], acc[rb][c], 0, 0, 0);
-                        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], lh[rb][ks], acc[rb][c], 0, 0, 0);
-                    }
-            }
-        }
-    };
-    // the epilogue of chunk ch on its products acc and W (qp_body's pass 2)
-    auto epilogue = [&](int64_t ch, const f32x4v (&acc)[RB][2], const uint4 (&wc)[RB]) {
-        const int64_t n0 = ch * QP_BN;
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const int64_t row = row0 + 16 * rb + l16;
-            if (row >= m) continue;
-            const int64_t e = row * n + n0 + 8 * lq;
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t pr = (&wc[rb].x)[u >> 1];
-                const float w = (float)__builtin_bit_cast(_Float16, (uint16_t)((u & 1) ? (pr >> 16) : (pr & 0xffffu)));
-                v[u] = __builtin_fmaf(-acc[rb][u >> 2][u & 3], sc, w);
-            }
-            uint64_t c[8];
-            float e8 = 0.f;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) c[u] = __ballot(__builtin_fabsf(v[u]) >= tau);
-#pragma unroll
-            for (int u = 0; u < 8; u += 2) mxf = qp_max3_abs(mxf, v[u], v[u + 1]);
-            if (EW) {
-                const float* wv = ewslot + 32 * (ch % 3) + 8 * lq;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u] * v[u], wv[u], e8);
-            } else {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) e8 = __builtin_fmaf(v[u], v[u], e8);
-            }
-            err += (double)e8;
-            uint64_t any = c[0], two = 0;
-#pragma unroll
-            for (int u = 1; u < 8; ++u) {
-                two |= any & c[u];
-                any |= c[u];
-            }
-            const uint64_t mA = any & ~two, mB = two;
-            if (mA | mB) {
-                if (__builtin_amdgcn_inverse_ballot_w64(mA)) {
-                    const int pos = gcurA + (int)__builtin_amdgcn_mbcnt_hi(
-                        (uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0u));
-                    if (pos < capA) {
-                        const bool b0 = __builtin_amdgcn_inverse_ballot_w64(c[1] | c[3] | c[5] | c[7]);
-                        const bool b1 = __builtin_amdgcn_inverse_ballot_w64(c[2] | c[3] | c[6] | c[7]);
-                        const bool b2 = __builtin_amdgcn_inverse_ballot_w64(c[4] | c[5] | c[6] | c[7]);
-                        const uint32_t u1 = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
-                        const float p0 = b0 ? v[1] : v[0], p1 = b0 ? v[3] : v[2];
-                        const float p2 = b0 ? v[5] : v[4], p3 = b0 ? v[7] : v[6];
-                        const float x1 = b2 ? (b1 ? p3 : p2) : (b1 ? p1 : p0);
-                        laR[pos] = make_uint2((uint32_t)e + u1, __float_as_uint(x1));
-                    }
-                }
-                if (__builtin_amdgcn_inverse_ballot_w64(mB)) {
-                    const int pos = gcur + (int)__builtin_amdgcn_mbcnt_hi(
-                        (uint32_t)(mB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mB, 0u));
-                    if (pos < capB) {
-                        gvR[2 * pos] = make_float4(v[0], v[1], v[2], v[3]);
-                        gvR[2 * pos + 1] = make_float4(v[4], v[5], v[6], v[7]);
-                        gidR[pos] = (uint32_t)e;
-                    }
-                }
-                gcurA += __builtin_popcountll(mA);
-                gcur += __builtin_popcountll(mB);
-            }
-        }
-    };
-    if (wid >= NW - 4) __builtin_amdgcn_s_setprio(1);
-    issue_r(0);
-    if (nchunks > 1) issue_r(1);
-    for (int64_t c = 0; c < QPP_WD - 1 && c < nchunks; ++c) issue_w(c);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    f32x4v acc[RB][2];
-    mma(0, acc);
-    for (int64_t ch = 0; ch < nchunks; ++ch) {
-        if (ch + 2 < nchunks) issue_r(ch + 2);
-        if (ch + QPP_WD - 1 < nchunks) issue_w(ch + QPP_WD - 1);
-        uint4 wc[RB];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-            wc[rb] = *reinterpret_cast<const uint4*>(wring + (ch % QPP_WD) * WSLOT + (wid * RB + rb) * 512 + 8 * lane);
-        f32x4v nxt[RB][2];
-        if (ch + 1 < nchunks) mma(ch + 1, nxt);
-        epilogue(ch, acc, wc);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) acc[rb][c] = nxt[rb][c];
-        // R^T stage ch + 2 (next iteration's products) and W ch + 1 landed; after list stores
-        // only a full drain is a safe wait
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    uint32_t mx = wave_max_u32(__float_as_uint(mxf));
-    if (lane == 0 && mx) atomicMax(q.absmax + b, mx);
-    if (lane == 0) {
-        q.cnt[region] = (uint32_t)(gcur <= capB ? gcur : capB);
-        q.cntA[region] = (uint32_t)(gcurA <= capA ? gcurA : capA);
-        if (gcur > capB || gcurA > capA) q.ovf[b] = 1u;
-    }
-    __shared__ double red2[16];
-    const double tsum = block_sum_f64(err, red2);
-    if (tid == 0) {
-        q.part0[b * panels + panel] = tsum;
-        if (tsum != tsum) {
-            q.ovf[b] = 1u;
-            atomicMax(q.absmax + b, 0x7fffffffu);
-        }
-    }
-}
-
 // list path geometry: K <= 128 runs 12 waves of 2 row blocks (three waves per SIMD at <= 168
 // VGPRs: the fragments are read per K step instead of up front), K <= 256 8 waves of 2
 constexpr int QP_CAND_NW_SMALL = 12;
-constexpr bool QP_PIPE = false;  // pass 2 at K <= 128 by the software-pipelined kernel: measured slower
-static_assert(QP_CAND_NW_SMALL == QPP_NW, "the pipelined pass 2 keeps the list regions");
 int qp_cand_rows(int K) { (void)K; return 32; }
 int qp_cand_waves(int K) { return K <= 128 ? QP_CAND_NW_SMALL : QP_WAVES; }
 
@@ -992,14 +758,7 @@ int64_t qp_launch_cand(QUK& q, const uint16_t* Lh, const uint16_t* Ll, const uin
     q_update_p_kernel<PS, 2, CQ_F16, RBV, KSV, NWV, true><<<PS == 2 ? g : gf, NWV * 64,    \
         qp_lds_bytes(NWV, RBV, KSV, true), s>>>(                                           \
         q, Lh, Ll, Rth, Rtl, K, (int)panels)
-    if (small && QP_PIPE) {
-        if (q.ew) q_update_pipe_kernel<true><<<g, QPP_NW * 64, qpp_lds_bytes(), s>>>(q, Lh, Ll, Rth, Rtl, K, (int)panels);
-        else q_update_pipe_kernel<false><<<g, QPP_NW * 64, qpp_lds_bytes(), s>>>(q, Lh, Ll, Rth, Rtl, K, (int)panels);
-    } else if (small) {
-        CQ_QPC(2, 2, 4, QP_CAND_NW_SMALL);
-    } else {
-        CQ_QPC(2, 2, 8, QP_WAVES);
-    }
+    if (small) CQ_QPC(2, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(2, 2, 8, QP_WAVES);
     qp_codes_kernel<<<(unsigned)(panels * batch * nw), 256, lds, s>>>(q, (int)panels, nw, rpw);
     q.only_fallback = 1;
     if (small) CQ_QPC(1, 2, 4, QP_CAND_NW_SMALL); else CQ_QPC(1, 2, 8, QP_WAVES);

@@ -9,7 +9,6 @@
 #   drain   the counted end-of-chunk wait even after list stores (timing only: with stores in
 #           flight the count does not prove the next stage landed)
 #   nostore the candidate lists classified but not stored
-#   nopipe  pass 2 at K <= 128 by qp_body (the lockstep kernel) instead of the pipelined one
 #   prio    s_setprio 1 for the second half of the waves (static priority); prio4 / prio8:
 #           for waves 4-11 / 8-11 of the 12
 #   xprio6 / xprio8 / xprio4: the same for the split-fp16 products' K loops (cq_x3.hip: waves >= 6 / 8 / 4
@@ -28,7 +27,6 @@ for v in ${@:-no_r no_w no_epi mfma1 drain nostore prio}; do
     mfma1) sed -i 's/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl\[ks\]\[c\], lh\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/; s/^\(\s*\)acc\[rb\]\[c\] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh\[ks\]\[c\], ll\[rb\]\[ks\], acc\[rb\]\[c\], 0, 0, 0);/\1(void)0;/' $f ;;
     drain) sed -i 's/^\(\s*\)if (!stored \&\& wlive) wait_vm(/\1if (wlive) wait_vm(/' $f ;;
     nostore) sed -i 's/^\(\s*\)laR\[pos\] = make_uint2/\1if (q.m < 0) laR[pos] = make_uint2/; s/^\(\s*\)gvR\[2 \* pos\] = /\1if (q.m < 0) gvR[2 * pos] = /; s/^\(\s*\)gvR\[2 \* pos + 1\] = /\1if (q.m < 0) gvR[2 * pos + 1] = /; s/^\(\s*\)gidR\[pos\] = /\1if (q.m < 0) gidR[pos] = /' $f ;;
-    nopipe) sed -i 's/^constexpr bool QP_PIPE = true; /constexpr bool QP_PIPE = false;/' $f ;;
     prio4) sed -i 's/^\(\s*\)int sw = 0;   \/\/ slot of chunk ch/\1if (wid >= 4) __builtin_amdgcn_s_setprio(1);\n\1int sw = 0;/' $f ;;
     prio8) sed -i 's/^\(\s*\)int sw = 0;   \/\/ slot of chunk ch/\1if (wid >= 8) __builtin_amdgcn_s_setprio(1);\n\1int sw = 0;/' $f ;;
     xprio*) th=${v#xprio}; g=$T/a/csrc/cq_x3.hip
