@@ -2,6 +2,7 @@
 matrices (after a warm-up step) and report the parity of seeds 0-3 (batch positions 0-3)
 against the reference's golden sketches (bench.parity_of_timed_step).
     python tools/tune_solver.py cfg2 128 "tol=1e-5" "deg_cold=(8,12,12,12)" "cheap_cold=2"
+    (--parts N: the batch as N interleaved parts, as bench.py's default two from 16 matrices)
 """
 import os
 import sys
@@ -15,6 +16,11 @@ import bench
 from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
 
 dev = torch.device("cuda", 0)
+parts = 1
+if "--parts" in sys.argv:
+    _i = sys.argv.index("--parts")
+    parts = int(sys.argv[_i + 1])
+    del sys.argv[_i:_i + 2]
 name, B = sys.argv[1], int(sys.argv[2])
 wl = bench.WORKLOADS[name]
 ep = EngineParams.from_caldera_params(bench.make_params(wl))
@@ -25,8 +31,11 @@ h = None if h is None else h.to(dev)
 
 def run(kw):
     tol = kw.pop("tol", 1e-5)
-    eng = CalderaEngine(ep, solver_tol=tol, solver_kwargs=kw)
-    return eng.run(Wb, h), eng
+    from ee274_convexcaldera_llm_quantization_amd.overlap import run_interleaved
+    engs = [CalderaEngine(ep, solver_tol=tol, solver_kwargs=dict(kw)) for _ in range(parts)]
+    bnd = [B * i // parts for i in range(parts + 1)]
+    outs = run_interleaved([e.run_iter(Wb[bnd[i]:bnd[i + 1]], h) for i, e in enumerate(engs)], dev)
+    return [d for o in outs for d in o], engs[0]
 
 
 for spec in sys.argv[3:]:
