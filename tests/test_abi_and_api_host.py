@@ -129,3 +129,12 @@ def test_diagonal_h_detection_and_weights():
     # not data-aware: H_sqrt = H -> lplr weights h^2, activation error weights h
     w3 = _Weights(h, 4, EngineParams(activation_aware_LR=False), "cpu")
     assert torch.equal(w3.lplr, h * h) and torch.equal(w3.err, h)
+
+
+def test_default_parts_policy():
+    """Batches of 16 matrices and more are decomposed as two interleaved parts by default
+    (overlap.default_parts: +13-14 % at B = 16 / 32, +5-9 % on configs 2-5), smaller ones as one
+    (they rely on split-K, which interleaving turns off: B = 8 / 4 measured slower)."""
+    from ee274_convexcaldera_llm_quantization_amd.overlap import default_parts
+    assert [default_parts(b) for b in (1, 4, 8, 15)] == [1, 1, 1, 1]
+    assert [default_parts(b) for b in (16, 32, 64, 256)] == [2, 2, 2, 2]

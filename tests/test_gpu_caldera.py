@@ -172,6 +172,28 @@ def test_stream_split_matches_single_stream():
         assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qa)) < 1e-4
 
 
+def test_default_two_parts_match_one_part():
+    """caldera_batch's default for 16 matrices is two interleaved parts (overlap.default_parts):
+    the same decompositions as one part -- the first Q bit-exact, Q + L R to the solver
+    tolerance (one part takes split-K for this small batch, two do not)."""
+    from ee274_convexcaldera_llm_quantization_amd.api import caldera_batch
+    from ee274_convexcaldera_llm_quantization_amd.overlap import default_parts
+    from src.caldera.utils.dataclasses import CalderaParams
+    assert default_parts(16) == 2
+    qp = CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=32, iters=3, update_order=["Q", "LR"],
+                       sigma_reg=1e-8)
+    g = torch.Generator().manual_seed(11)
+    W = (torch.randn(16, 384, 512, generator=g) * 0.02).half().to(DEV)
+    one = caldera_batch(qp, W, None, device=DEV, streams=1)
+    dflt = caldera_batch(qp, W, None, device=DEV)
+    for a, b in zip(one, dflt):
+        assert a.global_scale == b.global_scale
+        assert a.errors["Q"][0] == b.errors["Q"][0]
+        qa = a.Q.double() + a.L.double() @ a.R.double()
+        qb = b.Q.double() + b.L.double() @ b.R.double()
+        assert float(torch.linalg.norm(qa - qb) / torch.linalg.norm(qa)) < 1e-4
+
+
 def test_engine_reuse_is_stateless():
     """One CalderaEngine run twice on the same batch, then on another shape, then a third time
     on the first: every run starts cold (its own solver and warm start), so the repeated runs
