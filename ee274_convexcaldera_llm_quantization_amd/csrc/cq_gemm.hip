@@ -292,6 +292,75 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
     gemm_epilogue<EPI, DF16, NB>(a, acc, b, m0, n0, wm, wn, li, lk, lane);
 }
 
+// CholQR's X Wt (Wt upper triangular, K = N = 32 NBLK <= 192; solver._cholqr).  In
+// gemm_f32_kernel<TRIU> the waves of columns 0-95 skip half the K slices, but those of columns
+// 96-191 run all of them, and the SIMDs holding the latter set the time.  The measured
+// difference from the full product is 6 % (0.86 vs 0.915 ms per B = 256 call,
+// profiles/r05u_kt_kernel_stats.csv).  Here every wave owns 32 rows x all N columns (NBLK
+// blocks of 32 x 32).  A 16-deep slice t feeds only the blocks it reaches (block c: t <= 2c + 1),
+// unrolled at compile time, so the four waves carry equal work: 42 block-slices each at
+// N = 192 instead of 36 and 72.  Per output element it uses the same instruction, operands and
+// k order as gemm_f32_kernel, and the skipped terms are exact zeros, so the bits are the same
+// (test_gemm_b_triu_matches_plain).  LINEAR epilogue with alpha only.
+template <int NBLK>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_triu_kernel(KArgs a) {
+    static_assert(NBLK >= 1 && 32 * NBLK <= BN, "one 192-wide tile");
+    constexpr int NT = 2 * NBLK;   // 16-deep K slices (K = 32 NBLK)
+    __shared__ __attribute__((aligned(16))) float smem[2 * BK * LDA_S + 2 * BK * LDB_S];
+    float* As0 = smem;
+    float* Bs0 = smem + 2 * BK * LDA_S;
+    const int64_t b = blockIdx.z;
+    const int64_t m0 = (int64_t)blockIdx.y * BM;
+    const float* A = a.A + b * a.sa;
+    const float* B = a.B + b * a.sb;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int li = lane & 31, lk = lane >> 5;
+    f32x16 acc[NBLK];
+#pragma unroll
+    for (int c = 0; c < NBLK; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    float4 ra[2], rb[3];
+    load_a<false>(a, A, m0, 0, ra);
+    load_b<false, BN>(a, B, 0, 0, rb);
+    store_a<false>(As0, ra);
+    store_b<false, BN>(Bs0, rb);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < NT) {
+            load_a<false>(a, A, m0, (t + 1) * BK, ra);
+            load_b<false, BN>(a, B, 0, (t + 1) * BK, rb);
+        }
+        const float* As = As0 + cur * BK * LDA_S;
+        const float* Bs = Bs0 + cur * BK * LDB_S;
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2) {
+            const float a0 = As[(kk + lk) * LDA_S + 32 * wid + li];
+#pragma unroll
+            for (int c = t / 2; c < NBLK; ++c)
+                acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, Bs[(kk + lk) * LDB_S + 32 * c + li], acc[c], 0, 0, 0);
+        }
+        if (t + 1 < NT) {
+            store_a<false>(As0 + (1 - cur) * BK * LDA_S, ra);
+            store_b<false, BN>(Bs0 + (1 - cur) * BK * LDB_S, rb);
+        }
+        __syncthreads();
+    }
+    float* C = a.C + b * a.sc;
+    const float alpha = a.alpha_v ? a.alpha_v[b] : a.alpha;
+#pragma unroll
+    for (int c = 0; c < NBLK; ++c) {
+        const int64_t j = 32 * c + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t i = m0 + 32 * wid + (r & 3) + 8 * (r >> 2) + 4 * lk;
+            if (i < a.M) C[i * a.ldc + j] = alpha * acc[c][r];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ K-contiguous ("NT") GEMM
 // Both operands arrive with K contiguous: A row-major M x K, B stored N x K (op(B) = B^T).
 // LDS images [row][k] (row stride BK2 + 4 floats: 16 consecutive rows hit 16 distinct
@@ -538,6 +607,20 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
     }
     hipStream_t s = as_stream(stream);
     const bool ta = g->trans_a != 0, tb = g->trans_b != 0;
+    if (g->b_triu && g->N == g->K && g->N % 32 == 0 && g->N <= BN && g->beta == 0.f && !g->beta_v &&
+        g->gamma == 0.f && !g->gamma_v) {
+        // the solver's square triangular factor: balanced waves (gemm_triu_kernel)
+        const dim3 tg(1, (unsigned)ceil_div(g->M, BM), (unsigned)g->batch);
+        switch (g->N / 32) {
+            case 1: gemm_triu_kernel<1><<<tg, kGemmThreads, 0, s>>>(k); break;
+            case 2: gemm_triu_kernel<2><<<tg, kGemmThreads, 0, s>>>(k); break;
+            case 3: gemm_triu_kernel<3><<<tg, kGemmThreads, 0, s>>>(k); break;
+            case 4: gemm_triu_kernel<4><<<tg, kGemmThreads, 0, s>>>(k); break;
+            case 5: gemm_triu_kernel<5><<<tg, kGemmThreads, 0, s>>>(k); break;
+            default: gemm_triu_kernel<6><<<tg, kGemmThreads, 0, s>>>(k); break;
+        }
+        return check_launch("cq_gemm_f32");
+    }
     switch (g->epi) {
         case CQ_EPI_LINEAR:
             launch_gemm<CQ_EPI_LINEAR, false>(ta, tb, nb, grid, s, k);

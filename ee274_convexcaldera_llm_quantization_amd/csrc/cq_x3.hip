@@ -1625,7 +1625,12 @@ __global__ __launch_bounds__(256) void split_blocked_kernel(const float* __restr
 }
 
 // Batched transpose Y = X^T (X rows x cols, row-major) through a 64 x 65 LDS tile, with an
-// optional fp16 split of Y (scale s).
+// optional fp16 split of Y (scale s).  VEC (rows % 8 == 0, cols % 4 == 0, 16-byte aligned
+// buffers; the solver's k x p blocks): 16-byte loads of X, and each thread writes 8
+// consecutive Y columns of one Y row -- two 16-byte fp32 stores and one 16-byte store per
+// half -- instead of one 4-byte and two 2-byte stores per element (the tile's column reads
+// (8 g + q) x 65 + i, lane = (i, g), hit 64 different banks).  The same values either way.
+template <bool VEC>
 __global__ __launch_bounds__(256) void transpose_split_kernel(const float* __restrict__ X, int64_t rows, int64_t cols,
                                                               float* __restrict__ Y, _Float16* __restrict__ hi,
                                                               _Float16* __restrict__ lo, float s_fixed,
@@ -1635,13 +1640,56 @@ __global__ __launch_bounds__(256) void transpose_split_kernel(const float* __res
     const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
     const float* Xb = X + b * rows * cols;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int64_t ob = b * rows * cols;
+    const float s = s_v ? s_v[b] : s_fixed;
+    if constexpr (VEC) {
+        // load: 64 rows x 16 float4, 4 per thread (thread t: rows t / 16 + 16 u, float4 t % 16)
+        const int q4 = threadIdx.x & 15, rq = threadIdx.x >> 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = rq + 16 * u;
+            const int64_t r = r0 + i, c = c0 + 4 * q4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < rows && c < cols) v = *reinterpret_cast<const float4*>(Xb + r * cols + c);
+            tile[i][4 * q4] = v.x; tile[i][4 * q4 + 1] = v.y; tile[i][4 * q4 + 2] = v.z; tile[i][4 * q4 + 3] = v.w;
+        }
+        __syncthreads();
+        // store: Y row orow = c0 + i (64 of them), columns r0 + 8 g .. + 7 (g = 0..7): 512 tasks,
+        // 2 per thread; a wave covers 8 Y rows x 64 columns
+        const int g = threadIdx.x & 7, il = threadIdx.x >> 3;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = il + 32 * u;
+            const int64_t orow = c0 + i, ocol = r0 + 8 * g;
+            if (orow >= cols || ocol >= rows) continue;
+            float v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = tile[8 * g + q][i];
+            if (Y) {
+                float* yp = Y + ob + orow * rows + ocol;
+                *reinterpret_cast<float4*>(yp) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+            if (hi) {
+                _Float16 h[8], l[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float xs = v[q] * s;
+                    h[q] = (_Float16)xs;
+                    l[q] = (_Float16)(xs - (float)h[q]);
+                }
+                const int64_t o = blocked ? ob + (ocol >> 5) * cols * 32 + orow * 32 + (ocol & 31) : ob + orow * rows + ocol;
+                *reinterpret_cast<uint4*>(hi + o) = *reinterpret_cast<const uint4*>(h);
+                *reinterpret_cast<uint4*>(lo + o) = *reinterpret_cast<const uint4*>(l);
+            }
+        }
+        return;
+    }
     for (int i = ty; i < 64; i += 4) {
         const int64_t r = r0 + i, c = c0 + tx;
         tile[i][tx] = (r < rows && c < cols) ? Xb[r * cols + c] : 0.f;
     }
     __syncthreads();
-    const int64_t ob = b * rows * cols;
-    const float s = s_v ? s_v[b] : s_fixed;
     for (int i = ty; i < 64; i += 4) {
         const int64_t orow = c0 + i, ocol = r0 + tx;  // Y is cols x rows
         if (orow < cols && ocol < rows) {
@@ -1735,8 +1783,14 @@ int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch
     CQ_REQUIRE(!hi == !lo, "cq_transpose_split: hi and lo go together");
     CQ_REQUIRE(rows > 0 && cols > 0 && batch > 0 && batch < 65536, "cq_transpose_split: bad shape");
     dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64), (unsigned)batch);
-    transpose_split_kernel<<<grid, 256, 0, as_stream(stream)>>>(X, rows, cols, Y, reinterpret_cast<_Float16*>(hi),
-                                                                 reinterpret_cast<_Float16*>(lo), scale, scale_v, blocked);
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool vec = rows % 8 == 0 && cols % 4 == 0 && al16(X) && (!Y || al16(Y)) && (!hi || (al16(hi) && al16(lo)));
+    if (vec)
+        transpose_split_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(
+            X, rows, cols, Y, reinterpret_cast<_Float16*>(hi), reinterpret_cast<_Float16*>(lo), scale, scale_v, blocked);
+    else
+        transpose_split_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(
+            X, rows, cols, Y, reinterpret_cast<_Float16*>(hi), reinterpret_cast<_Float16*>(lo), scale, scale_v, blocked);
     return check_launch("cq_transpose_split");
 }
 

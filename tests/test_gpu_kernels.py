@@ -183,6 +183,10 @@ def test_gram_f64_mfma_paths(K, M, N, Kd, sym, tk):
     assert ((C.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-13
     if sym:
         assert torch.equal(C, C.transpose(1, 2))
+        # the mirrored lower tiles are the same bits the full product computes for them: a
+        # copy of A takes the non-symmetric path, which computes every tile
+        Cf = K.gram_f64(Ad, Ad.clone(), ta=tk, tb=tk)
+        assert torch.equal(C, Cf)
 
 
 def test_spd_whiten_and_jacobi(K):
@@ -418,16 +422,23 @@ def _x3_split_ref(x, s):
     return hi, lo
 
 
-def test_transpose_split_exact(K):
+@pytest.mark.parametrize("rows,cols", [(200, 130), (256, 192), (328, 100), (4096, 192)])
+def test_transpose_split_exact(K, rows, cols):
+    # (200, 130): the per-element path (cols % 4 != 0); the others take the 16-byte path
+    # (rows % 8 == 0, cols % 4 == 0), with partial 64 x 64 tiles at (328, 100)
     g = torch.Generator(device=DEV).manual_seed(3)
-    X = torch.randn(3, 200, 130, device=DEV, generator=g)
-    Y = torch.empty(3, 130, 200, device=DEV)
-    hi = torch.empty(3, 130, 200, device=DEV, dtype=torch.float16)
+    X = torch.randn(3, rows, cols, device=DEV, generator=g)
+    Y = torch.empty(3, cols, rows, device=DEV)
+    hi = torch.empty(3, cols, rows, device=DEV, dtype=torch.float16)
     lo = torch.empty_like(hi)
     K.transpose_split(X, out=Y, hi=hi, lo=lo, scale=64.0)
     assert torch.equal(Y, X.transpose(1, 2))
     rh, rl = _x3_split_ref(X.transpose(1, 2).contiguous(), 64.0)
     assert torch.equal(hi, rh) and torch.equal(lo, rl)
+    if rows % 32 == 0:   # K-blocked halves (the filter's A operand), without the fp32 output
+        bh, bl = torch.empty_like(hi), torch.empty_like(lo)
+        K.transpose_split(X, hi=bh, lo=bl, scale=64.0, blocked=True)
+        assert torch.equal(bh, _kblock(rh)) and torch.equal(bl, _kblock(rl))
     # hi + lo carries x * s to 2^-22 relative
     rec = (hi.double() + lo.double()) / 64.0
     # (plus the fp16 subnormal spacing of lo, 2^-24, for the smallest entries)
@@ -580,10 +591,12 @@ def test_gemm_x3_exact_b_matches_three_products(K, Bt, M, N, Kd, lda):
     assert torch.equal(C2k, C3k)
 
 
-@pytest.mark.parametrize("M,N", [(4096, 192), (1000, 64), (300, 100), (520, 300), (96, 384)])
+@pytest.mark.parametrize("M,N", [(4096, 192), (1000, 64), (777, 160), (130, 32), (11008, 128), (300, 100),
+                                 (520, 300), (96, 384)])
 def test_gemm_b_triu_matches_plain(K, M, N):
     """b_triu (CholQR's X Wt with Wt upper triangular, zeros stored): the same bits as the
-    plain product -- the skipped K slices only meet exact zeros of B."""
+    plain product -- the skipped K slices only meet exact zeros of B.  N % 32 == 0 and
+    N <= 192 take gemm_triu_kernel (ragged M included), the rest gemm_f32_kernel<TRIU>."""
     g = torch.Generator(device=DEV).manual_seed(M + N)
     A = torch.randn(3, M, N, device=DEV, generator=g)
     Bt = torch.triu(torch.randn(3, N, N, device=DEV, generator=g))
