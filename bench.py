@@ -785,11 +785,18 @@ def main():
     decs = eng = None
     if parts > 1 and world == 1 and probe["count"]:
         # the dominant kernel alone: one untimed step of the whole batch as one part (launches of
-        # B matrices, nothing beside them), HIP events as in the timed region
+        # B matrices, nothing beside them), HIP events as in the timed region.  The parts' cached
+        # scratch (scratch.py: per stream and shape) goes back to the device first: the one-part
+        # buffers are twice as large, and at config 3 (B = 192) both sets do not fit 288 GB
+        from ee274_convexcaldera_llm_quantization_amd import scratch
+        scratch.release()
+        torch.cuda.empty_cache()
         solver.EVENT_PROBE.enable(True)
         step(1)
         torch.cuda.synchronize()
         solver.EVENT_PROBE.enable(False)
+        scratch.release()
+        torch.cuda.empty_cache()
         psolo = solver.EVENT_PROBE.summary()
         if psolo["count"]:
             result["roofline_solo"] = roofline_of(psolo, B)
