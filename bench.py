@@ -783,25 +783,6 @@ def main():
         result["cpu_baseline"] = cpu
         result.update(par)
     decs = eng = None
-    if parts > 1 and world == 1 and probe["count"]:
-        # the dominant kernel alone: one untimed step of the whole batch as one part (launches of
-        # B matrices, nothing beside them), HIP events as in the timed region.  The parts' cached
-        # scratch (scratch.py: per stream and shape) goes back to the device first: the one-part
-        # buffers are twice as large, and at config 3 (B = 192) both sets do not fit 288 GB
-        from ee274_convexcaldera_llm_quantization_amd import scratch
-        scratch.release()
-        torch.cuda.empty_cache()
-        solver.EVENT_PROBE.enable(True)
-        step(1)
-        torch.cuda.synchronize()
-        solver.EVENT_PROBE.enable(False)
-        scratch.release()
-        torch.cuda.empty_cache()
-        psolo = solver.EVENT_PROBE.summary()
-        if psolo["count"]:
-            result["roofline_solo"] = roofline_of(psolo, B)
-            result["roofline_solo"]["note"] = ("one untimed step of the same batch as one part (no concurrent "
-                                               "kernels): the kernel's own efficiency")
     if not args.no_api_path:
         # the drop-in API (caldera_batch: the reference's output placement, W copied to the host
         # as alg.py:81 does, dataclass assembly) on one extra step of the same resident batch
@@ -821,6 +802,25 @@ def main():
                               "note": "one step through api.caldera_batch (drop-in layout, W to host)"}
         if rank == 0 and world == 1:
             result["api_single"] = single_call_latency(qp, Wb[0], h, dev)
+    if parts > 1 and world == 1 and probe["count"]:
+        # the dominant kernel alone: one untimed step of the whole batch as one part (launches of
+        # B matrices, nothing beside them), HIP events as in the timed region.  The parts' cached
+        # scratch (scratch.py: per stream and shape) goes back to the device first: the one-part
+        # buffers are twice as large, and at config 3 (B = 192) both sets do not fit 288 GB.
+        # Last, after the API path, which reuses the parts' warm scratch (after a release its
+        # step would time the re-allocation: 7.1 s instead of 0.85 s)
+        from ee274_convexcaldera_llm_quantization_amd import scratch
+        scratch.release()
+        torch.cuda.empty_cache()
+        solver.EVENT_PROBE.enable(True)
+        step(1)
+        torch.cuda.synchronize()
+        solver.EVENT_PROBE.enable(False)
+        psolo = solver.EVENT_PROBE.summary()
+        if psolo["count"]:
+            result["roofline_solo"] = roofline_of(psolo, B)
+            result["roofline_solo"]["note"] = ("one untimed step of the same batch as one part (no concurrent "
+                                               "kernels): the kernel's own efficiency")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
