@@ -121,6 +121,7 @@ _SIGS = {
                             c_i64, c_vp, c_i64, c_vp]),
     "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cq_transpose_split": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp, c_int, c_vp]),
+    "cq_gemm_triu_split": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_float, c_vp]),
     "cq_pow2_scale": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_split_f16": (c_int, [c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_i64, c_vp]),
     "cq_gemm_x3": (c_int, [ctypes.POINTER(X3Args), c_vp]),
@@ -649,6 +650,28 @@ def transpose_split(X: torch.Tensor, *, out=None, hi=None, lo=None, scale: float
                                      _stream(X.device)),
            "cq_transpose_split")
     return out, hi, lo
+
+
+TRIU_SPLIT_MAX_P = 192
+
+
+def triu_split_ok(M: int, p: int) -> bool:
+    """Shapes cq_gemm_triu_split takes (p % 32 == 0, p <= 192, M % 32 == 0)."""
+    return p % 32 == 0 and 0 < p <= TRIU_SPLIT_MAX_P and M % 32 == 0
+
+
+def gemm_triu_split(X: torch.Tensor, Wt: torch.Tensor, C: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor,
+                    scale: float):
+    """C = X Wt (Wt upper triangular) and hi/lo = the K-blocked split of C^T at `scale`: the
+    same bits as gemm(X, Wt, b_triu=True) followed by transpose_split(C, blocked=True)."""
+    _require_hip(X)
+    B, M, p = X.shape
+    assert X.dtype == Wt.dtype == C.dtype == torch.float32 and hi.dtype == lo.dtype == torch.float16
+    assert X.is_contiguous() and Wt.is_contiguous() and C.is_contiguous() and hi.is_contiguous() and lo.is_contiguous()
+    assert Wt.shape == (B, p, p) and C.shape == X.shape and hi.shape == (B, p, M) and lo.shape == hi.shape
+    _check(load().cq_gemm_triu_split(_p(X), _p(Wt), M, p, B, _p(C), _p(hi), _p(lo), float(scale),
+                                     _stream(X.device)), "cq_gemm_triu_split")
+    return C
 
 
 def pow2_scale(X: torch.Tensor, log2_target: int = 14, out=None):

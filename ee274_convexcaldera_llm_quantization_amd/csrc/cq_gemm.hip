@@ -40,6 +40,8 @@ struct KArgs {
     int vec_a, vec_b;
     int64_t tri;
     int b_triu;  // op(B) upper triangular (op(B)[k][n] = 0 for k > n): zero K slices skipped
+    _Float16 *th, *tl;  // gemm_triu_kernel<., true>: K-blocked split halves of C^T
+    float tscale;       // ... at this scale
 };
 
 // Stage one BM x BK slice of op(A) into registers (4 floats x 2 per thread).
@@ -301,8 +303,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_f32_kernel(KArgs a) {
 // unrolled at compile time, so the four waves carry equal work: 42 block-slices each at
 // N = 192 instead of 36 and 72.  Per output element it uses the same instruction, operands and
 // k order as gemm_f32_kernel, and the skipped terms are exact zeros, so the bits are the same
-// (test_gemm_b_triu_matches_plain).  LINEAR epilogue with alpha only.
-template <int NBLK>
+// (test_gemm_b_triu_matches_plain).  LINEAR epilogue with alpha only.  SPLIT: the epilogue
+// also writes the K-blocked split halves of C^T at a.tscale -- the operand of the Rayleigh-Ritz
+// product that follows CholQR (cq_gemm_triu_split), the same bits cq_transpose_split gives
+// from C, without its pass over C.
+template <int NBLK, bool SPLIT = false>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_triu_kernel(KArgs a) {
     static_assert(NBLK >= 1 && 32 * NBLK <= BN, "one 192-wide tile");
     constexpr int NT = 2 * NBLK;   // 16-deep K slices (K = 32 NBLK)
@@ -354,9 +359,30 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_triu_kernel(KArgs a) {
     for (int c = 0; c < NBLK; ++c) {
         const int64_t j = 32 * c + li;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t i = m0 + 32 * wid + (r & 3) + 8 * (r >> 2) + 4 * lk;
-            if (i < a.M) C[i * a.ldc + j] = alpha * acc[c][r];
+        for (int q = 0; q < 4; ++q) {   // registers 4q .. 4q + 3: rows i0 .. i0 + 3
+            const int64_t i0 = m0 + 32 * wid + 8 * q + 4 * lk;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = alpha * acc[c][4 * q + e];
+                if (i0 + e < a.M) C[(i0 + e) * a.ldc + j] = v[e];
+            }
+            if constexpr (SPLIT) {
+                if (i0 < a.M) {   // M % 32 == 0 (host check): the four rows are live together
+                    _Float16 h[4], l[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float xs = v[e] * a.tscale;
+                        h[e] = (_Float16)xs;
+                        l[e] = (_Float16)(xs - (float)h[e]);
+                    }
+                    // C^T (N x M) K-blocked over its columns (C's rows): (j, i) at
+                    // (i / 32) N 32 + j 32 + i % 32, four consecutive i in 8 bytes
+                    const int64_t o = b * a.M * a.N + (i0 >> 5) * a.N * 32 + j * 32 + (i0 & 31);
+                    *reinterpret_cast<uint2*>(a.th + o) = *reinterpret_cast<const uint2*>(h);
+                    *reinterpret_cast<uint2*>(a.tl + o) = *reinterpret_cast<const uint2*>(l);
+                }
+            }
         }
     }
 }
@@ -598,6 +624,8 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
     dim3 grid((unsigned)ceil_div(g->N, 64 * nb), (unsigned)ceil_div(g->M, BM), (unsigned)g->batch);
     k.tri = 0;
     k.b_triu = g->b_triu;
+    k.th = k.tl = nullptr;
+    k.tscale = 1.f;
     CQ_REQUIRE(!g->b_triu || (!g->trans_a && !g->trans_b && !g->syrk && g->epi == CQ_EPI_LINEAR),
                "cq_gemm_f32: b_triu needs a plain product (no transposes, LINEAR epilogue)");
     if (g->syrk) {
@@ -642,6 +670,40 @@ int cq_gemm_f32(const cq_gemm_args* g, void* ws, size_t ws_bytes, void* stream) 
             break;
     }
     return check_launch("cq_gemm_f32");
+}
+
+int cq_gemm_triu_split(const float* X, const float* Wt, int64_t M, int64_t p, int64_t batch, float* C,
+                       uint16_t* hi, uint16_t* lo, float scale, void* stream) {
+    CQ_REQUIRE(X && Wt && C && hi && lo, "cq_gemm_triu_split: null pointer");
+    CQ_REQUIRE(p > 0 && p % 32 == 0 && p <= BN, "cq_gemm_triu_split: p must be a multiple of 32, <= 192");
+    CQ_REQUIRE(M > 0 && M % 32 == 0 && batch > 0 && batch <= 65535 && ceil_div(M, BM) <= 65535,
+               "cq_gemm_triu_split: bad shape (M % 32 == 0)");
+    KArgs k{};
+    k.M = M; k.N = p; k.K = p;
+    k.A = X; k.lda = p; k.sa = M * p;
+    k.B = Wt; k.ldb = p; k.sb = p * p;
+    k.C = C; k.ldc = p; k.sc = M * p;
+    k.alpha = 1.f; k.beta = 0.f; k.gamma = 0.f;
+    auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    k.vec_a = al16(X);
+    k.vec_b = al16(Wt);
+    k.b_triu = 1;
+    k.th = reinterpret_cast<_Float16*>(hi);
+    k.tl = reinterpret_cast<_Float16*>(lo);
+    k.tscale = scale;
+    CQ_REQUIRE((reinterpret_cast<uintptr_t>(hi) & 7) == 0 && (reinterpret_cast<uintptr_t>(lo) & 7) == 0,
+               "cq_gemm_triu_split: halves must be 8-byte aligned");
+    const dim3 tg(1, (unsigned)ceil_div(M, BM), (unsigned)batch);
+    hipStream_t s = as_stream(stream);
+    switch (p / 32) {
+        case 1: gemm_triu_kernel<1, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+        case 2: gemm_triu_kernel<2, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+        case 3: gemm_triu_kernel<3, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+        case 4: gemm_triu_kernel<4, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+        case 5: gemm_triu_kernel<5, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+        default: gemm_triu_kernel<6, true><<<tg, kGemmThreads, 0, s>>>(k); break;
+    }
+    return check_launch("cq_gemm_triu_split");
 }
 
 }  // extern "C"

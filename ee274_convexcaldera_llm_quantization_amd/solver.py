@@ -222,6 +222,7 @@ class RankRSolver:
         self._bufs = None
         self._G = None
         self._yh = self._yl = None
+        self._halves_of = None   # the block whose X^T halves the last CholQR product wrote
         if filter_precision not in ("f16x3", "f32"):
             raise ValueError(f"filter_precision must be 'f16x3' or 'f32', got {filter_precision!r}")
         # split-fp16 filter needs K (= k) a multiple of 32 and 16-byte aligned rows
@@ -282,6 +283,7 @@ class RankRSolver:
         self._bufs = None
         self._G = None
         self._yh = self._yl = None
+        self._halves_of = None
         for name in ("_Gh", "_Gl", "_xt", "_xh", "_xl"):
             if hasattr(self, name):
                 setattr(self, name, None)
@@ -289,6 +291,7 @@ class RankRSolver:
     def split_block_t(self, X):
         """K-blocked split-fp16 halves of X^T (B, p, k) at X3_SCALE, in the solver's iterate
         buffers (valid until the next solve)."""
+        self._halves_of = None
         K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
         return self._xh[0], self._xl[0]
 
@@ -309,11 +312,19 @@ class RankRSolver:
             K.gemm(Y, Y, ta=True, C=self._G, syrk=True)
 
     # ------------------------------------------------------------------ steps
-    def _cholqr(self, X, *keep):
+    def _cholqr(self, X, *keep, halves=False):
+        """halves: the Rayleigh-Ritz step follows -- the product also writes its operand, the
+        K-blocked split of out^T, into the iterate halves (cq_gemm_triu_split: one pass instead
+        of the product and a transpose-split pass, the same bits)."""
         out = self._free(X, *keep)
         M = K.gram_f64(X, X)
         Wt32, _, info = K.spd_whiten(M)
-        K.gemm(X, Wt32, C=out, b_triu=True)  # Wt upper triangular (zeros stored)
+        self._halves_of = None
+        if halves and self.x3 and self._x3f and K.triu_split_ok(self.k, self.p):
+            K.gemm_triu_split(X, Wt32, out, self._xh[0], self._xl[0], X3_SCALE)
+            self._halves_of = out
+        else:
+            K.gemm(X, Wt32, C=out, b_triu=True)  # Wt upper triangular (zeros stored)
         return out, info
 
     def _rr(self, X, *keep, single=False, values_only=False):
@@ -326,7 +337,9 @@ class RankRSolver:
         G = self._G
         Z = self._free(X, *keep)
         if self.x3:  # Z = G X on split-fp16 products (X orthonormal: no overflow possible)
-            K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
+            if self._halves_of is not X:   # (else the CholQR product wrote them)
+                K.transpose_split(X, hi=self._xh[0], lo=self._xl[0], scale=X3_SCALE, blocked=True)
+            self._halves_of = None
             K.gemm_x3(self._xh[0], self._xl[0], self._Gh, self._Gl, self._ginv, self._xt[0], b_blocked=self._g_blocked,
                       a_blocked=True, single=single and self._x3f, Ct=Z if TRANSPOSED_OUT else None)
             if not TRANSPOSED_OUT:
@@ -434,6 +447,7 @@ class RankRSolver:
         product per step); X is left intact."""
         deg = coef.shape[0]
         xt, xh, xl = self._xt, self._xh, self._xl
+        self._halves_of = None
         # iterates' halves are K-blocked (each 32-deep step of a tile is one contiguous run)
         K.transpose_split(X, out=xt[0], hi=xh[0], lo=xl[0], scale=X3_SCALE, blocked=True)
         fl = 2.0 * self.k * self.k * self.p * self.B
@@ -572,7 +586,7 @@ class RankRSolver:
             if self.valid_k < k:  # zero-padded columns of W (engine.py): keep the block out of them
                 X[:, self.valid_k:, :] = 0.0
             X, _ = self._cholqr(X)
-            X, _ = self._cholqr(X)
+            X, _ = self._cholqr(X, halves=True)
             theta, X, Z = yield from self._rr(X, single=self.cheap_cold > 0, values_only=self.cheap_cold > 0)
             ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
             yield
@@ -620,7 +634,7 @@ class RankRSolver:
                 coef = self._cheb_coeffs(ends, d, dev)
                 Xf = self._filter(X, coef, single=cheap)
                 Xa, _ = self._cholqr(Xf, X)
-                Xb, _ = self._cholqr(Xa, X)
+                Xb, _ = self._cholqr(Xa, X, halves=True)
                 theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
                 # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
                 # stopping test: estimated relative error of the rank-r projection of Y (a

@@ -286,6 +286,13 @@ int cq_split_f16(const float* X, int64_t n_per, int64_t batch, const float* scal
 int cq_transpose_split(const float* X, int64_t rows, int64_t cols, int64_t batch, float* Y,
                        uint16_t* hi, uint16_t* lo, float scale, const float* scale_v, int blocked,
                        void* stream);
+/* CholQR's product with its triangular factor and the next product's operand in one pass:
+ * C[b] = X[b] Wt[b] (X M x p, Wt p x p upper triangular, both row-major and contiguous;
+ * p % 32 == 0, p <= 192, M % 32 == 0) and hi/lo[b] = the K-blocked split of C[b]^T at
+ * `scale` -- the same bits as cq_gemm_f32 (b_triu) followed by cq_transpose_split (blocked),
+ * without the second pass over C (the SVD replacement's CholQR -> Rayleigh-Ritz, alg.py:217). */
+int cq_gemm_triu_split(const float* X, const float* Wt, int64_t M, int64_t p, int64_t batch, float* C,
+                       uint16_t* hi, uint16_t* lo, float scale, void* stream);
 
 typedef struct cq_x3_args {
     int64_t M, N, K, batch;

@@ -605,6 +605,27 @@ def test_gemm_b_triu_matches_plain(K, M, N):
     assert torch.equal(C0, C1)
 
 
+@pytest.mark.parametrize("M,p", [(4096, 192), (1024, 96), (352, 32), (11008, 128), (160, 160)])
+def test_gemm_triu_split_matches_two_kernels(K, M, p):
+    """cq_gemm_triu_split (CholQR's X Wt writing the Rayleigh-Ritz operand, the K-blocked split
+    of its transpose, in the same pass): the same bits as the b_triu product followed by the
+    blocked transpose-split."""
+    g = torch.Generator(device=DEV).manual_seed(M + p)
+    X = torch.randn(3, M, p, device=DEV, generator=g)
+    Wt = torch.triu(torch.randn(3, p, p, device=DEV, generator=g))
+    C0 = K.gemm(X, Wt, C=torch.empty(3, M, p, device=DEV), b_triu=True)
+    h0 = torch.empty(3, p, M, device=DEV, dtype=torch.float16)
+    l0 = torch.empty_like(h0)
+    K.transpose_split(C0, hi=h0, lo=l0, scale=64.0, blocked=True)
+    C1 = torch.full((3, M, p), float("nan"), device=DEV)
+    h1 = torch.full_like(h0, float("nan"))
+    l1 = torch.full_like(l0, float("nan"))
+    assert K.triu_split_ok(M, p)
+    K.gemm_triu_split(X, Wt, C1, h1, l1, 64.0)
+    assert torch.equal(C0, C1)
+    assert torch.equal(h0, h1) and torch.equal(l0, l1)
+
+
 def test_residual_split_ycol_hi_matches_two_passes(K):
     """ycol_hi (the weighted Gram's operand): one pass writes the transposed halves and ||Y||^2
     with ycol and the column-blocked halves of res * ycol^2 at their own scale -- the same bits
