@@ -1216,9 +1216,15 @@ class CalderaEngine:
                 codes_all = K.unpack_codes(best.Qc, m * n, p.Q_bits, out=cbuf)
             else:
                 codes_all = best.Qc
-            # dequantize_block (quantization.py:103-105) on the reference int codes
+            # dequantize_block (quantization.py:103-105) on the reference int codes -- read from
+            # the packed form when there is one (the same code values: 1 byte per 4 or 2 codes
+            # instead of 1 per code, and no wait for the unpack)
             qbuf = work.view(-1) if work is not None and work.is_contiguous() else None
-            Qall = K.dequantize_uniform(codes_all, best.Qs, p.Q_bits, out=qbuf).view(B, m, n)
+            if best.q_packed and p.Q_bits <= 4 and best.Qc.is_contiguous():
+                Qall = K.dequantize_uniform(best.Qc, best.Qs, p.Q_bits, packed=True, numel=B * m * n,
+                                            out=qbuf).view(B, m, n)
+            else:
+                Qall = K.dequantize_uniform(codes_all, best.Qs, p.Q_bits, out=qbuf).view(B, m, n)
         for b in range(B):
             d = {}
             if best.flag_Q[b] and best.dense_q:
