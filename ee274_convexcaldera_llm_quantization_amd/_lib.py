@@ -7,8 +7,10 @@ fallback — a missing library or a non-HIP tensor raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -74,6 +76,7 @@ class X3Args(ctypes.Structure):
         ("absmax_out", c_vp),
         ("Ct", c_vp),
         ("stride_ct", c_i64),
+        ("stride_colw", c_i64),
     ]
 
 
@@ -84,21 +87,21 @@ _SIGS = {
     "cq_rms_scale": (c_int, [c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_quantize_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_quantize_uniform": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp,
-                                    c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+                                    c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_quantize_uniform_known_max": (c_int, [c_vp, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp,
-                                              c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+                                              c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_unpack_codes": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_quantize_nf_workspace": (c_size, [c_i64, c_i64, c_i64]),
-    "cq_quantize_nf": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
-                               c_vp, c_size, c_vp]),
+    "cq_quantize_nf": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                               c_vp, c_vp, c_size, c_vp]),
     "cq_dequant_nf": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_bbint_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_bbint_stats": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_bbint_emit": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
-                              c_vp, c_vp, c_size, c_vp]),
+                              c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_dequant_bbint": (c_int, [c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cq_dequant_uniform": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
-    "cq_build_residual": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp,
+    "cq_build_residual": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp,
                                   c_vp, c_vp]),
     "cq_gemm_workspace": (c_size, [ctypes.POINTER(GemmArgs)]),
     "cq_gemm_f32": (c_int, [ctypes.POINTER(GemmArgs), c_vp, c_size, c_vp]),
@@ -116,7 +119,7 @@ _SIGS = {
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
                                  c_vp]),
-    "cq_weighted_sqsum": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
+    "cq_weighted_sqsum": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_scale_rc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                             c_i64, c_vp, c_i64, c_vp]),
     "cq_sym_split_f16": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -130,24 +133,25 @@ _SIGS = {
     "cq_absmax": (c_int, [c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_residual_split_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_residual_split": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
-                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                  c_size, c_vp]),
     "cq_sgram_count": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                               c_vp, c_vp, c_vp, c_vp]),
+                               c_vp, c_i64, c_vp, c_vp, c_vp]),
     "cq_sgram_fill": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "cq_sgram_rows": (c_int, [c_i64]),
     "cq_pow2_from_absmax": (c_int, [c_vp, c_i64, c_int, c_vp]),
     "cq_sgram_split": (c_i64, [c_i64, c_i64]),
-    "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
-                              c_vp, c_vp]),
+    "cq_sgram_spmm": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_i64, c_vp, c_vp]),
     "cq_sgram_combine": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp]),
     "cq_codes_transpose": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "cq_codes_matmul": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
-                                c_i64, c_int, c_vp]),
-    "cq_codes_ysq_corr": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "cq_codes_matmul": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                c_vp, c_i64, c_i64, c_int, c_vp]),
+    "cq_codes_ysq_corr": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "cq_transpose_f16": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "cq_q_update_x3": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                               c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+                               c_float, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_ritz_product_error": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
     "cq_batched_dot": (c_int, [c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_size, c_vp]),
     "cq_act_sqsum_workspace": (c_size, [c_i64, c_i64]),
@@ -155,6 +159,7 @@ _SIGS = {
     "cq_act_sqsum_rows": (c_int, [c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_double, c_vp]),
 }
 EXPORTS = tuple(_SIGS)
+ABI_VERSION = 5  # include/caldera_hip.h CQ_ABI_VERSION
 
 _lib = None
 
@@ -181,7 +186,7 @@ def load(path: str = LIB_PATH):
         if fn is None:
             raise RuntimeError(f"{path} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.cq_abi_version() != 4 and not other:
+    if lib.cq_abi_version() != ABI_VERSION and not other:
         raise RuntimeError("libcaldera_hip.so ABI version mismatch")
     _lib = lib
     return lib
@@ -225,6 +230,15 @@ def _require_hip(*ts):
             raise RuntimeError("caldera-mi355x kernels need HIP device tensors (no CPU fallback)")
 
 
+def _wst(w: torch.Tensor | None, B: int) -> int:
+    """Batch stride of a column / error weight vector (ABI 5): (n,) is shared by the batch
+    (stride 0); (B, n) holds one vector per matrix (distinct diagonal Hessians, stride n)."""
+    if w is None or w.dim() == 1:
+        return 0
+    assert w.dim() == 2 and w.shape[0] == B and w.is_contiguous(), (tuple(w.shape), B)
+    return w.shape[1] if B > 1 else 0
+
+
 def workspace(nbytes: int, dev) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
 
@@ -254,7 +268,7 @@ def weighted_sqsum(x: torch.Tensor, w: torch.Tensor | None, ncols: int) -> torch
     out = torch.empty(B, dtype=torch.float64, device=x.device)
     lib = load()
     ws = workspace(lib.cq_rms_scale_workspace(B, numel), x.device)
-    _check(lib.cq_weighted_sqsum(dt, _p(x), B, numel, _p(w), ncols, _p(out), _p(ws), ws.numel(),
+    _check(lib.cq_weighted_sqsum(dt, _p(x), B, numel, _p(w), ncols, _wst(w, B), _p(out), _p(ws), ws.numel(),
                                  _stream(x.device)), "cq_weighted_sqsum")
     return out
 
@@ -296,7 +310,7 @@ def quantize_uniform(x: torch.Tensor, block_size: int, bits: int, eps: float = 1
     ws = workspace(lib.cq_quantize_workspace(B, numel, block_size), dev)
     _check(lib.cq_quantize_uniform(_p(x), B, numel, block_size, bits, eps, _p(out["codes"]),
                                    _p(out["packed"]), _p(out["deq"]), _p(out["scale"]), _p(err_w),
-                                   err_ncols, _p(out["err"]), _p(ws), ws.numel(), _stream(dev)),
+                                   err_ncols, _wst(err_w, B), _p(out["err"]), _p(ws), ws.numel(), _stream(dev)),
            "cq_quantize_uniform")
     return out
 
@@ -309,7 +323,7 @@ def quantize_known_max(x, absmax_bits, bits, eps=1e-8, *, codes=None, packed=Non
     lib = load()
     ws = workspace(lib.cq_quantize_workspace(B, numel, numel), x.device)
     _check(lib.cq_quantize_uniform_known_max(_p(x), B, numel, bits, eps, _p(absmax_bits), _p(codes),
-                                             _p(packed), _p(deq), _p(scale), _p(err_w), err_ncols,
+                                             _p(packed), _p(deq), _p(scale), _p(err_w), err_ncols, _wst(err_w, B),
                                              _p(err_out), _p(ws), ws.numel(), _stream(x.device)),
            "cq_quantize_uniform_known_max")
 
@@ -352,7 +366,7 @@ def quantize_nf(x: torch.Tensor, block_size: int, bits: int, eps: float = 1e-8, 
     lib = load()
     ws = workspace(lib.cq_quantize_nf_workspace(B, numel, block_size), dev)
     _check(lib.cq_quantize_nf(_p(x), B, numel, block_size, bits, eps, _p(out["idx"]), _p(out["deq"]),
-                              _p(out["scale"]), _p(err_w), err_ncols, _p(err_out), _p(ws), ws.numel(),
+                              _p(out["scale"]), _p(err_w), err_ncols, _wst(err_w, B), _p(err_out), _p(ws), ws.numel(),
                               _stream(dev)), "cq_quantize_nf")
     return out
 
@@ -397,7 +411,7 @@ def quantize_bbint(x: torch.Tensor, block_size: int, bits: int, eps: float = 1e-
     dq = torch.empty((B, numel), dtype=torch.float32, device=dev) if deq else None
     _check(lib.cq_bbint_emit(_p(x), B, numel, block_size, bits, _p(bmin), _p(bscale), _p(pk), _p(dq),
                              _p(vals) if tot else None, _p(oidx) if tot else None, _p(err_w), err_ncols,
-                             _p(err_out), _p(ws), ws.numel(), st), "cq_bbint_emit")
+                             _wst(err_w, B), _p(err_out), _p(ws), ws.numel(), st), "cq_bbint_emit")
     return {"packed": pk, "deq": dq, "bmin": bmin, "bscale": bscale, "n_out": counts, "vals": vals, "idx": oidx}
 
 
@@ -419,7 +433,7 @@ def build_residual(Ws, qcodes, qscale, bits, ycol, Y=None, res=None):
     _require_hip(Ws, qcodes, qscale, ycol, Y, res)
     dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[Ws.dtype]
     B, m, n = Ws.shape
-    _check(load().cq_build_residual(dt, _p(Ws), _p(qcodes), _p(qscale), bits, _p(ycol), B, m, n,
+    _check(load().cq_build_residual(dt, _p(Ws), _p(qcodes), _p(qscale), bits, _p(ycol), _wst(ycol, B), B, m, n,
                                     _p(Y), _p(res), _stream(Ws.device)), "cq_build_residual")
 
 
@@ -714,8 +728,28 @@ def split_f16(X: torch.Tensor, scale, *, hi=None, lo=None, blocked: bool = False
 
 
 # automatic split-K of small-batch split-fp16 products (gemm_x3); False: every product in one
-# pass, so results do not depend on the batch a matrix is decomposed in (slower at small B)
+# pass, so results do not depend on the batch a matrix is decomposed in (slower at small B).
+# The process default; split_k_policy() overrides it for the calling thread only.
 AUTO_SPLIT_K = True
+_POLICY = threading.local()
+
+
+@contextlib.contextmanager
+def split_k_policy(enabled: bool):
+    """Within the block, this thread's gemm_x3 calls use automatic split-K iff `enabled`
+    (overlap.run_interleaved turns it off while batches share the chip); other threads keep
+    their own policy."""
+    prev = getattr(_POLICY, "auto", None)
+    _POLICY.auto = bool(enabled)
+    try:
+        yield
+    finally:
+        _POLICY.auto = prev
+
+
+def auto_split_k() -> bool:
+    v = getattr(_POLICY, "auto", None)
+    return AUTO_SPLIT_K if v is None else v
 
 
 def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_v=None, gamma_v=None,
@@ -730,7 +764,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     C may then be None.  lda / M (a_blocked only): A holds lda >= M rows of which the first M
     are used (C has M rows).  b_exact: B is exactly fp16 (Bl = 0, e.g. W's halves written
     under a split scale >= 1); Bl is not read and may be None.  colw (N,) fp32: the product
-    term of column j scaled by colw[j] (before beta P + gamma D).  absmax_out (B,) int32/uint32/fp32
+    term of column j scaled by colw[j] (before beta P + gamma D; (B, N): per matrix).  absmax_out (B,) int32/uint32/fp32
     (plain products): zeroed here, receives the bits of max|C[b]| (pow2_from_absmax turns them
     into the next split's scale without a pass over C).  Ct (B, N, M) fp32: C^T as well (not
     with tri / sym_out; C required)."""
@@ -771,8 +805,8 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     g.single = int(bool(single))
     g.b_exact = int(bool(b_exact))
     if colw is not None:
-        assert colw.dtype == torch.float32 and colw.is_contiguous() and colw.numel() == N
-        g.colw = colw.data_ptr()
+        assert colw.dtype == torch.float32 and colw.is_contiguous() and colw.shape[-1] == N
+        g.colw, g.stride_colw = colw.data_ptr(), _wst(colw, Bt)
     if absmax_out is not None:
         assert absmax_out.numel() == Bt and absmax_out.element_size() == 4 and absmax_out.is_contiguous()
         absmax_out.zero_()
@@ -788,7 +822,7 @@ def gemm_x3(Ah, Al, Bh, Bl, inv_scale, C, *, P=None, D=None, alpha_v=None, beta_
     # the products' rounding, not bit for bit; AUTO_SPLIT_K = False pins one pass everywhere
     tiles = -(-N // 384) * -(-M // 192) * Bt
     splittable = not tri and sym_bound is None and C is not None and N % 4 == 0
-    if ksplit is None and not AUTO_SPLIT_K:
+    if ksplit is None and not auto_split_k():
         ksplit = 1
     if ksplit is None:  # automatic
         ks = min(Kd // 32 // 8, -(-512 // tiles)) if splittable and tiles < 256 and Kd >= 512 else 1
@@ -847,7 +881,8 @@ def q_update_x3(W: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None,
     if events is not None:  # HIP events around the quantise kernels only (bench roofline)
         events[0].record()
     _check(lib.cq_q_update_x3(dt, _p(W), m, n, r, B, *[_p(t) for t in halves], _p(inv), bits, float(eps), _p(codes),
-                              _p(packed), _p(scale), _p(err_w), _p(err_out), _p(absmax_in if r == 0 else None),
+                              _p(packed), _p(scale), _p(err_w), _wst(err_w, B), _p(err_out),
+                              _p(absmax_in if r == 0 else None),
                               _p(scale_hint if r else None), _p(fallback_out), _p(ws), ws.numel(), _stream(dev)),
            "cq_q_update_x3")
     if events is not None:
@@ -896,7 +931,8 @@ def sgram_count(packed, k, L, row_nnz, perm, slice_off, total, W=None, qscale=No
         assert W.dtype == torch.float16 and W.is_contiguous() and W.shape == (B, k, L)
         assert corr_ws.numel() >= B * k and corr_ws.dtype == torch.float64 and corr_out.numel() == B
     _check(load().cq_sgram_count(_p(packed), 2, B, k, L, _p(row_nnz), _p(perm), _p(slice_off), _p(total), Lh,
-                                 _p(row_nnz1), _p(slice_w1), _p(W), _p(qscale), _p(wcol), _p(corr_ws), _p(corr_out),
+                                 _p(row_nnz1), _p(slice_w1), _p(W), _p(qscale), _p(wcol), _wst(wcol, B), _p(corr_ws),
+                                 _p(corr_out),
                                  _stream(packed.device)), "cq_sgram_count")
 
 
@@ -929,13 +965,14 @@ def codes_matmul(packed, rows, cols, X, r, out, *, colw=None, roww=None, trans=F
     """out[b] = diag(roww) c[b] diag(colw) X[b][:, :r] (rows x r; trans: its transpose, r x rows) for
     2-bit packed codes c (B, rows, cols) and X (B, cols, ldx) fp32 (cq_codes_matmul)."""
     _require_hip(packed, X, colw, roww, out)
-    assert roww is None or (roww.numel() == rows and roww.dtype == torch.float32 and roww.is_contiguous())
     B = packed.shape[0]
+    assert roww is None or (roww.shape[-1] == rows and roww.dtype == torch.float32 and roww.is_contiguous())
     assert packed.numel() == B * rows * cols // 4 and X.shape[:2] == (B, cols) and X.stride(2) == 1
     assert X.dtype == torch.float32 and out.dtype == torch.float32 and out.is_contiguous()
     assert out.shape == ((B, r, rows) if trans else (B, rows, r))
-    assert colw is None or (colw.numel() == cols and colw.dtype == torch.float32 and colw.is_contiguous())
-    _check(load().cq_codes_matmul(_p(packed), 2, B, rows, cols, _p(X), X.stride(1), X.stride(0), _p(colw), _p(roww), r, _p(out),
+    assert colw is None or (colw.shape[-1] == cols and colw.dtype == torch.float32 and colw.is_contiguous())
+    _check(load().cq_codes_matmul(_p(packed), 2, B, rows, cols, _p(X), X.stride(1), X.stride(0), _p(colw), _wst(colw, B),
+                                  _p(roww), _wst(roww, B), r, _p(out),
                                   out.shape[2], out.stride(0), int(bool(trans)), _stream(packed.device)),
            "cq_codes_matmul")
     return out
@@ -949,7 +986,7 @@ def codes_ysq_corr(packed, W, qscale, colw=None, out=None):
     assert W.dtype == torch.float16 and W.is_contiguous() and packed.numel() == B * m * n // 4
     if out is None:
         out = torch.empty(B, dtype=torch.float64, device=W.device)
-    _check(load().cq_codes_ysq_corr(_p(packed), 2, _p(W), CQ_F16, _p(qscale), _p(colw), B, m, n, _p(out),
+    _check(load().cq_codes_ysq_corr(_p(packed), 2, _p(W), CQ_F16, _p(qscale), _p(colw), _wst(colw, B), B, m, n, _p(out),
                                     _stream(W.device)), "cq_codes_ysq_corr")
     return out
 
@@ -976,9 +1013,9 @@ def sgram_spmm(W, packed, qscale, wcol, ell, perm, slice_off, stride, P, Lh=None
     _require_hip(W, packed, qscale, wcol, ell, perm, slice_off, P, slice_w1)
     B, k, L = W.shape
     assert W.dtype == torch.float16 and W.is_contiguous() and P.shape == (B, k, k) and P.is_contiguous()
-    assert wcol is None or (wcol.numel() == L and wcol.dtype == torch.float32)
+    assert wcol is None or (wcol.shape[-1] == L and wcol.dtype == torch.float32)
     Lh = L if Lh is None else Lh
-    _check(load().cq_sgram_spmm(CQ_F16, _p(W), _p(packed), _p(qscale), _p(wcol), B, k, L, _p(ell), _p(perm),
+    _check(load().cq_sgram_spmm(CQ_F16, _p(W), _p(packed), _p(qscale), _p(wcol), _wst(wcol, B), B, k, L, _p(ell), _p(perm),
                                 _p(slice_off), _p(slice_w1), Lh, stride, _p(P), _stream(W.device)), "cq_sgram_spmm")
 
 
@@ -995,15 +1032,24 @@ def sgram_combine(A, P, qscale, bound, out_scale, Gh, Gl, scale_out, inv_out, G3
 def residual_split(Ws, packed, qscale, bits, wmax, *, ycol=None, ycol_max=1.0, res=None, Y=None, hi=None, lo=None,
                    thi=None, tlo=None, scale=None, sq=None, ycol_hi=None, ycol_hi_max=1.0, scale_hi=None):
     """Fused LR-step residual (see include/caldera_hip.h cq_residual_split).  Ws (B, m, n).
-    ycol_hi: hi/lo are the halves of res * ycol_hi (their scale in scale_hi) instead."""
+    ycol_hi: hi/lo are the halves of res * ycol_hi (their scale in scale_hi) instead.
+    Per-matrix weights: ycol / ycol_hi (B, n) with ycol_max / ycol_hi_max (B,) fp32 tensors."""
     _require_hip(Ws, packed, qscale, wmax, ycol, res, Y, hi, lo, thi, tlo, scale, sq, ycol_hi, scale_hi)
     B, m, n = Ws.shape
     dt = {torch.float16: CQ_F16, torch.float32: CQ_F32}[Ws.dtype]
+    yst = max(_wst(ycol, B), _wst(ycol_hi, B))
+    assert ycol is None or ycol_hi is None or ycol.shape == ycol_hi.shape
+    ymv = ycol_max if torch.is_tensor(ycol_max) else None
+    yhmv = ycol_hi_max if torch.is_tensor(ycol_hi_max) else None
+    for t in (ymv, yhmv):
+        assert t is None or (t.dtype == torch.float32 and t.numel() == B and t.is_contiguous() and t.is_cuda)
     lib = load()
     ws = workspace(lib.cq_residual_split_workspace(m, n, B), Ws.device) if sq is not None else None
-    _check(lib.cq_residual_split(dt, _p(Ws), _p(packed), _p(qscale), int(bits), _p(ycol), float(ycol_max), _p(wmax),
+    _check(lib.cq_residual_split(dt, _p(Ws), _p(packed), _p(qscale), int(bits), _p(ycol),
+                                 1.0 if ymv is not None else float(ycol_max), _p(wmax),
                                  B, m, n, _p(res), _p(Y), _p(hi), _p(lo), _p(thi), _p(tlo), _p(scale), _p(sq),
-                                 _p(ycol_hi), float(ycol_hi_max), _p(scale_hi), _p(ws),
+                                 _p(ycol_hi), 1.0 if yhmv is not None else float(ycol_hi_max), _p(scale_hi), yst,
+                                 _p(ymv), _p(yhmv), _p(ws),
                                  0 if ws is None else ws.numel(), _stream(Ws.device)), "cq_residual_split")
 
 

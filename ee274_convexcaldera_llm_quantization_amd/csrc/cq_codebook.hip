@@ -60,7 +60,7 @@ template <int BITS>
 __global__ __launch_bounds__(kCbThreads) void nf_block_kernel(
     const float* __restrict__ x, int64_t nbt, int64_t bs, int64_t nblk_per, float eps,
     uint8_t* __restrict__ idx, float* __restrict__ deq, float* __restrict__ scale,
-    const float* __restrict__ ew, int64_t encols, double* __restrict__ perr) {
+    const float* __restrict__ ew, int64_t encols, double* __restrict__ perr, int64_t ews) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * kCbThreads + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * kCbThreads) >> 6;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kCbThreads) void nf_block_kernel(
             if (deq) deq[blk * bs + i] = d;
             if (perr) {
                 const float df = d - xv;
-                acc += (double)(df * df) * (ew ? (double)ew[(e_in_mat0 + i) % encols] : 1.0);
+                acc += (double)(df * df) * (ew ? (double)ew[(blk / nblk_per) * ews + (e_in_mat0 + i) % encols] : 1.0);
             }
         }
         if (perr) {
@@ -120,9 +120,10 @@ template <int BITS>
 __global__ __launch_bounds__(kCbThreads) void nf_known_kernel(
     const float* __restrict__ x, int64_t numel, int64_t bs, float eps, const uint32_t* __restrict__ mx,
     uint8_t* __restrict__ idx, float* __restrict__ deq, float* __restrict__ scale,
-    const float* __restrict__ ew, int64_t encols, double* __restrict__ part) {
+    const float* __restrict__ ew, int64_t encols, double* __restrict__ part, int64_t ews) {
     __shared__ double lds[16];
     const int64_t b = blockIdx.y;
+    if (ew) ew += b * ews;  // per-matrix error weights (stride 0: shared)
     const int64_t nb = numel / bs;
     const float* xb = x + b * numel;
     double acc = 0.0;
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(kCbThreads) void bb_emit_kernel(
     const float* __restrict__ x, BBGeom g, const float* __restrict__ mean32, const float* __restrict__ thr,
     const float* __restrict__ bmin, const float* __restrict__ bscale, const int64_t* __restrict__ poff,
     uint8_t* __restrict__ packed, float* __restrict__ deq, float* __restrict__ out_vals, int64_t* __restrict__ out_idx,
-    const float* __restrict__ ew, int64_t encols, double* __restrict__ perr) {
+    const float* __restrict__ ew, int64_t encols, double* __restrict__ perr, int64_t ews) {
     constexpr int BITS = 1 << LB;
     constexpr int PER = 8 / BITS;
     constexpr float LEVELS = (float)((1 << BITS) - 1);
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(kCbThreads) void bb_emit_kernel(
         if (in && deq) deq[e] = d;
         if (in && perr) {
             const float df = d - xv;
-            acc += (double)(df * df) * (ew ? (double)ew[((row * g.bs) + c0 + i) % encols] : 1.0);
+            acc += (double)(df * df) * (ew ? (double)ew[(blk / g.nblk_per) * ews + ((row * g.bs) + c0 + i) % encols] : 1.0);
         }
         if (packed) {  // PER consecutive codes per byte, first code in the high bits
             uint32_t code = in ? (uint32_t)q : 0u;
@@ -506,8 +507,8 @@ size_t cq_quantize_nf_workspace(int64_t batch, int64_t numel, int64_t block_size
 }
 
 int cq_quantize_nf(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, float eps,
-                   uint8_t* idx, float* deq, float* scale, const float* err_w, int64_t err_ncols, double* err_out,
-                   void* ws, size_t ws_bytes, void* stream) {
+                   uint8_t* idx, float* deq, float* scale, const float* err_w, int64_t err_ncols, int64_t err_w_stride,
+                   double* err_out, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(x && scale && batch > 0 && numel > 0 && block_size > 0, "cq_quantize_nf: bad args");
     CQ_REQUIRE(bits == 2 || bits == 4, "cq_quantize_nf: bits must be 2 (nf2) or 4 (nf4)");
     CQ_REQUIRE(numel % block_size == 0, "cq_quantize_nf: numel %% block_size != 0");
@@ -523,8 +524,8 @@ int cq_quantize_nf(const float* x, int64_t batch, int64_t numel, int64_t block_s
     if (block_size <= 4096) {
         const int g = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nbt, kCbThreads / 64), 8192));
         double* pe = err_out ? pblk : nullptr;
-        if (bits == 4) nf_block_kernel<4><<<g, kCbThreads, 0, s>>>(x, nbt, block_size, nblk, eps, idx, deq, scale, err_w, err_ncols, pe);
-        else nf_block_kernel<2><<<g, kCbThreads, 0, s>>>(x, nbt, block_size, nblk, eps, idx, deq, scale, err_w, err_ncols, pe);
+        if (bits == 4) nf_block_kernel<4><<<g, kCbThreads, 0, s>>>(x, nbt, block_size, nblk, eps, idx, deq, scale, err_w, err_ncols, pe, err_w_stride);
+        else nf_block_kernel<2><<<g, kCbThreads, 0, s>>>(x, nbt, block_size, nblk, eps, idx, deq, scale, err_w, err_ncols, pe, err_w_stride);
         if (err_out) cb_sum_parts_kernel<<<batch, 64, 0, s>>>(pblk, nblk, err_out);
         return check_launch("cq_quantize_nf(block)");
     }
@@ -532,8 +533,8 @@ int cq_quantize_nf(const float* x, int64_t batch, int64_t numel, int64_t block_s
     const int g = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(numel, kCbThreads * 4), std::max<int64_t>(64, kMaxGrid / batch)));
     cb_absmax_kernel<<<dim3(g, batch), kCbThreads, 0, s>>>(x, numel, block_size, mx);
     double* pe = err_out ? part : nullptr;
-    if (bits == 4) nf_known_kernel<4><<<dim3(g, batch), kCbThreads, 0, s>>>(x, numel, block_size, eps, mx, idx, deq, scale, err_w, err_ncols, pe);
-    else nf_known_kernel<2><<<dim3(g, batch), kCbThreads, 0, s>>>(x, numel, block_size, eps, mx, idx, deq, scale, err_w, err_ncols, pe);
+    if (bits == 4) nf_known_kernel<4><<<dim3(g, batch), kCbThreads, 0, s>>>(x, numel, block_size, eps, mx, idx, deq, scale, err_w, err_ncols, pe, err_w_stride);
+    else nf_known_kernel<2><<<dim3(g, batch), kCbThreads, 0, s>>>(x, numel, block_size, eps, mx, idx, deq, scale, err_w, err_ncols, pe, err_w_stride);
     if (err_out) cb_sum_parts_kernel<<<batch, 64, 0, s>>>(part, g, err_out);
     return check_launch("cq_quantize_nf");
 }
@@ -578,7 +579,8 @@ int cq_bbint_stats(const float* x, int64_t batch, int64_t numel, int64_t block_s
 
 int cq_bbint_emit(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, const float* bmin,
                   const float* bscale, uint8_t* packed, float* deq, float* out_vals, int64_t* out_idx,
-                  const float* err_w, int64_t err_ncols, double* err_out, void* ws, size_t ws_bytes, void* stream) {
+                  const float* err_w, int64_t err_ncols, int64_t err_w_stride, double* err_out, void* ws, size_t ws_bytes,
+                  void* stream) {
     CQ_REQUIRE(x && bmin && bscale && batch > 0 && numel > 0 && block_size > 0, "cq_bbint_emit: bad args");
     CQ_REQUIRE(bits == 2 || bits == 4, "cq_bbint_emit: bits must be 2 or 4");
     CQ_REQUIRE(!packed || block_size % (8 / bits) == 0, "cq_bbint_emit: block_size must be a multiple of %d", 8 / bits);
@@ -593,10 +595,10 @@ int cq_bbint_emit(const float* x, int64_t batch, int64_t numel, int64_t block_si
     double* pe = err_out ? w.perr : nullptr;
     if (bits == 4)
         bb_emit_kernel<2><<<nchunks, kCbThreads, 0, s>>>(x, g, w.mean32, w.thr, bmin, bscale, w.poff, packed, deq,
-                                                         out_vals, out_idx, err_w, err_ncols, pe);
+                                                         out_vals, out_idx, err_w, err_ncols, pe, err_w_stride);
     else
         bb_emit_kernel<1><<<nchunks, kCbThreads, 0, s>>>(x, g, w.mean32, w.thr, bmin, bscale, w.poff, packed, deq,
-                                                         out_vals, out_idx, err_w, err_ncols, pe);
+                                                         out_vals, out_idx, err_w, err_ncols, pe, err_w_stride);
     if (err_out) cb_sum_parts_kernel<<<batch, 64, 0, s>>>(w.perr, g.nblk_per * g.nch, err_out);
     return check_launch("cq_bbint_emit");
 }

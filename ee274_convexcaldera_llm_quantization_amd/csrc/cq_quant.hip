@@ -159,9 +159,10 @@ template <int DT>
 __global__ __launch_bounds__(kThreads) void wsq_partial_kernel(const void* __restrict__ X,
                                                                 int64_t numel,
                                                                 const float* __restrict__ w,
-                                                                int64_t ncols, double* part) {
+                                                                int64_t ncols, double* part, int64_t wst) {
     __shared__ double lds[16];
     const int64_t b = blockIdx.y;
+    if (w) w += b * wst;  // per-matrix weights (stride 0: shared)
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < numel; i += stride) {
@@ -177,9 +178,10 @@ __global__ __launch_bounds__(kThreads) void wsq_partial_kernel(const void* __res
 template <int DT>
 __global__ __launch_bounds__(kThreads) void wsq_partial8_kernel(const void* __restrict__ X, int64_t numel,
                                                                  const float* __restrict__ w, int64_t ncols,
-                                                                 double* part) {
+                                                                 double* part, int64_t wst) {
     __shared__ double lds[16];
     const int64_t b = blockIdx.y;
+    if (w) w += b * wst;  // per-matrix weights (stride 0: shared)
     double acc0 = 0.0, acc1 = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kThreads * 8;
     for (int64_t e = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 8; e < numel; e += stride) {
@@ -301,10 +303,11 @@ template <int BITS, bool PACK, bool ERR>
 __global__ __launch_bounds__(kThreads) void quant_known_kernel(
     const float* __restrict__ x, int64_t numel, int64_t bs, float eps,
     const uint32_t* __restrict__ mx, void* __restrict__ codes, uint8_t* __restrict__ packed,
-    float* __restrict__ deq, const float* __restrict__ ew, int64_t encols, double* part) {
+    float* __restrict__ deq, const float* __restrict__ ew, int64_t encols, double* part, int64_t ews) {
     constexpr float k = (float)((1 << (BITS - 1)) - 1);
     __shared__ double lds[16];
     const int64_t b = blockIdx.y;
+    if (ew) ew += b * ews;  // per-matrix error weights (stride 0: shared)
     const int64_t nb = numel / bs;
     const float* xb = x + b * numel;
     double acc = 0.0;
@@ -476,9 +479,10 @@ template <int DT, int BITS>
 __global__ __launch_bounds__(kThreads) void build_residual_kernel(
     const void* __restrict__ Ws, const uint8_t* __restrict__ qc, const float* __restrict__ qscale,
     const float* __restrict__ ycol, int64_t m, int64_t n, float* __restrict__ Y,
-    float* __restrict__ res) {
+    float* __restrict__ res, int64_t ycs) {
     constexpr float k = BITS == 32 ? 1.f : (float)((1 << (BITS - 1)) - 1);
     const int64_t b = blockIdx.y;
+    if (ycol) ycol += b * ycs;  // per-matrix column weights (stride 0: shared)
     const int64_t numel = m * n;
     const float s = (qc && qscale) ? qscale[b] : 0.f;
     const int64_t ngroups = numel / 4;  // n % 4 == 0 guaranteed by caller
@@ -560,8 +564,8 @@ template <int BITS>
 static void launch_known(bool pack, bool err, dim3 grid, hipStream_t s, const float* x,
                          int64_t numel, int64_t bs, float eps, const uint32_t* mx, void* codes,
                          uint8_t* packed, float* deq, const float* ew, int64_t encols,
-                         double* part) {
-#define CQ_LK(P, E) quant_known_kernel<BITS, P, E><<<grid, kThreads, 0, s>>>(x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part)
+                         double* part, int64_t ews) {
+#define CQ_LK(P, E) quant_known_kernel<BITS, P, E><<<grid, kThreads, 0, s>>>(x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part, ews)
     if (pack && err) CQ_LK(true, true);
     else if (pack) CQ_LK(true, false);
     else if (err) CQ_LK(false, true);
@@ -572,16 +576,16 @@ static void launch_known(bool pack, bool err, dim3 grid, hipStream_t s, const fl
 static int quant_known_dispatch(const float* x, int64_t batch, int64_t numel, int64_t bs,
                                 int bits, float eps, const uint32_t* mx, void* codes,
                                 uint8_t* packed, float* deq, float* scale, const float* ew,
-                                int64_t encols, double* err_out, double* part, hipStream_t s) {
+                                int64_t encols, int64_t ews, double* err_out, double* part, hipStream_t s) {
     const int g = grid_for(numel, batch);
     dim3 grid(g, batch);
     const bool err = ew != nullptr || err_out != nullptr;
     const bool pack = packed != nullptr && bits <= 4;
     switch (bits) {
-        case 2: launch_known<2>(pack, err, grid, s, x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part); break;
-        case 4: launch_known<4>(pack, err, grid, s, x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part); break;
-        case 8: launch_known<8>(false, err, grid, s, x, numel, bs, eps, mx, codes, nullptr, deq, ew, encols, part); break;
-        default: launch_known<16>(false, err, grid, s, x, numel, bs, eps, mx, codes, nullptr, deq, ew, encols, part); break;
+        case 2: launch_known<2>(pack, err, grid, s, x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part, ews); break;
+        case 4: launch_known<4>(pack, err, grid, s, x, numel, bs, eps, mx, codes, packed, deq, ew, encols, part, ews); break;
+        case 8: launch_known<8>(false, err, grid, s, x, numel, bs, eps, mx, codes, nullptr, deq, ew, encols, part, ews); break;
+        default: launch_known<16>(false, err, grid, s, x, numel, bs, eps, mx, codes, nullptr, deq, ew, encols, part, ews); break;
     }
     const int64_t nsc = batch * (numel / bs);
     if (scale) finalize_scale_kernel<<<(int)ceil_div(nsc, 256), 256, 0, s>>>(mx, nsc, eps, scale);
@@ -630,7 +634,7 @@ int cq_rms_scale(int dtype, const void* W, int64_t batch, int64_t numel, int do_
 }
 
 int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel, const float* w,
-                      int64_t ncols, double* out, void* ws, size_t ws_bytes, void* stream) {
+                      int64_t ncols, int64_t w_stride, double* out, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(x && out && batch > 0 && numel > 0, "cq_weighted_sqsum: bad args");
     CQ_REQUIRE(!w || ncols > 0, "cq_weighted_sqsum: ncols");
     const int g = grid_for(numel, batch);
@@ -640,14 +644,14 @@ int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel, co
     double* part = reinterpret_cast<double*>(ws);
     dim3 grid(g, batch);
     const bool v8 = numel % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-                    (!w || (ncols % 8 == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0));
+                    (!w || (ncols % 8 == 0 && w_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0));
     if (v8) {
-        if (dtype == CQ_F16) wsq_partial8_kernel<CQ_F16><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part);
-        else wsq_partial8_kernel<CQ_F32><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part);
+        if (dtype == CQ_F16) wsq_partial8_kernel<CQ_F16><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part, w_stride);
+        else wsq_partial8_kernel<CQ_F32><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part, w_stride);
     } else if (dtype == CQ_F16) {
-        wsq_partial_kernel<CQ_F16><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part);
+        wsq_partial_kernel<CQ_F16><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part, w_stride);
     } else {
-        wsq_partial_kernel<CQ_F32><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part);
+        wsq_partial_kernel<CQ_F32><<<grid, kThreads, 0, s>>>(x, numel, w, ncols, part, w_stride);
     }
     sum_parts_kernel<<<batch, 64, 0, s>>>(part, g, out, 0);
     return check_launch("cq_weighted_sqsum");
@@ -681,8 +685,8 @@ size_t cq_quantize_workspace(int64_t batch, int64_t numel, int64_t block_size) {
 
 int cq_quantize_uniform(const float* x, int64_t batch, int64_t numel, int64_t block_size,
                         int bits, float eps, void* codes, uint8_t* packed, float* deq,
-                        float* scale, const float* err_w, int64_t err_ncols, double* err_out,
-                        void* ws, size_t ws_bytes, void* stream) {
+                        float* scale, const float* err_w, int64_t err_ncols, int64_t err_w_stride,
+                        double* err_out, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(x && scale && batch > 0 && numel > 0 && block_size > 0, "cq_quantize_uniform: bad args");
     CQ_REQUIRE(bits == 2 || bits == 4 || bits == 8 || bits == 16, "Bit-width not supported!");
     CQ_REQUIRE(numel % block_size == 0, "cq_quantize_uniform: numel %% block_size != 0");
@@ -717,14 +721,14 @@ int cq_quantize_uniform(const float* x, int64_t batch, int64_t numel, int64_t bl
         return set_error(CQ_EHIP, "cq_quantize_uniform: memset failed");
     absmax_atomic_kernel<<<dim3(grid_for(numel, batch), batch), kThreads, 0, s>>>(x, numel, block_size, mx);
     return quant_known_dispatch(x, batch, numel, block_size, bits, eps, mx, codes, packed, deq,
-                                scale, err_w, err_ncols, err_out, part, s);
+                                scale, err_w, err_ncols, err_w_stride, err_out, part, s);
 }
 
 int cq_quantize_uniform_known_max(const float* x, int64_t batch, int64_t numel, int bits,
                                   float eps, const uint32_t* absmax_bits, void* codes,
                                   uint8_t* packed, float* deq, float* scale,
-                                  const float* err_w, int64_t err_ncols, double* err_out,
-                                  void* ws, size_t ws_bytes, void* stream) {
+                                  const float* err_w, int64_t err_ncols, int64_t err_w_stride,
+                                  double* err_out, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(x && absmax_bits && batch > 0 && numel > 0, "cq_quantize_uniform_known_max: bad args");
     CQ_REQUIRE(bits == 2 || bits == 4 || bits == 8 || bits == 16, "Bit-width not supported!");
     CQ_REQUIRE(numel % 4 == 0, "cq_quantize_uniform_known_max: numel %% 4 != 0");
@@ -732,7 +736,7 @@ int cq_quantize_uniform_known_max(const float* x, int64_t batch, int64_t numel, 
     if (err && (ws_bytes < (size_t)batch * grid_for(numel, batch) * sizeof(double) || !ws))
         return set_error(CQ_EWORKSPACE, "cq_quantize_uniform_known_max: workspace too small");
     return quant_known_dispatch(x, batch, numel, numel, bits, eps, absmax_bits, codes, packed,
-                                deq, scale, err_w, err_ncols, err_out,
+                                deq, scale, err_w, err_ncols, err_w_stride, err_out,
                                 reinterpret_cast<double*>(ws), as_stream(stream));
 }
 
@@ -786,8 +790,8 @@ int cq_unpack_codes(const uint8_t* packed, int64_t batch, int64_t numel, int bit
 }
 
 int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const float* scale,
-                      int bits, const float* ycol, int64_t batch, int64_t m, int64_t n, float* Y,
-                      float* res_out, void* stream) {
+                      int bits, const float* ycol, int64_t ycol_stride, int64_t batch, int64_t m, int64_t n,
+                      float* Y, float* res_out, void* stream) {
     CQ_REQUIRE(Ws && batch > 0 && m > 0 && n > 0 && (Y || res_out), "cq_build_residual: bad args");
     CQ_REQUIRE(n % 4 == 0, "cq_build_residual: n %% 4 != 0");
     CQ_REQUIRE(!packed || scale || bits == 32, "cq_build_residual: scale required with codes");
@@ -795,7 +799,7 @@ int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const fl
     const int g = grid_for(m * n, batch);
     dim3 grid(g, batch);
     hipStream_t s = as_stream(stream);
-#define CQ_BR(DT, B) build_residual_kernel<DT, B><<<grid, kThreads, 0, s>>>(Ws, packed, scale, ycol, m, n, Y, res_out)
+#define CQ_BR(DT, B) build_residual_kernel<DT, B><<<grid, kThreads, 0, s>>>(Ws, packed, scale, ycol, m, n, Y, res_out, ycol_stride)
     const int bsel = packed ? bits : 2;
     if (dtype == CQ_F16) {
         switch (bsel) { case 2: CQ_BR(CQ_F16, 2); break; case 4: CQ_BR(CQ_F16, 4); break;

@@ -122,6 +122,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const int64_t qq = total / 8, r8 = total % 8, xcd = orig % 8;
     const int64_t lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + orig / 8;
     const int64_t b = lin / panels, panel = lin % panels;
+    const float* __restrict__ ewb = q.ew ? q.ew + b * q.sew : nullptr;  // this matrix's error weights
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, lq = lane >> 4;
@@ -200,7 +201,7 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
     const bool ewl = PASS == 2 && WL && q.ew != nullptr;
     auto issue_ew = [&](int64_t chn) {
         if (ewl && wid == 0 && lane < 8)
-            __builtin_amdgcn_global_load_lds((const void*)(q.ew + chn * QP_BN + 4 * lane),
+            __builtin_amdgcn_global_load_lds((const void*)(ewb + chn * QP_BN + 4 * lane),
                                              (__attribute__((address_space(3))) void*)(ewslot + 32 * (chn & 1)), 16, 0,
                                              0);
     };
@@ -412,8 +413,8 @@ __device__ __forceinline__ void qp_body(const QUK& q, const uint16_t* __restrict
                     e4[t] = d * d;
                     cf[4 * h + t] = c;
                 }
-                if (q.ew) {  // error column weights (activation-aware error, alg.py:286-302)
-                    const float4 wv = *reinterpret_cast<const float4*>(q.ew + n0 + 8 * lq + 4 * h);
+                if (ewb) {  // error column weights (activation-aware error, alg.py:286-302)
+                    const float4 wv = *reinterpret_cast<const float4*>(ewb + n0 + 8 * lq + 4 * h);
                     e4[0] *= wv.x; e4[1] *= wv.y; e4[2] *= wv.z; e4[3] *= wv.w;
                 }
                 err += (double)((e4[0] + e4[1]) + (e4[2] + e4[3]));  // fp32 within a run of 4, fp64 across
@@ -669,7 +670,7 @@ __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw
                 atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
                 const float d = c * s - x;
                 if (q.ew) {
-                    const float w = q.ew[(int64_t)en.x % n];
+                    const float w = q.ew[b * q.sew + (int64_t)en.x % n];
                     delta += (double)((d * d) * w) - (double)((x * x) * w);
                 } else {
                     delta += (double)(d * d) - (double)(x * x);
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(256) void qp_codes_kernel(QUK q, int panels, int nw
                     atomicXor(&qc_lds[loc >> 4], (c > 0.f ? 3u : 1u) << sh);
                     const float d = c * s - x;
                     if (q.ew) {
-                        const float w = q.ew[(loc + base) % n];
+                        const float w = q.ew[b * q.sew + (loc + base) % n];
                         delta += (double)((d * d) * w) - (double)((x * x) * w);
                     } else {
                         delta += (double)(d * d) - (double)(x * x);

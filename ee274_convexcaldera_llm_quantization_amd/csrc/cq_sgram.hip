@@ -48,10 +48,11 @@ __global__ __launch_bounds__(256) void sgram_count_kernel(const uint8_t* __restr
                                                           int32_t* __restrict__ row_nnz, const _Float16* __restrict__ W,
                                                           const float* __restrict__ qscale,
                                                           const float* __restrict__ wcol, double* __restrict__ row_corr,
-                                                          int64_t Lh, int32_t* __restrict__ row_nnz1) {
+                                                          int64_t Lh, int32_t* __restrict__ row_nnz1, int64_t wcs) {
     const int lane = threadIdx.x & 63;
     const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t b = blockIdx.y;
+    if (wcol) wcol += b * wcs;  // per-matrix column weights (stride 0: shared)
     if (j >= k) return;
     const uint32_t* row = reinterpret_cast<const uint32_t*>(packed + b * (k * L / 4) + j * (L / 4));
     const int64_t nw = L / 16;
@@ -461,9 +462,10 @@ __global__ __launch_bounds__(1024) void sgram_spmm_kernel(const _Float16* __rest
                                                          const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ slice_off,
                                                          const int32_t* __restrict__ slice_w1, int64_t Lh,
-                                                         int64_t stride_ell, float* __restrict__ P) {
+                                                         int64_t stride_ell, float* __restrict__ P, int64_t wcs) {
     extern __shared__ __attribute__((aligned(16))) float slab[];
     const int64_t b = blockIdx.y;
+    if (wcol) wcol += b * wcs;  // per-matrix column weights (stride 0: shared)
     const int64_t i0 = (int64_t)blockIdx.x * R;
     const float hs = 0.5f * qscale[b];
     const int64_t KL = k * L;
@@ -800,12 +802,15 @@ __global__ __launch_bounds__(256) void codes_matmul_kernel(const uint32_t* __res
                                                            int64_t cols, const float* __restrict__ X, int64_t ldx,
                                                            int64_t sx, const float* __restrict__ w,
                                                            const float* __restrict__ roww, int r,
-                                                           float* __restrict__ out, int64_t ldo, int64_t so) {
+                                                           float* __restrict__ out, int64_t ldo, int64_t so,
+                                                           int64_t ws_, int64_t rws) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cm_lds[];
     uint32_t* list = cm_lds + (threadIdx.x >> 6) * CM_LIST;
     float* tile = reinterpret_cast<float*>(cm_lds + 4 * CM_LIST);   // TRANS: [r][65]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t b = blockIdx.y, row0 = (int64_t)blockIdx.x * 64;
+    if (w) w += b * ws_;        // per-matrix column / row weights (stride 0: shared)
+    if (roww) roww += b * rws;
     const int64_t nw = cols / 16;
     const uint32_t* pb = packed + b * rows * nw;
     const float* Xb = X + b * sx;
@@ -929,9 +934,10 @@ __global__ __launch_bounds__(1024) void codes_ysq_corr_kernel(const uint32_t* __
                                                               const _Float16* __restrict__ W,
                                                               const float* __restrict__ qscale,
                                                               const float* __restrict__ w, int64_t rows,
-                                                              int64_t cols, double* __restrict__ out) {
+                                                              int64_t cols, double* __restrict__ out, int64_t wst) {
     __shared__ double red[16];
     const int64_t b = blockIdx.x;
+    if (w) w += b * wst;  // per-matrix column weights (stride 0: shared)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const double s = (double)qscale[b];
     const int64_t nw = cols / 16;
@@ -991,8 +997,9 @@ int cq_codes_transpose(const uint8_t* packed, int bits, int64_t batch, int64_t r
 }
 
 int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, const float* X,
-                    int64_t ldx, int64_t stride_x, const float* colw, const float* roww, int64_t r, float* out,
-                    int64_t ldo, int64_t stride_out, int trans, void* stream) {
+                    int64_t ldx, int64_t stride_x, const float* colw, int64_t colw_stride, const float* roww,
+                    int64_t roww_stride, int64_t r, float* out, int64_t ldo, int64_t stride_out, int trans,
+                    void* stream) {
     CQ_REQUIRE(packed && X && out, "cq_codes_matmul: null argument");
     CQ_REQUIRE(bits == 2, "cq_codes_matmul: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0 && cols % 16 == 0 && cols < (1ll << 29),
@@ -1003,7 +1010,7 @@ int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows
     hipStream_t s = as_stream(stream);
     const uint32_t* pk = reinterpret_cast<const uint32_t*>(packed);
 #define CQ_CM(RV, T) codes_matmul_kernel<RV, T><<<grid, 256, lds, s>>>(pk, rows, cols, X, ldx, stride_x, colw, roww, (int)r, \
-                                                                       out, ldo, stride_out)
+                                                                       out, ldo, stride_out, colw_stride, roww_stride)
     const int rv = (int)ceil_div(r, 64);
     if (trans) {
         if (rv == 1) CQ_CM(1, true); else if (rv == 2) CQ_CM(2, true); else if (rv == 3) CQ_CM(3, true); else CQ_CM(4, true);
@@ -1015,12 +1022,12 @@ int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows
 }
 
 int cq_codes_ysq_corr(const uint8_t* packed, int bits, const void* W, int dtype, const float* qscale, const float* colw,
-                      int64_t batch, int64_t rows, int64_t cols, double* out, void* stream) {
+                      int64_t colw_stride, int64_t batch, int64_t rows, int64_t cols, double* out, void* stream) {
     CQ_REQUIRE(packed && W && qscale && out, "cq_codes_ysq_corr: null argument");
     CQ_REQUIRE(bits == 2 && dtype == CQ_F16, "cq_codes_ysq_corr: 2-bit codes, fp16 W only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && rows > 0 && cols > 0 && cols % 16 == 0, "cq_codes_ysq_corr: bad shape");
     codes_ysq_corr_kernel<<<(unsigned)batch, 1024, 0, as_stream(stream)>>>(
-        reinterpret_cast<const uint32_t*>(packed), reinterpret_cast<const _Float16*>(W), qscale, colw, rows, cols, out);
+        reinterpret_cast<const uint32_t*>(packed), reinterpret_cast<const _Float16*>(W), qscale, colw, rows, cols, out, colw_stride);
     return check_launch("cq_codes_ysq_corr");
 }
 
@@ -1034,8 +1041,8 @@ int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t col
 
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
                    int32_t* perm, int64_t* slice_off, int64_t* total, int64_t Lh, int32_t* row_nnz1,
-                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, double* corr_ws,
-                   double* corr_out, void* stream) {
+                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, int64_t wcol_stride,
+                   double* corr_ws, double* corr_out, void* stream) {
     CQ_REQUIRE(packed && row_nnz && perm && slice_off && total, "cq_sgram_count: null argument");
     CQ_REQUIRE(bits == 2, "cq_sgram_count: 2-bit codes only");
     CQ_REQUIRE(batch > 0 && batch < 65536 && k > 0 && L > 0 && L % 64 == 0, "cq_sgram_count: bad shape");
@@ -1046,7 +1053,7 @@ int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, in
     hipStream_t s = as_stream(stream);
     sgram_count_kernel<<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), 256, 0, s>>>(
         packed, k, L, row_nnz, reinterpret_cast<const _Float16*>(W), qscale, wcol, corr_ws, split ? Lh : L,
-        split ? row_nnz1 : nullptr);
+        split ? row_nnz1 : nullptr, wcol_stride);
     sgram_slices_kernel<<<(unsigned)batch, 256, 0, s>>>(row_nnz, k, perm, slice_off, total, W ? corr_ws : nullptr,
                                                         corr_out, split ? row_nnz1 : nullptr, slice_w1);
     return check_launch("cq_sgram_count");
@@ -1080,7 +1087,7 @@ int64_t cq_sgram_split(int64_t k, int64_t L) {
 }
 
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
-                  int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
+                  int64_t wcol_stride, int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
                   const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh, int64_t stride_ell, float* P,
                   void* stream) {
     CQ_REQUIRE(W && packed && qscale && ell && perm && slice_off && P, "cq_sgram_spmm: null argument");
@@ -1092,7 +1099,7 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
         CQ_REQUIRE(Lh == cq_sgram_split(k, L) && slice_w1, "cq_sgram_spmm: Lh must be cq_sgram_split(k, L)");
         const size_t lds = ((size_t)Lh * 4 + (size_t)k * 4) * sizeof(float);
         sgram_spmm_kernel<4, -1, true><<<dim3((unsigned)ceil_div(k, 4), (unsigned)batch), SG_THREADS, lds, s>>>(
-            Wh, packed, qscale, wcol, k, L, ell, perm, slice_off, slice_w1, Lh, stride_ell, P);
+            Wh, packed, qscale, wcol, k, L, ell, perm, slice_off, slice_w1, Lh, stride_ell, P, wcol_stride);
         return check_launch("cq_sgram_spmm");
     }
     const int R = cq_sgram_rows(L);
@@ -1108,7 +1115,8 @@ int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* 
     const bool ldsout = !held && R < 8 && lds + (size_t)k * R * sizeof(float) <= 150 * 1024;
     if (ldsout) lds += (size_t)k * R * sizeof(float);
 #define CQ_SP(RR, NN) sgram_spmm_kernel<RR, NN><<<grid, SG_THREADS, lds, s>>>(Wh, packed, qscale, wcol, k, L, ell, \
-                                                                             perm, slice_off, nullptr, L, stride_ell, P)
+                                                                             perm, slice_off, nullptr, L, stride_ell, P, \
+                                                                             wcol_stride)
     if (R == 8) {
         if (held) CQ_SP(8, 4); else CQ_SP(8, 0);
     } else if (R == 4) {

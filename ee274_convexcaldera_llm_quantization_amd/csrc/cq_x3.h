@@ -36,6 +36,7 @@ struct X3K {
     int ksplit;                // > 1: K cut into ksplit chunks, fp32 partials in part (split-K)
     float* part;               // [ksplit][batch][M][N]
     const float* colw = nullptr;  // [N] (or NULL): the product term scaled per C column
+    int64_t scolw = 0;            // colw batch stride (0: one vector for every matrix)
     uint32_t* absmax_out = nullptr;  // [batch] (or NULL, plain products): atomic max of |C| bits
     float* Ct = nullptr; int64_t sct = 0;  // C^T too (N x M, row stride M), batch stride sct
 };
@@ -54,6 +55,7 @@ struct QUK {
     uint8_t* packed;             // packed bytes (m n bits / 8), or NULL
     float* scale;                // [batch] out (pass 1)
     const float* ew;             // error column weights [n] or NULL (= 1)
+    int64_t sew = 0;             // ew batch stride (0: one vector for every matrix)
     double* part;                // [batch * tiles] error partials
     // single-recompute 2-bit path (qp_launch cand = true): pass 2 = pass 0 + the error of
     // all-zero codes + a list of the candidates |res| >= tau (tau = QP_TAU x the previous

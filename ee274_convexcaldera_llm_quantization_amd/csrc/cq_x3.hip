@@ -622,9 +622,10 @@ __global__ __launch_bounds__(XW_THREADS, 1) void gemm_x3v_kernel(X3K a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = al_ * (acc[i][j][r] * sc);
             if (a.colw) {
+                const float* cw = a.colw + b * a.scolw;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (col + r < a.N) v[r] *= a.colw[col + r];
+                    if (col + r < a.N) v[r] *= cw[col + r];
             }
             if (vec) {
                 if (a.P && be_ != 0.f) {
@@ -829,7 +830,7 @@ __global__ __launch_bounds__(256) void x3_splitk_epi_kernel(X3K a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         float w = al_ * s[r];
-        if (a.colw) w *= a.colw[col + r];
+        if (a.colw) w *= a.colw[b * a.scolw + col + r];
         if (a.P && be_ != 0.f) w += be_ * a.P[b * a.sp + row * a.ldp + col + r];
         if (a.D && ga_ != 0.f) w += ga_ * a.D[b * a.sd + row * a.ldd + col + r];
         a.C[b * a.sc + row * a.ldc + col + r] = w;
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void q_update_x3_kernel(QUK q) {
                     for (int u = 0; u < 4; ++u) {
                         c[u] = quant_code(v[u], s, kq);
                         const float d = dequant(c[u], kq, s) - v[u];
-                        err += (double)(d * d) * (q.ew ? (double)q.ew[col + u] : 1.0);
+                        err += (double)(d * d) * (q.ew ? (double)q.ew[b * q.sew + col + u] : 1.0);
                     }
                     if constexpr (BITS <= 4) {
                         if (q.packed) {
@@ -1043,7 +1044,7 @@ __global__ __launch_bounds__(XW_THREADS, 1) void q_update_v_kernel(QUK q) {
             int cq[4];
             float e4[4];
             float4 wv = make_float4(1.f, 1.f, 1.f, 1.f);
-            if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + col + 4 * j);
+            if (q.ew) wv = *reinterpret_cast<const float4*>(q.ew + b * q.sew + col + 4 * j);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float c = quant_code_r(v[r], s, ys, kq);
@@ -1197,7 +1198,7 @@ __device__ __forceinline__ void qstream_load(const QUK& q, int64_t b, int64_t MN
     // load_ew false: the caller holds them (a thread whose columns do not change)
     if (!load_ew) return qstream_load<DT>(q, b, MN, e, wr);
     if (q.ew) {
-        const float* ew = q.ew + e % q.n;
+        const float* ew = q.ew + b * q.sew + e % q.n;
 #pragma unroll
         for (int j = 0; j < 4; ++j) ewv[j] = *reinterpret_cast<const float4*>(ew + 4 * j);
     } else {
@@ -1309,13 +1310,20 @@ __global__ __launch_bounds__(256) void residual_split_kernel(
     const float* __restrict__ ycol, const float* __restrict__ wmax, float ycmax, int64_t m, int64_t n,
     float* __restrict__ res, float* __restrict__ Y, _Float16* __restrict__ hi, _Float16* __restrict__ lo,
     _Float16* __restrict__ thi, _Float16* __restrict__ tlo, float* __restrict__ scale_out,
-    double* __restrict__ part, const float* __restrict__ ycol_hi, float ychmax, float* __restrict__ scale_hi_out) {
+    double* __restrict__ part, const float* __restrict__ ycol_hi, float ychmax, float* __restrict__ scale_hi_out,
+    int64_t ycs, const float* __restrict__ ycmax_v, const float* __restrict__ ychmax_v) {
     __shared__ float tile[64][33];
     __shared__ double red[4];
     constexpr float k = BITS == 32 ? 1.f : (float)((1 << (BITS - 1)) - 1);
     const int64_t b = blockIdx.z;
     const int64_t MN = m * n;
     const float qs = qc ? qscale[b] : 0.f;
+    // per-matrix column weights (distinct diagonal Hessians): this matrix's row of ycol / ycol_hi
+    // and its own bounds
+    if (ycol) ycol += b * ycs;
+    if (ycol_hi) ycol_hi += b * ycs;
+    if (ycmax_v) ycmax = ycmax_v[b];
+    if (ychmax_v) ychmax = ychmax_v[b];
     int e2 = 0;
     {
         const float bnd = (wmax[b] + qs) * ycmax;
@@ -1846,9 +1854,9 @@ int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out
 
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch, const uint16_t* Lh,
                    const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl, const float* inv_scale, int bits,
-                   float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w, double* err_out,
-                   const float* absmax_in, const float* scale_hint, int* fallback_out, void* ws, size_t ws_bytes,
-                   void* stream) {
+                   float eps, void* codes, uint8_t* packed, float* scale_out, const float* err_w,
+                   int64_t err_w_stride, double* err_out, const float* absmax_in, const float* scale_hint,
+                   int* fallback_out, void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(W && m > 0 && n > 0 && batch > 0 && r >= 0, "cq_q_update_x3: bad shape");
     CQ_REQUIRE(dtype == CQ_F16 || dtype == CQ_F32, "cq_q_update_x3: dtype must be f16/f32");
     if (bits != 2 && bits != 4 && bits != 8 && bits != 16) return set_error(CQ_EINVAL, "Bit-width not supported!");
@@ -1864,7 +1872,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     memset(&q, 0, sizeof(q));  // a_blocked = b_blocked = 0, no active mask, no list path
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool vk = n % 16 == 0 && al16(W) && (!codes || al16(codes)) && (!packed || al16(packed)) &&
-                    (!err_w || al16(err_w));
+                    (!err_w || (al16(err_w) && err_w_stride % 4 == 0));
     if (vk) {
         // A operand L (m x r): tile rows run over W's rows; B operand R^T (n x r): tile
         // columns over W's columns (see q_update_v_kernel)
@@ -1893,7 +1901,7 @@ int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, in
     q.W = W; q.wf16 = dtype == CQ_F16; q.m = m; q.n = n;
     q.absmax = reinterpret_cast<uint32_t*>(ws);
     q.part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + align_up((size_t)batch * sizeof(uint32_t), 256));
-    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w;
+    q.eps = eps; q.codes = codes; q.packed = packed; q.scale = scale_out; q.ew = err_w; q.sew = err_w ? err_w_stride : 0;
     hipStream_t s = as_stream(stream);
     const bool known = absmax_in && r == 0;  // max|W| bits given: skip the absmax pass
     if (known) {
@@ -2002,6 +2010,7 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
                       const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m, int64_t n,
                       float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo, uint16_t* thi, uint16_t* tlo,
                       float* scale_out, double* sq_out, const float* ycol_hi, float ycol_hi_max, float* scale_hi_out,
+                      int64_t ycol_stride, const float* ycol_max_v, const float* ycol_hi_max_v,
                       void* ws, size_t ws_bytes, void* stream) {
     CQ_REQUIRE(Ws && wmax && batch > 0 && batch < 65536 && m > 0 && n > 0, "cq_residual_split: bad args");
     CQ_REQUIRE(m % 32 == 0 && n % 64 == 0, "cq_residual_split: m % 32 and n % 64 must be 0");
@@ -2019,7 +2028,8 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
     double* part = sq_out ? reinterpret_cast<double*>(ws) : nullptr;
     auto h = [](uint16_t* p) { return reinterpret_cast<_Float16*>(p); };
 #define CQ_RS(DT, B) residual_split_kernel<DT, B><<<grid, 256, 0, s>>>(Ws, packed, qscale, ycol, wmax, ycol_max, m, n, \
-        res_out, Y_out, h(hi), h(lo), h(thi), h(tlo), scale_out, part, ycol_hi, ycol_hi_max, scale_hi_out)
+        res_out, Y_out, h(hi), h(lo), h(thi), h(tlo), scale_out, part, ycol_hi, ycol_hi_max, scale_hi_out, \
+        ycol_stride, ycol_max_v, ycol_hi_max_v)
     const int bsel = packed ? bits : 2;
     if (dtype == CQ_F16) {
         switch (bsel) { case 2: CQ_RS(CQ_F16, 2); break; case 4: CQ_RS(CQ_F16, 4); break;
@@ -2070,6 +2080,7 @@ int cq_gemm_x3(const cq_x3_args* g, void* stream) {
                "cq_gemm_x3: tri needs a square plain product");
     a.single = g->single;
     a.colw = g->colw;
+    a.scolw = g->stride_colw;
     a.absmax_out = g->absmax_out;
     a.Ct = g->Ct;
     a.sct = g->stride_ct;

@@ -82,12 +82,22 @@ class _Weights:
     ycol  : diag of H_sqrt (data-aware) — Y = residual * ycol  (alg.py:211)
     rinv  : 1/sqrt(eigenvalues) in original column order (alg.py:223)
     lplr  : weights of ||(res - L R) H_sqrt||^2 (alg.py:182): ycol^2 (aware) / h^2 (not)
+
+    Shared H: (n,) vectors and a float ycol_max.  Per-matrix diagonal H (`batched`, h (B, n):
+    main.py:163-165 gives every layer its own Hall[name]): (B, n) vectors, row b matrix b's,
+    and ycol_max (B,) fp32 -- the kernels read row b at a batch stride (ABI 5).  Every row takes
+    the same arithmetic as a shared h would (the sigma_reg shift only where that row needs
+    it), so a matrix gets the same weights in a mixed batch as alone.  The flags (identity,
+    err_unit) choose code paths and must agree over the batch (`kind` groups callers' matrices).
     """
 
     dense = False
 
-    def __init__(self, h: torch.Tensor | None, n: int, p: EngineParams, dev):
+    def __init__(self, h: torch.Tensor | None, n: int, p: EngineParams, dev, batched: bool = False):
         f32 = torch.float32
+        if batched:
+            self._init_batched(h.to(device=dev, dtype=f32), n, p, dev)
+            return
         if h is not None and h.dim() == 2:
             self._init_dense(h.to(device=dev, dtype=f32), n, p, dev)
             return
@@ -120,6 +130,55 @@ class _Weights:
         self.rinv = None if self.identity else 1.0 / sq
         self.lplr = None if self.identity else lam  # ||Y - L (R*ycol)||^2 uses unit weights
         self.err_unit = bool(torch.all(herr == 1.0).item())
+
+    @staticmethod
+    def kind(h: torch.Tensor | None, n: int, p: EngineParams, dev) -> tuple:
+        """(identity, err_unit) of one matrix's diagonal h: matrices batched with per-matrix
+        weights must agree on them (they select code paths, not values)."""
+        w = _Weights(h, n, p, dev)
+        return (w.identity, w.err_unit)
+
+    def _init_batched(self, h: torch.Tensor, n: int, p: EngineParams, dev):
+        """Per-matrix diagonal H, h (B, n): row b is what _Weights(h[b]) computes for that
+        matrix alone (alg.py:11-23, :44-68), evaluated for all rows at once."""
+        f32 = torch.float32
+        B = h.shape[0]
+        assert h.dim() == 2 and h.shape[1] == n
+        h = h.contiguous()
+        if not p.activation_aware_LR:
+            unit = torch.all(h == 1.0, dim=1).tolist()
+            if len(set(unit)) > 1:
+                raise ValueError("per-matrix H: unit and non-unit error weights in one batch (group by _Weights.kind)")
+            self.err = h
+            self.err_unit = unit[0]
+            self.ycol = None
+            self.ycol_max = 1.0
+            self.rinv = None
+            self.lplr = (h * h).contiguous()
+            self.identity = False
+            return
+        ident = torch.all(torch.abs(h - 1.0) <= 1e-8 + 1e-5, dim=1)  # optimized_eigh per matrix
+        lam = torch.where(ident.view(B, 1), torch.ones_like(h), h)
+        herr = h.clone()
+        lmin = lam.min(dim=1).values
+        # alg.py:59-64 per matrix: the comparison in double as float(lmin.item()) < sigma_reg,
+        # the shift in fp32 (sigma_reg - lmin) added only to the rows that need it
+        need = (lmin.double() < p.sigma_reg).view(B, 1)
+        shift = (torch.tensor(p.sigma_reg, dtype=f32, device=dev) - lmin).view(B, 1)
+        herr = torch.where(need, herr + shift, herr)
+        lam = torch.where(need, lam + shift, lam)
+        identity = (ident & torch.all(lam == 1.0, dim=1)).tolist()
+        err_unit = torch.all(herr == 1.0, dim=1).tolist()
+        if len(set(identity)) > 1 or len(set(err_unit)) > 1:
+            raise ValueError("per-matrix H: identity and non-identity weights in one batch (group by _Weights.kind)")
+        self.identity = identity[0]
+        self.err = herr.contiguous()
+        sq = torch.sqrt(lam).contiguous()
+        self.ycol = None if self.identity else sq
+        self.ycol_max = 1.0 if self.identity else sq.max(dim=1).values.contiguous()
+        self.rinv = None if self.identity else (1.0 / sq).contiguous()
+        self.lplr = None if self.identity else lam.contiguous()
+        self.err_unit = err_unit[0]
 
 
     def _init_dense(self, H, n, p: EngineParams, dev):
@@ -1002,7 +1061,8 @@ class CalderaEngine:
     # ------------------------------------------------------------------ driver
     def run(self, W: torch.Tensor, h: torch.Tensor | None = None, scale_W: bool = True,
             use_tqdm: bool = False):
-        """W (B, m, n) fp16/fp32 on a HIP device; h: (n,) diagonal of H or None.
+        """W (B, m, n) fp16/fp32 on a HIP device; h: (n,) diagonal of H, (n, n) dense H, None,
+        or a list of B per-matrix diagonals (each (n,) or None: distinct Hessians, main.py:163-165).
         Returns a list of per-matrix result dicts (see api.py for the dataclass view)."""
         return run_to_end(self.run_iter(W, h, scale_W, use_tqdm))
 
@@ -1036,6 +1096,16 @@ class CalderaEngine:
         if p.compute_low_rank_factors and "LR" in p.update_order and (p.L_bits < 16 or p.R_bits < 16):
             qlog.check_method_bits(p.method_LR, p.L_bits)
             qlog.check_method_bits(p.method_LR, p.R_bits)
+        per_matrix = isinstance(h, (list, tuple))
+        if per_matrix:
+            # one diagonal per matrix, stacked (B, n); None = H = I for that matrix
+            if len(h) != B:
+                raise ValueError(f"{len(h)} per-matrix H for a batch of {B}")
+            for x in h:
+                if x is not None and (x.dim() != 1 or x.shape[0] != n):
+                    raise NotImplementedError("per-matrix H must be diagonals of length n (dense H: one per batch)")
+            h = torch.stack([torch.ones(n, dtype=torch.float32, device=dev) if x is None
+                             else x.to(device=dev, dtype=torch.float32) for x in h])
         gs, Ws = K.rms_scale(W, scale_W)  # on the true numel (alg.py:38-42)
         Ws_out = Ws
         host_copy = self._start_host_copy(Ws) if w_to_host else None
@@ -1050,9 +1120,11 @@ class CalderaEngine:
             n_true = n
             Ws = torch.nn.functional.pad(Ws, (0, pad))
             n = n + pad
-            if h is not None:
+            if h is not None and per_matrix:
+                h = torch.cat([h, h.max(dim=1, keepdim=True).values.expand(B, pad)], dim=1)
+            elif h is not None:
                 h = torch.cat([h, h.max().expand(pad)])
-        wts = _Weights(h, n, p, dev)
+        wts = _Weights(h, n, p, dev, batched=per_matrix)
         self._wmax = K.absmax(Ws)  # bound for the split scale of the LR-step residual
         self._w_finite = None
         self._sg_A = self._sg = self._sg_w = None  # sparse-code Gram (sgram.py): A per run

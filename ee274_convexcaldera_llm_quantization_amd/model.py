@@ -13,8 +13,10 @@ Here the selection and accounting are the reference's (including its substring l
 `any(f'layers.{i}' in name ...)`, main.py:158), the Hessian diagonal is passed as a vector
 (no n x n diag_embed), `Q + L R` is one fused HIP GEMM epilogue, and the Hadamard branch
 (main.py:224-240, `H1 W H2` with normalised Sylvester matrices padded to powers of two) runs
-as HIP GEMMs on the device instead of numpy on the host.  Layers that share a shape and a
-Hessian (H = None, the synthetic configs) are decomposed in one lockstep batch.
+as HIP GEMMs on the device instead of numpy on the host.  Layers that share a shape are
+decomposed in one lockstep batch, each with its own Hessian diagonal (the engine reads
+per-matrix weights at a batch stride; api.caldera_batch groups by code-path flags and
+interleaves the groups on HIP streams), where the reference runs one caldera() per layer.
 """
 from __future__ import annotations
 
@@ -193,62 +195,66 @@ def apply_caldera_quantization(model: torch.nn.Module, hessians=None, quant_para
     hadamard_gate: apply the 0.99 error gate and the bit accounting to the Hadamard branch
       too (off by default: main.py:221-240 writes the recovered weight unconditionally and
       counts nothing).
-    decompose(quant_params, Ws, H) -> list of CalderaDecomposition: the engine
-      (`api.caldera_batch`) unless given (tests pass a stand-in).
+    decompose(quant_params, Ws, H) -> list of CalderaDecomposition: the engine unless given
+      (tests pass a stand-in).  The engine runs every shape batch at once
+      (`api.caldera_groups`: all batches interleaved on HIP streams).
     Returns the QuantizationReport (counters + per-layer outcomes)."""
-    if decompose is None:
-        from .api import caldera_batch
-
-        def decompose(qp, Ws, H):
-            return caldera_batch(qp, Ws, H, device=device, scale_W=scale_W)
     qp = quant_params if quant_params is not None else driver_params()
     say = log or (lambda *a: None)
     jobs, rep = select_layers(model, hessians, selection, say)
-    # batches: same shape, same Hessian object (None for all when hessians is None)
+    # batches: same shape; every layer keeps its own Hessian (a list of per-matrix H, or one
+    # shared H / None when the whole batch has the same object)
     groups: dict = {}
     for job in jobs:
-        key = (tuple(job[1].weight.shape), id(job[2]) if job[2] is not None else None)
-        groups.setdefault(key, []).append(job)
+        groups.setdefault(tuple(job[1].weight.shape), []).append(job)
     outcomes = {}
-    for key, members in groups.items():
-        for s in range(0, len(members), max_batch):
-            part = members[s:s + max_batch]
-            h = part[0][2]
-            with torch.no_grad():
+    batches = []  # (jobs, Ws, shapes, H)
+    with torch.no_grad():
+        for key, members in groups.items():
+            for s in range(0, len(members), max_batch):
+                part = members[s:s + max_batch]
+                h = part[0][2] if all(j[2] is part[0][2] for j in part) else [j[2] for j in part]
                 Ws, shapes = [], []
-                for name, module, _ in part:
+                for name, module, hj in part:
                     W = module.weight.data
                     if hadamard:  # main.py:224-232: transform, decompose the fp32 transform
-                        if h is not None and _next_pow2(W.shape[1]) != W.shape[1]:
+                        if hj is not None and _next_pow2(W.shape[1]) != W.shape[1]:
                             raise ValueError(f"{name}: Hadamard padding changes n ({W.shape[1]}) but H is n x n")
                         Wt, shp = hadamard_transform(W.to(device))
                         Ws.append(Wt)
                         shapes.append(shp)
                     else:
                         Ws.append(W)
-                decs = decompose(qp, Ws, h)
-                for (name, module, _), dec, i in zip(part, decs, range(len(part))):
-                    W = module.weight.data
-                    dev = W.device if W.device.type == "cuda" else torch.device(device)
-                    out = _reconstruct(dec, dev)
-                    if hadamard:
-                        out = hadamard_transform(out, inverse=True, original_shape=shapes[i]).contiguous()
-                    err = _rel_error(W.to(dev), out)
-                    if hadamard and not hadamard_gate:
-                        # main.py:221-240: the Hadamard branch always writes the recovered
-                        # weight back, with no error gate and no parameter counting
-                        module.weight.data = out.to(W.dtype).to(W.device)
-                        say(f"Applied CALDERA (Hadamard) to {name}.weight, shape: {tuple(W.shape)}")
-                        outcomes[name] = LayerOutcome(name, tuple(W.shape), err, True, dict(dec.errors))
-                        continue
-                    ok = err <= error_threshold
-                    if ok:
-                        module.weight.data = (out.to(W.dtype) if keep_dtype else out).to(W.device)
-                        rep.quantized_param_count += W.numel()
-                        say(f"Applied CALDERA to {name}.weight, shape: {tuple(W.shape)}")
-                    else:
-                        rep.unquantized_language_param_count += W.numel()
-                        say(f"Error of the decomposition is greater than threshold for {name}. Skipping quantization")
-                    outcomes[name] = LayerOutcome(name, tuple(W.shape), err, ok, dict(dec.errors))
+                batches.append((part, Ws, shapes, h))
+        if decompose is None:
+            from .api import caldera_groups
+            all_decs = caldera_groups(qp, [(Ws, h) for _, Ws, _, h in batches], device=device, scale_W=scale_W)
+        else:
+            all_decs = [decompose(qp, Ws, h) for _, Ws, _, h in batches]
+    for (part, Ws, shapes, h), decs in zip(batches, all_decs):
+        with torch.no_grad():
+            for (name, module, _), dec, i in zip(part, decs, range(len(part))):
+                W = module.weight.data
+                dev = W.device if W.device.type == "cuda" else torch.device(device)
+                out = _reconstruct(dec, dev)
+                if hadamard:
+                    out = hadamard_transform(out, inverse=True, original_shape=shapes[i]).contiguous()
+                err = _rel_error(W.to(dev), out)
+                if hadamard and not hadamard_gate:
+                    # main.py:221-240: the Hadamard branch always writes the recovered
+                    # weight back, with no error gate and no parameter counting
+                    module.weight.data = out.to(W.dtype).to(W.device)
+                    say(f"Applied CALDERA (Hadamard) to {name}.weight, shape: {tuple(W.shape)}")
+                    outcomes[name] = LayerOutcome(name, tuple(W.shape), err, True, dict(dec.errors))
+                    continue
+                ok = err <= error_threshold
+                if ok:
+                    module.weight.data = (out.to(W.dtype) if keep_dtype else out).to(W.device)
+                    rep.quantized_param_count += W.numel()
+                    say(f"Applied CALDERA to {name}.weight, shape: {tuple(W.shape)}")
+                else:
+                    rep.unquantized_language_param_count += W.numel()
+                    say(f"Error of the decomposition is greater than threshold for {name}. Skipping quantization")
+                outcomes[name] = LayerOutcome(name, tuple(W.shape), err, ok, dict(dec.errors))
     rep.layers = [outcomes[j[0]] for j in jobs]
     return rep

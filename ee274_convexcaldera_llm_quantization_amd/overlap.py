@@ -14,6 +14,8 @@ single host thread.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 
@@ -65,15 +67,13 @@ def run_interleaved(gens, device, ready_first: bool = True):
     if len(gens) == 1:
         return [run_to_end(gens[0])]
     # concurrent batches fill the chip together: a small batch's split-fp16 products need no
-    # split-K here (_lib.AUTO_SPLIT_K; its partial sums and epilogue launches only add traffic:
-    # config-4 rank share 0.159 -> 0.136 s, profiles/r05f_share*.log)
+    # split-K here (its partial sums and epilogue launches only add traffic: config-4 rank
+    # share 0.159 -> 0.136 s, profiles/r05f_share*.log).  The policy is this thread's only
+    # (_lib.split_k_policy), so a matrix's summation order depends on whether its batch is
+    # split into parts (default_parts: from 16 matrices on), not on other threads' calls.
     from . import _lib
-    auto_split = _lib.AUTO_SPLIT_K
-    _lib.AUTO_SPLIT_K = False
-    try:
+    with _lib.split_k_policy(False):
         return _run_interleaved(gens, device, ready_first)
-    finally:
-        _lib.AUTO_SPLIT_K = auto_split
 
 
 def _run_interleaved(gens, device, ready_first):
@@ -102,11 +102,17 @@ def _run_interleaved(gens, device, ready_first):
                 # started / resumed since its work completed
                 pick = None
                 order = sorted(live, key=lambda j: (j - nxt) % len(gens))
+                spins = 0
                 while pick is None:
                     for j in order:
                         if not pending[j] or events[j].query():
                             pick = j
                             break
+                    spins += 1
+                    if pick is None and spins >= 64:
+                        # every part is waiting on the GPU: poll at ~0.1 ms instead of keeping a
+                        # host core at 100 % (other ranks share the host); still ready-first
+                        time.sleep(1e-4)
                 i = pick
                 pending[i] = False
                 torch.cuda.set_stream(streams[i])

@@ -3,8 +3,8 @@
 The reference decomposes a model's linear layers one after another in one process
 (main.py:135-251, `apply_CALDERA_quantization`).  The units are independent (no state is
 shared between `caldera()` calls), so here every rank (one process per GPU)
-decomposes the matrices i with i % world == rank, batching same-shape, same-H matrices in
-lockstep on its GPU, and the only collective is the final gather of the packed results to
+decomposes the matrices i with i % world == rank, batching same-shape matrices in lockstep on
+its GPU (each with its own diagonal Hessian: per-matrix weights, ABI 5), and the only collective is the final gather of the packed results to
 rank 0 (torch.distributed `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo" on
 CPU tests).
 
@@ -173,8 +173,8 @@ def decompose_sharded(items, decompose_batch, *, rank: int, world: int, max_batc
                       group=None, gather: bool = True, device=None, h_key=None, resume_path=None):
     """items: list of (name, m, n, seed).  decompose_batch(list_of_items) -> list of
     MatrixResult (the GPU engine on MI355X; a stub in the CPU gloo tests).  Matrices of this
-    rank's shard that share shape AND Hessian (h_key(name), default: all the same) run
-    together in batches of <= max_batch.  resume_path: per-rank results file; names in it
+    rank's shard that share a shape run together in batches of <= max_batch, each with its
+    own Hessian (h_key(name): an optional extra grouping key).  resume_path: per-rank results file; names in it
     are not decomposed again, and it is rewritten with this rank's results at the end."""
     mine = [items[i] for i in shard_indices(len(items), world, rank)]
     done = []
@@ -225,9 +225,9 @@ def decompose_sharded(items, decompose_batch, *, rank: int, world: int, max_batc
 
 def engine_decompose_batch(quant_params, device, H_of=None):
     """decompose_batch for the MI355X engine: synthetic fp16 weights randn*0.02 per seed
-    (random-init model, no checkpoint access), H_of(name) -> diagonal (n,) or None.  Every
-    matrix of a batch must have the same H (decompose_sharded groups by h_key; this checks)."""
-    from .engine import CalderaEngine, EngineParams
+    (random-init model, no checkpoint access), H_of(name) -> diagonal (n,) or None per matrix
+    (distinct Hessians share a batch: api._Group groups them by code-path flags only)."""
+    from .api import _Group
     from .overlap import run_interleaved
 
     def weights(batch_items):
@@ -241,19 +241,18 @@ def engine_decompose_batch(quant_params, device, H_of=None):
         if H_of is None:
             return None
         hs = [H_of(it[0]) for it in batch_items]
-        h0 = hs[0]
-        for h in hs[1:]:
-            if h is not h0 and not (h is not None and h0 is not None and torch.equal(h, h0)):
-                raise ValueError("engine_decompose_batch: matrices of one batch need the same H "
-                                 "(pass h_key to decompose_sharded)")
-        return h0
+        if all(h is hs[0] for h in hs):
+            return None if hs[0] is None else hs[0].to(device)
+        return [None if h is None else h.to(device) for h in hs]
 
-    def results(batch_items, eng):
-        out = []
-        for (name, m, n, seed), d in zip(batch_items, eng.last_packed):
-            extra = {"n_padded": d["n_padded"]} if "n_padded" in d else {}
-            out.append(MatrixResult(name, m, n, d["L"].shape[1], quant_params.Q_bits, d["codes"], d["Q_scale"],
-                                    d["L"], d["R"], d["global_scale"], d["errors"], extra))
+    def results(batch_items, group):
+        out = [None] * len(batch_items)
+        for idx, eng, _ in group.parts:
+            for b, d in zip(idx, eng.last_packed):
+                name, m, n, seed = batch_items[b]
+                extra = {"n_padded": d["n_padded"]} if "n_padded" in d else {}
+                out[b] = MatrixResult(name, m, n, d["L"].shape[1], quant_params.Q_bits, d["codes"], d["Q_scale"],
+                                      d["L"], d["R"], d["global_scale"], d["errors"], extra)
         return out
 
     def run_all(batches):
@@ -261,12 +260,11 @@ def engine_decompose_batch(quant_params, device, H_of=None):
         the host syncs: the one-CU-per-matrix p x p kernels of a small batch leave most of
         the 256 CUs to the other batches' GEMMs (config 4 share of one rank at 8 GPUs:
         0.43 s vs 0.78 s one batch after another, tools/bench_model.py)."""
-        Ws = [weights(b) for b in batches]
-        hs = [h_of(b) for b in batches]
-        engines = [CalderaEngine(EngineParams.from_caldera_params(quant_params)) for _ in batches]
-        run_interleaved([e.run_iter(W, None if h is None else h.to(device))
-                         for e, W, h in zip(engines, Ws, hs)], torch.device(device))
-        return [r for b, e in zip(batches, engines) for r in results(b, e)]
+        dev = torch.device(device)
+        groups = [_Group(quant_params, weights(b), h_of(b), dev, scale_W=True, use_tqdm=False, engine_kwargs=None,
+                         streams=1, w_to_host=False) for b in batches]
+        run_interleaved([gen for g in groups for _, _, gen in g.parts], dev)
+        return [r for b, g in zip(batches, groups) for r in results(b, g)]
 
     def run(batch_items):
         return run_all([batch_items])

@@ -609,6 +609,12 @@ class RankRSolver:
         used = []
         hist = []                               # per-matrix test values of the full iterations
         stalled = np.zeros(B, dtype=bool)
+        # matrices that passed the test (or stalled) are FROZEN until every matrix has: the
+        # filter passes their block through (active = 0) and the CholQR / Rayleigh-Ritz steps that
+        # still run batch-wide are undone for them by restoring the state they froze with.  A
+        # matrix's result then does not depend on how long its batch-mates take: it is the same
+        # in any batch of the same size (main.py's layers, each with its own Hessian, batched).
+        frz = None                              # (host mask, device index, X, Z, theta, ends, resid)
         n_outer = 0
         while n_outer < MAX_OUTER:
             d = degs[min(n_outer, len(degs) - 1)]
@@ -655,6 +661,16 @@ class RankRSolver:
                 chk = chk.cpu().numpy()
                 n_unconv = int(chk[-1])
                 chk = chk[:-1]
+                if frz is not None and Zn is not None:
+                    # restore the frozen matrices' block, products, values and test (batch-wide
+                    # CholQR / Rayleigh-Ritz rotated them; an overflow redo keeps them frozen too)
+                    fm, fi, fX, fZ, fth, fends, fres = frz
+                    Xn.index_copy_(0, fi, fX)
+                    Zn.index_copy_(0, fi, fZ)
+                    theta_n = theta_n.index_copy(0, fi, fth)
+                    chk[1:1 + B][fm] = fends[fm, 0]
+                    chk[1 + B:1 + 2 * B][fm] = fends[fm, 1]
+                    chk[1 + 2 * B:][fm] = fres[fm]
                 self.stats.jacobi_unconverged += n_unconv
                 if self.x3 and self._x3f and chk[0] != 0:
                     # an fp16 half overflowed (a Ritz value far below the true top of the
@@ -708,6 +724,14 @@ class RankRSolver:
             self._active.copy_(torch.from_numpy(live.astype(np.int32)))
             if not live.any():
                 break
+            if (~live).any() and (frz is None or (frz[0] != ~live).any()):
+                # the frozen set grew (or a refinement reopened it): snapshot the frozen rows
+                fm = ~live
+                fi = torch.from_numpy(np.nonzero(fm)[0]).to(dev)
+                frz = (fm, fi, X.index_select(0, fi), Z.index_select(0, fi), theta.index_select(0, fi),
+                       ends.copy(), resid.copy())
+            elif live.all():
+                frz = None
         if Z is None:  # left the loop on a values-only iteration (MAX_OUTER): rotate once
             theta, X, Z = yield from self._rr(X)
         self.stats.history.append((cold, used, list(self.stats.resid_hist)))

@@ -17,6 +17,10 @@
  *   - all matrices are row-major; "batch" = number of independent matrices of one shape,
  *     laid out at a fixed element stride (stride 0 = broadcast one operand).
  *   - pointers are device pointers unless the name ends in _host.
+ *   - column / error weight vectors (a diagonal Hessian's derived weights) carry a batch
+ *     stride (ABI 5): 0 = one vector shared by the batch, else matrix b reads its own vector
+ *     at w + b * stride -- a batch of layers with distinct diagonal Hessians (main.py:163-165
+ *     gives every layer its own Hall[name]) runs in one call.
  */
 #ifndef CALDERA_HIP_H
 #define CALDERA_HIP_H
@@ -28,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CQ_ABI_VERSION 4
+#define CQ_ABI_VERSION 5
 
 #define CQ_OK 0
 #define CQ_EINVAL (-1)   /* bad argument (shape, bits, null pointer) */
@@ -72,8 +76,8 @@ int cq_rms_scale(int dtype, const void* W, int64_t batch, int64_t numel, int do_
 size_t cq_quantize_workspace(int64_t batch, int64_t numel, int64_t block_size);
 int cq_quantize_uniform(const float* x, int64_t batch, int64_t numel, int64_t block_size,
                         int bits, float eps, void* codes, uint8_t* packed, float* deq,
-                        float* scale, const float* err_w, int64_t err_ncols, double* err_out,
-                        void* ws, size_t ws_bytes, void* stream);
+                        float* scale, const float* err_w, int64_t err_ncols, int64_t err_w_stride,
+                        double* err_out, void* ws, size_t ws_bytes, void* stream);
 
 /* Same quantiser when the whole-matrix absmax is already known (bits of |x|max as
  * uint32 in absmax_bits[b], e.g. produced by cq_gemm_f32 EPI_RESID).  Replaces
@@ -81,8 +85,8 @@ int cq_quantize_uniform(const float* x, int64_t batch, int64_t numel, int64_t bl
 int cq_quantize_uniform_known_max(const float* x, int64_t batch, int64_t numel, int bits,
                                   float eps, const uint32_t* absmax_bits, void* codes,
                                   uint8_t* packed, float* deq, float* scale,
-                                  const float* err_w, int64_t err_ncols, double* err_out,
-                                  void* ws, size_t ws_bytes, void* stream);
+                                  const float* err_w, int64_t err_ncols, int64_t err_w_stride,
+                                  double* err_out, void* ws, size_t ws_bytes, void* stream);
 
 /* Dequantise (quantization.py:103-105, :292-295): out[e] = (float(c_e)/k) * scale[e / block_size].
  * codes: int8 (bits <= 8) / int16 (bits 16), or offset-binary packed if `packed` (bits 2/4).
@@ -104,7 +108,7 @@ int cq_unpack_codes(const uint8_t* packed, int64_t batch, int64_t numel, int bit
 size_t cq_quantize_nf_workspace(int64_t batch, int64_t numel, int64_t block_size);
 int cq_quantize_nf(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, float eps,
                    uint8_t* idx, float* deq, float* scale, const float* err_w, int64_t err_ncols,
-                   double* err_out, void* ws, size_t ws_bytes, void* stream);
+                   int64_t err_w_stride, double* err_out, void* ws, size_t ws_bytes, void* stream);
 /* out[e] = level[idx[e]] * scale[e / block_size]  (quantization.py:87-91) */
 int cq_dequant_nf(const uint8_t* idx, const float* scale, int64_t total, int64_t block_size, int bits,
                   float* out, void* stream);
@@ -127,7 +131,8 @@ int cq_bbint_stats(const float* x, int64_t batch, int64_t numel, int64_t block_s
                    float* bmin, float* bscale, int64_t* n_outliers, void* ws, size_t ws_bytes, void* stream);
 int cq_bbint_emit(const float* x, int64_t batch, int64_t numel, int64_t block_size, int bits, const float* bmin,
                   const float* bscale, uint8_t* packed, float* deq, float* out_vals, int64_t* out_idx,
-                  const float* err_w, int64_t err_ncols, double* err_out, void* ws, size_t ws_bytes, void* stream);
+                  const float* err_w, int64_t err_ncols, int64_t err_w_stride, double* err_out, void* ws,
+                  size_t ws_bytes, void* stream);
 /* out = u * bscale[blk] + bmin[blk] from the packed codes, then out[row*bs + col] = value for
  * each of the n_outliers listed outliers. */
 int cq_dequant_bbint(const uint8_t* packed, int bits, const float* bmin, const float* bscale, int64_t total,
@@ -145,7 +150,7 @@ int cq_dequant_bbint(const uint8_t* packed, int bits, const float* bmin, const f
  * whose Q is not an affine function of one scale); `scale` is then unused.
  */
 int cq_build_residual(int dtype, const void* Ws, const uint8_t* packed, const float* scale,
-                      int bits, const float* ycol, int64_t batch, int64_t m, int64_t n,
+                      int bits, const float* ycol, int64_t ycol_stride, int64_t batch, int64_t m, int64_t n,
                       float* Y, float* res_out, void* stream);
 
 /* ---------------------------------------------------------------------------------
@@ -350,6 +355,8 @@ typedef struct cq_x3_args {
                                       solver's filter and Rayleigh-Ritz products hand their
                                       result back in the k x p layout without a transpose pass */
     int64_t stride_ct;
+    int64_t stride_colw;           /* colw batch stride (ABI 5; 0: one vector for every matrix,
+                                      N: per-matrix weights -- distinct diagonal Hessians) */
 } cq_x3_args;
 /* C = alpha * (A B^T) + beta * P + gamma * D, per batch coefficient vectors; K % 32 == 0. */
 int cq_gemm_x3(const cq_x3_args* a, void* stream);
@@ -368,6 +375,8 @@ int cq_absmax(int dtype, const void* X, int64_t n_per, int64_t batch, float* out
  * only the hi halves).  ycol_hi (optional, with hi/lo): the column-blocked halves are of
  * res * ycol_hi instead (the weighted Gram's W diag(ycol^2) operand), at the power of two for
  * (wmax[b] + Q_scale[b]) * ycol_hi_max, written to scale_hi_out[b]; everything else keeps ycol.
+ * Per-matrix weights (ABI 5): ycol / ycol_hi at + b * ycol_stride, and ycol_max_v[b] /
+ * ycol_hi_max_v[b] (when non-NULL) replace the scalar bounds.
  * m % 32 == 0, n % 64 == 0.
  * bits == 32: `packed` is a dense fp32 Q and qscale[b] a bound on max|Q[b]|. */
 size_t cq_residual_split_workspace(int64_t m, int64_t n, int64_t batch);
@@ -375,8 +384,9 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
                       const float* ycol, float ycol_max, const float* wmax, int64_t batch, int64_t m,
                       int64_t n, float* res_out, float* Y_out, uint16_t* hi, uint16_t* lo,
                       uint16_t* thi, uint16_t* tlo, float* scale_out, double* sq_out,
-                      const float* ycol_hi, float ycol_hi_max, float* scale_hi_out, void* ws,
-                      size_t ws_bytes, void* stream);
+                      const float* ycol_hi, float ycol_hi_max, float* scale_hi_out, int64_t ycol_stride,
+                      const float* ycol_max_v, const float* ycol_hi_max_v, void* ws, size_t ws_bytes,
+                      void* stream);
 
 /* Gram of the LR step's Y from sparse 2-bit codes (cq_sgram.hip).  Replaces, for m <= n,
  * Q_bits = 2 and a diagonal (or no) H, the Gram Y Y^T of Y = (W - Q) diag(ycol) that the SVD
@@ -409,15 +419,15 @@ int cq_residual_split(int dtype, const void* Ws, const uint8_t* packed, const fl
  * k % 64 == 0, L % 64 == 0. */
 int cq_sgram_count(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, int32_t* row_nnz,
                    int32_t* perm, int64_t* slice_off, int64_t* total, int64_t Lh, int32_t* row_nnz1,
-                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, double* corr_ws,
-                   double* corr_out, void* stream);
+                   int32_t* slice_w1, const void* W, const float* qscale, const float* wcol, int64_t wcol_stride,
+                   double* corr_ws, double* corr_out, void* stream);
 int cq_sgram_fill(const uint8_t* packed, int bits, int64_t batch, int64_t k, int64_t L, const int32_t* row_nnz,
                   const int32_t* perm, const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh,
                   int64_t stride_ell, uint32_t* ell, void* stream);
 int cq_sgram_rows(int64_t L);
 int64_t cq_sgram_split(int64_t k, int64_t L);
 int cq_sgram_spmm(int dtype, const void* W, const uint8_t* packed, const float* qscale, const float* wcol,
-                  int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
+                  int64_t wcol_stride, int64_t batch, int64_t k, int64_t L, const uint32_t* ell, const int32_t* perm,
                   const int64_t* slice_off, const int32_t* slice_w1, int64_t Lh, int64_t stride_ell, float* P,
                   void* stream);
 int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_t batch, int64_t k,
@@ -440,10 +450,12 @@ int cq_sgram_combine(const float* A, const float* P, const float* qscale, int64_
 int cq_codes_transpose(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, uint8_t* out,
                        void* stream);
 int cq_codes_matmul(const uint8_t* packed, int bits, int64_t batch, int64_t rows, int64_t cols, const float* X,
-                    int64_t ldx, int64_t stride_x, const float* colw, const float* roww, int64_t r, float* out,
-                    int64_t ldo, int64_t stride_out, int trans, void* stream);
+                    int64_t ldx, int64_t stride_x, const float* colw, int64_t colw_stride, const float* roww,
+                    int64_t roww_stride, int64_t r, float* out, int64_t ldo, int64_t stride_out, int trans,
+                    void* stream);
 int cq_codes_ysq_corr(const uint8_t* packed, int bits, const void* W, int dtype, const float* qscale,
-                      const float* colw, int64_t batch, int64_t rows, int64_t cols, double* out, void* stream);
+                      const float* colw, int64_t colw_stride, int64_t batch, int64_t rows, int64_t cols, double* out,
+                      void* stream);
 int cq_transpose_f16(const uint16_t* X, int64_t batch, int64_t rows, int64_t cols, uint16_t* Y, void* stream);
 
 /* Fused Q update.  Replaces alg.py:253-283 (maybe_update_Q / update_Q_non_data_aware:
@@ -477,14 +489,15 @@ int cq_q_update_list_geometry(int64_t m, int64_t n, int64_t r, int64_t* rows_out
 int cq_q_update_x3(int dtype, const void* W, int64_t m, int64_t n, int64_t r, int64_t batch,
                    const uint16_t* Lh, const uint16_t* Ll, const uint16_t* Rth, const uint16_t* Rtl,
                    const float* inv_scale, int bits, float eps, void* codes, uint8_t* packed,
-                   float* scale_out, const float* err_w, double* err_out, const float* absmax_in,
-                   const float* scale_hint, int* fallback_out, void* ws, size_t ws_bytes, void* stream);
+                   float* scale_out, const float* err_w, int64_t err_w_stride, double* err_out,
+                   const float* absmax_in, const float* scale_hint, int* fallback_out, void* ws,
+                   size_t ws_bytes, void* stream);
 
 /* Chebyshev 3-term recurrence support and elementwise helpers. */
 /* out[b] = sum(x[b]^2 * w[j % ncols]) fp64 (w may be NULL) — denominators of alg.py:298 */
 int cq_weighted_sqsum(int dtype, const void* x, int64_t batch, int64_t numel,
-                      const float* w, int64_t ncols, double* out, void* ws, size_t ws_bytes,
-                      void* stream);
+                      const float* w, int64_t ncols, int64_t w_stride, double* out, void* ws,
+                      size_t ws_bytes, void* stream);
 /* out[b] = sum_i x[b][i] * y[b][i], fp64 accumulation; dtype CQ_F32 | CQ_F64.  Workspace
  * as cq_weighted_sqsum (cq_rms_scale_workspace(batch, numel)).  Replaces the separate
  * m x n x r error GEMM of the LPLR loop (alg.py:182): with Y R^T and the r x r Grams

@@ -21,8 +21,13 @@ the number of final-code flips between the two runs).  Config 5 (the chaotic 4-b
 path, where two identical reference calls diverge in Q + L R) records the flips of the final
 codes between two more reference runs of the same W (none: the kept iterate's Q is stable).
 
-Usage:  python tests/golden/gen_golden_codes.py [cfg2seeds] [cfg3] [cfg4t] [main] [cfg5]
-Output: tests/golden/final_codes.npz, tests/golden/ref_spread_cfg2_seeds16.json
+Held-out set (round 6): config 2 seeds 16-47 -- matrices the engine's solver schedules and
+tolerances were never tuned on -- recorded the same way (final codes, near-ties, sketch, errors,
+4- vs 8-thread spread) into separate files, so parity measured on them is out-of-sample.
+
+Usage:  python tests/golden/gen_golden_codes.py [cfg2seeds] [cfg3] [cfg4t] [main] [cfg5] [cfg2holdout]
+Output: tests/golden/final_codes.npz, tests/golden/ref_spread_cfg2_seeds16.json,
+        (cfg2holdout) tests/golden/final_codes_holdout.npz, tests/golden/ref_spread_cfg2_holdout.json
 """
 import hashlib
 import json
@@ -40,6 +45,9 @@ import gen_golden as G  # noqa: E402
 
 OUT = os.path.join(HERE, "final_codes.npz")
 SPREAD = os.path.join(HERE, "ref_spread_cfg2_seeds16.json")
+OUT_HOLDOUT = os.path.join(HERE, "final_codes_holdout.npz")
+SPREAD_HOLDOUT = os.path.join(HERE, "ref_spread_cfg2_holdout.json")
+HOLDOUT_SEEDS = range(16, 48)
 TIE_TOL = 1e-3
 CFG2 = dict(Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5)
 
@@ -94,7 +102,7 @@ def sketch(d, n):
     return ((d.Q.double() + d.L.double() @ d.R.double()).numpy() @ G.sketch_omega(n)).astype(np.float32)
 
 
-def gen_cfg2_seeds(alg, CP, o, seeds=range(16)):
+def gen_cfg2_seeds(alg, CP, o, seeds=range(16), spread_path=SPREAD, out_path=OUT):
     large = np.load(os.path.join(HERE, "sum_large.npz"))
     spread = {"generated_by": "tests/golden/gen_golden_codes.py cfg2seeds (unmodified reference, CPU, "
                               "4 vs 8 torch threads)", "tie_tol_code_units": TIE_TOL, "seeds": {}}
@@ -126,8 +134,8 @@ def gen_cfg2_seeds(alg, CP, o, seeds=range(16)):
             "errors_ref8": d.errors, "errors_ref4": d4.errors, "seconds_8": el, "seconds_4": el4}
         print(f"{tag}: ref4 vs ref8 {spread['seeds'][str(s)]['rel_frob_QLR_ref4_vs_ref8']:.2e}, "
               f"{flips.size} code flips ({at_ties} at near-ties)", flush=True)
-        json.dump(spread, open(SPREAD, "w"), indent=1)
-        np.savez_compressed(OUT, **o)
+        json.dump(spread, open(spread_path, "w"), indent=1)
+        np.savez_compressed(out_path, **o)
     torch.set_num_threads(8)
 
 
@@ -189,5 +197,8 @@ if __name__ == "__main__":
             if w in what:
                 f(alg, CP, o)
                 np.savez_compressed(OUT, **o)
+        if "cfg2holdout" in what:
+            oh = dict(np.load(OUT_HOLDOUT)) if os.path.exists(OUT_HOLDOUT) else {}
+            gen_cfg2_seeds(alg, CP, oh, seeds=HOLDOUT_SEEDS, spread_path=SPREAD_HOLDOUT, out_path=OUT_HOLDOUT)
     finally:
         os.chdir(cwd)

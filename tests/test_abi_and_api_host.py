@@ -27,8 +27,29 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(K.EXPORTS), set(names) ^ set(K.EXPORTS)
-    assert lib.cq_abi_version() == 4
+    assert lib.cq_abi_version() == K.ABI_VERSION == 5
     assert isinstance(lib.cq_last_error(), bytes)
+
+
+def header_param_counts():
+    """{function: number of parameters} of every prototype in include/caldera_hip.h."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(cq_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes declaration in _lib.py passes as many arguments as the header's prototype
+    takes (ABI 5 added weight batch strides to twelve entries: a missed one would shift every
+    later argument)."""
+    import ee274_convexcaldera_llm_quantization_amd._lib as K
+    counts = header_param_counts()
+    assert set(counts) == set(K.EXPORTS)
+    for name, (_, args) in K._SIGS.items():
+        assert len(args) == counts[name], (name, len(args), counts[name])
 
 
 def _struct_fields(name):
