@@ -38,6 +38,7 @@ diagonal Hessian, batched with per-matrix Hessians, beside the reference's one-c
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -185,6 +186,7 @@ def cpu_baseline(name, wl, dec0):
     el = time.perf_counter() - t0
     per = el * wl["iters"] / iters
     cpu = {"value": 1.0 / per, "unit": "matrices/s", "cores": torch.get_num_threads(), "kind": "port",
+           "host": host_cpu_info(),
            "sample": (f"seed-0 {wl['m']}x{wl['n']} matrix, {iters} of {wl['iters']} outer iterations of the "
                       f"reference's torch-CPU op sequence (torch.linalg svd/lstsq on MKL, fp32), {el:.1f} s on "
                       f"{torch.get_num_threads()} host threads" + ("" if iters == wl["iters"] else
@@ -195,6 +197,28 @@ def cpu_baseline(name, wl, dec0):
         got = (dec0["Q"].double() + dec0["L"].double() @ dec0["R"].double()).cpu()
         par["frob_err_vs_cpu_baseline"] = float(torch.linalg.norm(got - exp) / torch.linalg.norm(exp))
     return cpu, par
+
+
+def host_cpu_info():
+    """the CPU model (/proc/cpuinfo 'model name', as lscpu reports it), the
+    host's logical CPUs, and torch's BLAS/LAPACK build (the MKL line of torch.__config__.show())
+    the CPU baseline runs on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cfg = torch.__config__.show()
+    mkl = next((ln.strip(" -") for ln in cfg.splitlines() if "Math Kernel Library" in ln), None)
+    cap = next((ln.strip(" -") for ln in cfg.splitlines() if "CPU capability" in ln), None)
+    blas = re.findall(r"\b(BLAS_INFO=[^,]*|LAPACK_INFO=[^,]*)", cfg)
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "torch_threads": torch.get_num_threads(),
+            "torch": torch.__version__, "mkl": mkl, "cpu_capability": cap, "blas_lapack": blas,
+            "mkl_available": bool(torch.backends.mkl.is_available())}
 
 
 def single_call_latency(qp, W0, h, dev, calls=3):

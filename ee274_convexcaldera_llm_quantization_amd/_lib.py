@@ -178,16 +178,21 @@ def load(path: str = LIB_PATH):
             raise RuntimeError(f"{path} is stale (built from other sources than csrc/ now holds, or "
                                f"unstamped): rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
-    other = path != LIB_PATH  # another build (A/B timing of a kernel change, tools/probes/build_rev.sh)
+    # any build (also another one for an A/B timing, tools/probes/build_rev.sh) must speak this
+    # ABI: the declarations below are this ABI's signatures, and calling an export of another
+    # layout through them is undefined behaviour on the GPU rather than a clean error
+    abi = getattr(lib, "cq_abi_version", None)
+    if abi is None:
+        raise RuntimeError(f"{path} does not export cq_abi_version")
+    abi.restype, abi.argtypes = c_int, []
+    if abi() != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {abi()} != {ABI_VERSION} (include/caldera_hip.h); rebuild it "
+                           f"from these sources")
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name, None)
-        if fn is None and other:
-            continue  # an older build: only the exports both know are declared
         if fn is None:
             raise RuntimeError(f"{path} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.cq_abi_version() != ABI_VERSION and not other:
-        raise RuntimeError("libcaldera_hip.so ABI version mismatch")
     _lib = lib
     return lib
 

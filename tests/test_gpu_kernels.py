@@ -506,13 +506,17 @@ def test_gemm_x3_matches_fp64(K, M, N, Kd):
     assert err < max(3 * err32, 1e-6), (err, err32)
 
 
-@pytest.mark.parametrize("M,N,Kd,blocked", [(256, 1024, 4096, True), (512, 256, 256, False), (256, 4096, 128, False)])
+@pytest.mark.parametrize("M,N,Kd,blocked", [(256, 1024, 4096, True), (256, 1024, 512, True), (512, 256, 256, False),
+                                            (256, 4096, 128, False)])
 def test_gemm_x3_square_tile_bit_identical(K, M, N, Kd, blocked):
     """The 256 x 256 tile (gemm_x3s_kernel: rank-256 products, config 5's LPLR loop and normal
     equations) against the 192 x 384 kernel on the same operands: an N a multiple of 384 but
     not of 256 (N + 128) keeps the 192 x 384 tiling, whose first N columns must be the same
     bits (same fragments, MFMA order per 16 x 16 block and epilogue roundings); and fp32-grade
-    against fp64."""
+    against fp64.  ksplit = 1 on both calls: the square kernel only runs one-pass products (a
+    small batch's long-K products would otherwise take split-K on both sides and compare split-K
+    with split-K), so the blocked long-K cases pin gemm_x3s_kernel itself -- the production path
+    of config 5's LPLR products under interleaving (overlap.py turns split-K off)."""
     Bt = 2
     g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
     A = torch.randn(Bt, M, Kd, device=DEV, generator=g) * 0.1
@@ -522,14 +526,14 @@ def test_gemm_x3_square_tile_bit_identical(K, M, N, Kd, blocked):
     Bh, Bl = K.split_f16(Bm.contiguous(), 2.0 ** 10, blocked=blocked)
     inv = torch.full((Bt,), 2.0 ** -16, device=DEV)
     C_wide = torch.full((Bt, M, N + 128), float("nan"), device=DEV)
-    K.gemm_x3(Ah, Al, Bh, Bl, inv, C_wide, a_blocked=blocked, b_blocked=blocked)
+    K.gemm_x3(Ah, Al, Bh, Bl, inv, C_wide, a_blocked=blocked, b_blocked=blocked, ksplit=1)
     if blocked:   # the first N rows of B in the K-blocked layout [K/32][rows][32]
         Bh_n = Bh.view(Bt, Kd // 32, N + 128, 32)[:, :, :N].contiguous().view(Bt, N, Kd)
         Bl_n = Bl.view(Bt, Kd // 32, N + 128, 32)[:, :, :N].contiguous().view(Bt, N, Kd)
     else:
         Bh_n, Bl_n = Bh[:, :N].contiguous(), Bl[:, :N].contiguous()
     C = torch.full((Bt, M, N), float("nan"), device=DEV)
-    K.gemm_x3(Ah, Al, Bh_n, Bl_n, inv, C, a_blocked=blocked, b_blocked=blocked)
+    K.gemm_x3(Ah, Al, Bh_n, Bl_n, inv, C, a_blocked=blocked, b_blocked=blocked, ksplit=1)
     assert torch.equal(C, C_wide[:, :, :N])
     ref = torch.matmul(A.double(), Bm[:, :N].double().transpose(1, 2))
     err = ((C.double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
@@ -1196,3 +1200,30 @@ def test_gemm_x3_transposed_output(K, Bt, M, N, Kd, ks):
     Ct = torch.empty((Bt, N, M), device=DEV)
     K.gemm_x3(Ah, Al, Bh, Bl, inv, C, a_blocked=True, b_blocked=bb, Ct=Ct, ksplit=1)
     assert torch.equal(Ct, C.transpose(1, 2))
+
+
+@pytest.mark.parametrize("M,N,Kd,Bt,ksplit", [(192, 768, 256, 2, 1),      # 192 x 384 one-pass kernel
+                                               (192, 768, 4096, 2, 8),     # split-K epilogue
+                                               (256, 1024, 512, 2, 1),     # 256 x 256 square tile
+                                               (100, 1000, 64, 3, 1)])     # ragged tiles
+def test_absmax_out_gives_pow2_scale_of_C(K, M, N, Kd, Bt, ksplit):
+    """gemm_x3's absmax_out epilogue (the LPLR split scales rely on it, engine.lplr_rhs and
+    lplr_R_step): pow2_from_absmax(absmax_out) equals pow2_scale(C) bit for bit on the plain,
+    split-K and 256 x 256 paths; and a quantiser's scale taken as the bound (the r_bound /
+    l_bound shortcut) equals pow2_scale of its dequantised output, whose max |.| it attains."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + Kd)
+    A = torch.randn(Bt, M, Kd, device=DEV, generator=g) * torch.tensor([1e-3, 1.0, 37.0][:Bt], device=DEV).view(Bt, 1, 1)
+    Bm = torch.randn(Bt, N, Kd, device=DEV, generator=g)
+    sA = K.pow2_scale(A.contiguous(), 14)
+    sB = K.pow2_scale(Bm.contiguous(), 14)
+    Ah, Al = K.split_f16(A.contiguous(), sA)
+    Bh, Bl = K.split_f16(Bm.contiguous(), sB)
+    C = torch.empty(Bt, M, N, device=DEV)
+    amx = torch.empty(Bt, dtype=torch.int32, device=DEV)
+    K.gemm_x3(Ah, Al, Bh, Bl, 1.0 / (sA * sB), C, absmax_out=amx, ksplit=ksplit)
+    assert torch.equal(K.pow2_from_absmax(amx), K.pow2_scale(C, 14))
+    # quantiser scale as the bound of its own dequantised output (uniform, whole matrix)
+    for bits in (2, 4):
+        q = K.quantize_uniform(C.view(Bt, -1).contiguous(), M * N, bits, codes=True, deq=True)
+        assert torch.equal(K.pow2_from_absmax(q["scale"].view(Bt).clone()),
+                           K.pow2_scale(q["deq"].view(Bt, M, N).contiguous(), 14))
