@@ -71,6 +71,7 @@ WORKLOADS = {
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 PEAK_F16_MFMA_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense fp16/bf16 MFMA)
 PEAK_HBM_GBS = 8000.0
+XGMI_LINK_GBS = 153.0  # one xGMI link, MI355X (SURVEY.md "Comm note for MI355X": 7 links x ~153 GB/s per GPU)
 
 
 def golden():
@@ -308,28 +309,48 @@ def run_model(args):
     max_batch = args.model_batch or (16 if world >= 8 else 64)
     group = args.model_group or (4 if max_batch <= 16 else 2)
 
-    def split_parts(grp, nparts):
-        """each same-shape batch of the group as nparts interleaved parts (engines in batch order)"""
-        out = []
-        for b in grp:
-            k = max(1, min(nparts, len(b)))
-            out += [b[len(b) * i // k:len(b) * (i + 1) // k] for i in range(k)]
-        return out
+    def make_run_all(grp_size):
+        def run_all(batches, on_batch_done=None):
+            """groups of grp_size same-shape batches interleaved on HIP streams, one group after
+            another; on_batch_done(j, results) as batch j's last part finishes (the overlapped
+            gather issues batch j's transfer then, sharding.decompose_sharded)"""
+            res = []
+            for g0 in range(0, len(batches), grp_size):
+                gb = batches[g0:g0 + grp_size]
+                parts, owner = [], []
+                for j, b in enumerate(gb):
+                    k = max(1, min(args.model_parts, len(b)))
+                    for i in range(k):
+                        parts.append(b[len(b) * i // k:len(b) * (i + 1) // k])
+                        owner.append(g0 + j)
+                engines = [CalderaEngine(ep) for _ in parts]
+                left = {}
+                for o in owner:
+                    left[o] = left.get(o, 0) + 1
 
-    def run_all(batches):
-        res = []
-        for g0 in range(0, len(batches), group):
-            grp = split_parts(batches[g0:g0 + group], args.model_parts)
-            engines = [CalderaEngine(ep) for _ in grp]
-            run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)], dev)
-            res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"], d["R"],
-                                   d["global_scale"], d["errors"])
-                    for b, e in zip(grp, engines) for (name, m, n, _), d in zip(b, e.last_packed)]
-        return res
+                def results_of(j):
+                    return [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"],
+                                           d["R"], d["global_scale"], d["errors"])
+                            for b, e, o in zip(parts, engines, owner) if o == j
+                            for (name, m, n, _), d in zip(b, e.last_packed)]
+
+                def part_done(i, _):
+                    left[owner[i]] -= 1
+                    if left[owner[i]] == 0 and on_batch_done is not None:
+                        on_batch_done(owner[i], results_of(owner[i]))
+
+                run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, parts)],
+                                dev, on_done=part_done)
+                res += [r for j in range(g0, g0 + len(gb)) for r in results_of(j)]
+            return res
+        return run_all
+
+    run_all = make_run_all(group)
 
     def decompose(batch_items):
         return run_all([batch_items])
     decompose.run_all = run_all
+    decompose.blob_bound = lambda m, n: S.blob_bound(m, n, qp.Q_bits, qp.rank)
 
     def step():
         return S.decompose_sharded(items, decompose, rank=rank, world=world, max_batch=max_batch, device=dev)
@@ -345,42 +366,67 @@ def run_model(args):
         mb_e = args.model_batch or (16 if W_ >= 8 else 64)
         grp_e = args.model_group or (4 if mb_e <= 16 else 2)
 
-        def run_all_e(batches):
-            res = []
-            for g0 in range(0, len(batches), grp_e):
-                grp = split_parts(batches[g0:g0 + grp_e], args.model_parts)
-                engines = [CalderaEngine(ep) for _ in grp]
-                run_interleaved([e.run_iter(torch.stack([Wd[it[0]] for it in b])) for e, b in zip(engines, grp)],
-                                dev)
-                res += [S.MatrixResult(name, m, n, d["L"].shape[1], qp.Q_bits, d["codes"], d["Q_scale"], d["L"],
-                                       d["R"], d["global_scale"], d["errors"])
-                        for b, e in zip(grp, engines) for (name, m, n, _), d in zip(b, e.last_packed)]
-            return res
+        run_all_e = make_run_all(grp_e)
 
         def dec_e(batch_items):
             return run_all_e([batch_items])
         dec_e.run_all = run_all_e
         ranks = [args.emulate_rank] if args.emulate_rank is not None else list(range(W_))
-        share_t = {}
+        share_t, tails = {}, {}
         for r_ in ranks:
-            def share_step():
-                res = S.decompose_sharded(items, dec_e, rank=r_, world=W_, max_batch=mb_e, gather=False, device=dev)
-                return S.pack_results(res, device=dev)  # what the rank hands to the gather
+            events = []
+
+            def share_step(rec=None):
+                t0 = time.perf_counter()
+
+                def done(j, res_j):  # batch j of this share finished: its transfer could start now
+                    if rec is not None:
+                        rec.append((time.perf_counter() - t0, sum(r.codes.numel() * r.codes.element_size()
+                                                                  + 4 * r.L.numel() + 4 * r.R.numel() for r in res_j)))
+                S.decompose_sharded(items, dec_e, rank=r_, world=W_, max_batch=mb_e, gather=False, device=dev,
+                                    on_batch_done=done)
             for _ in range(max(1, args.warmup)):
                 share_step()
             torch.cuda.synchronize()
-            ts = []
+            ts, recs = [], []
             for _ in range(args.steps):
+                rec = []
                 t0 = time.perf_counter()
-                share_step()
+                share_step(rec)
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
-            share_t[r_] = sorted(ts)[len(ts) // 2]
+                recs.append(rec)
+            k = sorted(range(len(ts)), key=lambda i: ts[i])[len(ts) // 2]
+            share_t[r_] = ts[k]
+            tails[r_] = recs[k]
+        # the overlapped gather (sharding.decompose_sharded): batch j's packed arrays leave as it
+        # finishes; a rank's transfers queue on its own xGMI link to rank 0 (fully connected, 7 x
+        # ~153 GB/s per GPU: SURVEY.md "Comm note for MI355X"), so only what is still in flight when
+        # the share's compute ends is exposed.  Rank 0's own share is local (no link)
+        link = XGMI_LINK_GBS * 1e9
+
+        def exposed(rec, t_end):
+            busy = 0.0
+            for t, nb in sorted(rec):
+                busy = max(busy, t) + nb / link
+            return max(0.0, busy - t_end)
+
+        exp_s = {r_: (0.0 if r_ == 0 else exposed(tails[r_], share_t[r_])) for r_ in ranks}
+        nov_s = {r_: (0.0 if r_ == 0 else sum(nb for _, nb in tails[r_]) / link) for r_ in ranks}
+        # worst case: rank 0's ingress serialised onto one link, every peer's batches in one queue
+        allrec = [(t, nb) for r_ in ranks if r_ != 0 for t, nb in tails[r_]]
+        ser = exposed(allrec, max(share_t.values())) if allrec else 0.0
         emu = {"world": W_, "ranks_timed": ranks, "max_batch": mb_e, "interleaved_batches": grp_e,
                "matrices_per_share": len(S.shard_indices(len(items), W_, ranks[0])),
                "share_s": {str(k): v for k, v in share_t.items()}, "max_share_s": max(share_t.values()),
-               "note": "rank r's round-robin share decomposed + packed on one GPU (median of --steps); "
-                       "excludes the RCCL transfer to rank 0"}
+               "gather_model": {"xgmi_link_gbs": XGMI_LINK_GBS,
+                                "source": "SURVEY.md comm note: 8 GPUs fully connected, 7 links x ~153 GB/s per GPU",
+                                "share_payload_bytes": {str(k): int(sum(nb for _, nb in v)) for k, v in tails.items()},
+                                "exposed_overlapped_s": {str(k): v for k, v in exp_s.items()},
+                                "exposed_unoverlapped_s": {str(k): v for k, v in nov_s.items()},
+                                "exposed_serialised_ingress_s": ser},
+               "note": "rank r's round-robin share decomposed on one GPU (median of --steps); the gather's exposed "
+                       "tail is modelled from each batch's measured finish time and packed bytes"}
 
     for _ in range(args.warmup):
         step()
@@ -417,10 +463,21 @@ def run_model(args):
                        "parallelism": f"dp{world} (matrix-sharded)"},
             "gathered_bytes": int(sum(r.codes.numel() * r.codes.element_size() + r.L.numel() * 4 + r.R.numel() * 4
                                       for r in out)),
+            "gather": dict(S.LAST_GATHER),
         }
         if emu is not None:
-            emu["t_model_1gpu_s"] = el / args.steps
-            emu[f"projected_speedup_{emu['world']}"] = emu["t_model_1gpu_s"] / emu["max_share_s"]
+            t1 = el / args.steps
+            emu["t_model_1gpu_s"] = t1
+            W_ = emu["world"]
+            sh = {int(k): v for k, v in emu["share_s"].items()}
+            gm = emu["gather_model"]
+            emu[f"projected_speedup_{W_}"] = t1 / emu["max_share_s"]
+            emu[f"projected_speedup_{W_}_incl_gather"] = t1 / max(
+                sh[r_] + gm["exposed_overlapped_s"][str(r_)] for r_ in sh)
+            emu[f"projected_speedup_{W_}_incl_gather_unoverlapped"] = t1 / max(
+                sh[r_] + gm["exposed_unoverlapped_s"][str(r_)] for r_ in sh)
+            emu[f"projected_speedup_{W_}_incl_gather_serialised_ingress"] = t1 / (emu["max_share_s"]
+                                                                               + gm["exposed_serialised_ingress_s"])
             result["strong_scaling_projection"] = emu
         if not args.no_parity:
             result["parity_pinned"] = model_parity(out, dev)
@@ -729,7 +786,7 @@ def main():
     if os.environ.get("CQ_BENCH_VERBOSE"):
         print(f"warmup done; reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     # time the dominant kernel (the G X filter GEMMs) with HIP events on its stream
-    solver.EVENT_PROBE.enable(True)
+    solver.EVENT_PROBE.enable(True, max_pairs=400)
     solver.QUANT_PROBE.enable(True, max_pairs=8 * args.steps * parts)
     solver.LPLR_PROBE.enable(wl["L_bits"] < 16, max_pairs=64)
     solver.GRAM_PROBE.enable(True, max_pairs=16 * args.steps * parts)
@@ -811,8 +868,37 @@ def main():
                      "matrices_per_launch": launch_batch})
         return roof
 
-    if probe["count"]:
-        result["roofline"] = roofline_of(probe, B // parts)
+    def probe_of(summ, key):
+        """the summary restricted to one probed kernel (the split-fp16 filter step <0> is the
+        headline kernel; <1> the single-product steps)"""
+        for kn, g in summ.get("kernels", {}).items():
+            if kn.startswith(key):
+                return {"count": g["count"], "avg_ms": g["avg_ms"], "flops_per_launch": g["flops_per_launch"],
+                        "bytes_per_launch": g["bytes_per_launch"], "kernel": kn}
+        return None
+
+    p0 = probe_of(probe, "gemm_x3v_kernel<0>") if probe["count"] else None
+    if p0 is None and probe["count"]:
+        p0 = probe
+    if p0 is not None:
+        result["roofline"] = roofline_of(p0, B // parts)
+        p1 = probe_of(probe, "gemm_x3v_kernel<1>")
+        if p1 is not None:
+            r1 = roofline_of(p1, B // parts)
+            result["roofline_single_product"] = {k: r1[k] for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                                   "kernel", "launches_timed", "avg_launch_ms",
+                                                                   "bytes_per_launch")}
+        ag = probe.get("aggregate")
+        if ag and ag["busy_ms"] > 0:
+            gbs = ag["bytes"] / (ag["busy_ms"] * 1e-3) / 1e9
+            result["roofline_aggregate"] = {
+                "bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                "launches": ag["launches"], "bytes": ag["bytes"], "busy_ms": ag["busy_ms"],
+                "window_ms": ag["window_ms"],
+                "note": (f"all probed filter launches (split <0> and single-product <1>) of the {parts} interleaved "
+                         "parts' streams: their algorithmic bytes over the UNION of their launch windows (one clock "
+                         "for all streams) -- the chip-level filter rate while the parts share it; the per-launch "
+                         "frac above is one launch's rate under that sharing")}
         if parts > 1:
             result["roofline"]["concurrency"] = (
                 f"{parts} interleaved batch parts on separate HIP streams: each launch shares the chip with the "
@@ -941,15 +1027,27 @@ def main():
         from ee274_convexcaldera_llm_quantization_amd import scratch
         scratch.release()
         torch.cuda.empty_cache()
-        solver.EVENT_PROBE.enable(True)
+        solver.EVENT_PROBE.enable(True, max_pairs=400)
+        solver.QUANT_PROBE.enable(True, max_pairs=16)
         step(1)
         torch.cuda.synchronize()
         solver.EVENT_PROBE.enable(False)
         psolo = solver.EVENT_PROBE.summary()
+        qsolo = solver.QUANT_PROBE.summary()
+        solver.QUANT_PROBE.enable(False)
         if psolo["count"]:
-            result["roofline_solo"] = roofline_of(psolo, B)
+            result["roofline_solo"] = roofline_of(probe_of(psolo, "gemm_x3v_kernel<0>") or psolo, B)
             result["roofline_solo"]["note"] = ("one untimed step of the same batch as one part (no concurrent "
                                                "kernels): the kernel's own efficiency")
+            p1 = probe_of(psolo, "gemm_x3v_kernel<1>")
+            if p1 is not None:
+                result["roofline_solo"]["single_product_frac"] = roofline_of(p1, B)["frac"]
+        for kind, g in qsolo.items():
+            gbs = g["bytes_per_launch"] / (g["avg_ms"] * 1e-3) / 1e9
+            result.setdefault("roofline_quantise_solo", {})["first_Q" if kind == "w" else "Q_with_LR"] = {
+                "achieved_gbs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS, "avg_call_ms": g["avg_ms"],
+                "launches_timed": g["count"], "bytes_per_call": g["bytes_per_launch"],
+                "note": "the same untimed one-part step: the quantise kernel without a concurrent stream"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

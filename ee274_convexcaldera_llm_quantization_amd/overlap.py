@@ -54,9 +54,11 @@ def _part_streams(device, n):
     return lst[:n]
 
 
-def run_interleaved(gens, device, ready_first: bool = True):
+def run_interleaved(gens, device, ready_first: bool = True, on_done=None):
     """Drive generators, each on its own stream of `device` (a fixed per-device set).
     Returns the list of their return values.  The caller's stream is joined before and after.
+    on_done(i, value): called as generator i finishes, with its stream current (e.g. to start
+    the gather of that batch's results while the others still run).
 
     ready_first (default): a generator that yielded (it is about to read results back) gets an
     event recorded behind the work it queued, and the host next resumes a generator whose
@@ -65,7 +67,10 @@ def run_interleaved(gens, device, ready_first: bool = True):
     event has completed does it wait (spinning on the events).  False: plain round-robin,
     each resume blocking on that generator's own stream."""
     if len(gens) == 1:
-        return [run_to_end(gens[0])]
+        v = run_to_end(gens[0])
+        if on_done is not None:
+            on_done(0, v)
+        return [v]
     # concurrent batches fill the chip together: a small batch's split-fp16 products need no
     # split-K here (its partial sums and epilogue launches only add traffic: config-4 rank
     # share 0.159 -> 0.136 s, profiles/r05f_share*.log).  The policy is this thread's only
@@ -73,10 +78,10 @@ def run_interleaved(gens, device, ready_first: bool = True):
     # split into parts (default_parts: from 16 matrices on), not on other threads' calls.
     from . import _lib
     with _lib.split_k_policy(False):
-        return _run_interleaved(gens, device, ready_first)
+        return _run_interleaved(gens, device, ready_first, on_done)
 
 
-def _run_interleaved(gens, device, ready_first):
+def _run_interleaved(gens, device, ready_first, on_done=None):
     caller = torch.cuda.current_stream(device)
     streams = _part_streams(device, len(gens))
     for s in streams:
@@ -93,6 +98,8 @@ def _run_interleaved(gens, device, ready_first):
                     except StopIteration as stop:
                         out[i] = stop.value
                         live.remove(i)
+                        if on_done is not None:
+                            on_done(i, stop.value)
         else:
             events = [torch.cuda.Event() for _ in gens]
             pending = [False] * len(gens)  # yielded, event recorded, not yet resumed
@@ -123,6 +130,8 @@ def _run_interleaved(gens, device, ready_first):
                 except StopIteration as stop:
                     out[i] = stop.value
                     live.remove(i)
+                    if on_done is not None:
+                        on_done(i, stop.value)
                 nxt = (i + 1) % len(gens)
     finally:
         torch.cuda.set_stream(caller)

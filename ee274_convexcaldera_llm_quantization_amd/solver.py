@@ -48,13 +48,21 @@ class _EventProbe:
     """HIP-event timing of the dominant kernel (the G X filter GEMM) on the stream it is
     launched on; used by bench.py inside its timed region (roofline.achieved).  The event
     pairs are created up front (hipEventCreate per launch costs more than the launch) and
-    the first `max_pairs` filter launches of the timed region are sampled."""
+    the first `max_pairs` filter launches of the timed region are sampled.
+
+    Launches of several kernels may be probed (the split-fp16 and the single-product filter
+    steps): summary() reports the kernel with the most probed time at the top level, per-kernel
+    groups under "kernels", and "aggregate" -- the algorithmic bytes of every probed launch on
+    every stream divided by the union of their [start, end] windows (a reference event recorded
+    at enable() puts all streams on one clock): the chip-level rate of interleaved parts, where
+    a per-launch rate only says how fast one launch ran while sharing the chip."""
 
     def __init__(self):
         self.on = False
         self.pool = []
         self.used = 0
-        self.flops = 0
+        self.meta = []
+        self.ref = None
 
     def enable(self, on: bool, max_pairs: int = 96):
         self.on = on
@@ -62,6 +70,9 @@ class _EventProbe:
             self.pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                          for _ in range(max_pairs)]
             self.used = 0
+            self.meta = []
+            self.ref = torch.cuda.Event(enable_timing=True)
+            self.ref.record()
 
     def start(self, flops, nbytes=0.0, kernel=""):
         if not self.on or self.used >= len(self.pool):
@@ -69,7 +80,7 @@ class _EventProbe:
         ev = self.pool[self.used]
         self.used += 1
         ev[0].record()
-        self.flops, self.nbytes, self.kernel = flops, nbytes, kernel
+        self.meta.append((flops, nbytes, kernel))
         return ev
 
     def stop(self, ev):
@@ -80,9 +91,33 @@ class _EventProbe:
         if not self.used:
             return {"count": 0}
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b in self.pool[: self.used]]
-        return {"count": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": self.flops,
-                "bytes_per_launch": self.nbytes, "kernel": self.kernel}
+        pairs = self.pool[: self.used]
+        ms = [a.elapsed_time(b) for a, b in pairs]
+        groups = {}
+        for t, (fl, nb, kn) in zip(ms, self.meta):
+            g = groups.setdefault(kn, {"count": 0, "ms": 0.0, "flops_per_launch": fl, "bytes_per_launch": nb})
+            g["count"] += 1
+            g["ms"] += t
+        for g in groups.values():
+            g["avg_ms"] = g["ms"] / g["count"]
+        top = max(groups, key=lambda k: groups[k]["ms"])
+        g = groups[top]
+        out = {"count": g["count"], "avg_ms": g["avg_ms"], "flops_per_launch": g["flops_per_launch"],
+               "bytes_per_launch": g["bytes_per_launch"], "kernel": top, "kernels": groups}
+        if self.ref is not None:
+            iv = sorted((self.ref.elapsed_time(a), self.ref.elapsed_time(b)) for a, b in pairs)
+            union, cur_s, cur_e = 0.0, None, None
+            for s0, e0 in iv:
+                if cur_e is None or s0 > cur_e:
+                    if cur_e is not None:
+                        union += cur_e - cur_s
+                    cur_s, cur_e = s0, e0
+                else:
+                    cur_e = max(cur_e, e0)
+            union += cur_e - cur_s
+            out["aggregate"] = {"launches": len(iv), "bytes": float(sum(nb for _, nb, _ in self.meta)),
+                                "busy_ms": union, "window_ms": iv[-1][1] - iv[0][0] if iv else 0.0}
+        return out
 
 
 EVENT_PROBE = _EventProbe()
@@ -455,9 +490,12 @@ class RankRSolver:
         # new out (fp32) + new halves out
         nb = float(self.B) * (4.0 * self.k * self.k + 20.0 * self.p * self.k)
         kn = "gemm_x3v_kernel<0> (split-fp16 G X, Chebyshev filter)"
-        # the probe (bench.py's roofline) times the split-fp16 steps only: a single-product
-        # step moves 2k^2 + 18pk bytes per matrix, not the 4k^2 + 20pk counted here
-        probe = EVENT_PROBE.start if not single else (lambda *a: None)
+        # the probe (bench.py's roofline) times both kinds of step, each with its own bytes: a
+        # single-product step moves G's hi half and one iterate half per matrix, 2k^2 + 18pk
+        if single:
+            nb = float(self.B) * (2.0 * self.k * self.k + 18.0 * self.p * self.k)
+            kn = "gemm_x3v_kernel<1> (single fp16 product G X, Chebyshev filter)"
+        probe = EVENT_PROBE.start
         # the last step also writes its result in X's own k x p layout (Ct): no transpose pass
         out = self._free(X)
         ct = out if TRANSPOSED_OUT else None

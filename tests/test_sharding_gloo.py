@@ -47,6 +47,75 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+class _RunAllStub:
+    """decompose_batch with the interface of the engine's (sharding.engine_decompose_batch):
+    run_all(batches, on_batch_done) -- batches finishing out of order, as interleaved HIP
+    streams let them -- and blob_bound(m, n), which enables the overlapped gather."""
+
+    def __call__(self, batch_items):
+        return _stub(batch_items)
+
+    def run_all(self, batches, on_batch_done=None):
+        res = [_stub(b) for b in batches]
+        for j in reversed(range(len(batches))):  # the last batch finishes first
+            if on_batch_done is not None:
+                on_batch_done(j, res[j])
+        return [r for b in res for r in b]
+
+    @staticmethod
+    def blob_bound(m, n):
+        return S.blob_bound(m, n, 2, 3)
+
+
+def _worker_overlapped(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        done = []
+        res = S.decompose_sharded(_items(), _RunAllStub(), rank=rank, world=world, max_batch=2,
+                                  on_batch_done=lambda j, r: done.append(j))
+        info = dict(S.LAST_GATHER)
+        if rank == 0:
+            q.put((rank, info, done, [(r.name, r.codes.numpy().copy(), r.L.numpy().copy(), r.R.numpy().copy(),
+                                       r.Q_scale, r.errors) for r in res]))
+        else:
+            q.put((rank, info, done, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gather_overlapped_world2_gloo():
+    """The overlapped gather (one asynchronous gather per batch, issued in batch order as soon
+    as the batch and every earlier one finished; metadata gathered at the end) delivers exactly
+    what the one-shot gather does, in item order, with batches finishing out of order and the
+    ranks holding different numbers of batches (35 matrices over 2 ranks)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_overlapped, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = sorted([q.get(timeout=90) for _ in range(2)], key=lambda o: o[0])
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    items = _items()
+    plans = [S._plan(items, 2, r, 2) for r in range(2)]
+    assert len(plans[0]) != len(plans[1])  # unequal rounds: the shorter rank sends empty rounds
+    for rank, info, done, _ in outs:
+        assert info["mode"] == "overlapped" and info["rounds"] == max(len(p) for p in plans), info
+        assert sorted(done) == list(range(len(plans[rank])))
+    assert outs[1][3] is None
+    got = outs[0][3]
+    assert [g[0] for g in got] == [it[0] for it in items]
+    ref = {r.name: r for r in _stub(items)}
+    for name, codes, L, R, qs, errs in got:
+        assert torch.equal(torch.from_numpy(codes), ref[name].codes) and torch.equal(torch.from_numpy(L), ref[name].L)
+        assert torch.equal(torch.from_numpy(R), ref[name].R) and qs == ref[name].Q_scale and errs == ref[name].errors
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -101,8 +170,9 @@ def test_gather_world2_gloo():
 
 
 def test_batches_group_by_hessian():
-    """Same-shape matrices of different layers carry different diagonal Hessians: a batch
-    (one engine run, one H) must never mix them (decompose_sharded h_key)."""
+    """h_key adds a grouping key (batches never mix its values); without it, same-shape
+    matrices of different layers -- different diagonal Hessians -- share batches (the engine
+    reads per-matrix weights, ABI 5)."""
     items = _items()
     seen = []
 
