@@ -97,6 +97,9 @@ def synth_W(wl, seed):
 
 
 PINNED = 16  # batch positions whose matrices the golden runs pin (seeds 0-15, host RNG)
+# config 2: positions 16-47 hold seeds 16-47 too -- the HELD-OUT goldens (tests/golden/
+# final_codes_holdout.npz, exact_codes_cfg2_holdout.npz), matrices no schedule was tuned on
+HOLDOUT = range(16, 48)
 
 
 def synth_batch(wl, B, seed0, dev, host=PINNED):
@@ -163,6 +166,9 @@ def parity_of_timed_step(name, decs, wl):
         out["final_codes_vs_exact_lr"] = {
             "matrices": len(vs), "bit_exact": sum(c["sha_equal"] for c in vs.values()),
             "differing": {k: c for k, c in vs.items() if not c["sha_equal"]}}
+    if name == "cfg2" and len(decs) >= HOLDOUT[-1] + 1 and os.path.exists(
+            os.path.join(ROOT, "tests", "golden", "final_codes_holdout.npz")):
+        out["holdout"] = holdout_parity(decs, wl)
     if name == "cfg2":  # the reference's own spread on the same matrices (4 vs 8 CPU threads)
         sp = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_spread_cfg2_seeds16.json")))["seeds"]
         out["reference_4_vs_8_threads"] = {f"seed{k}": v["rel_frob_QLR_ref4_vs_ref8"] for k, v in sp.items()}
@@ -170,6 +176,46 @@ def parity_of_timed_step(name, decs, wl):
         out["seeds_over_1e-4"] = {k: {"ours": v, "reference_spread": out["reference_4_vs_8_threads"].get(k)}
                                   for k, v in over.items()}
     return out
+
+
+def holdout_parity(decs, wl):
+    """Config 2's held-out seeds 16-47 (batch positions 16-47, host RNG): final codes against the
+    reference's runs and against an exact rank-r step, Q + L R against the reference's sketch, with
+    the reference's own 4- vs 8-thread spread.  No solver schedule or tolerance was chosen on these
+    matrices (tests/golden/gen_golden_codes.py cfg2holdout, gen_exact_codes.py holdout)."""
+    from final_codes import compare
+    gd = os.path.join(ROOT, "tests", "golden")
+    fx = np.load(os.path.join(gd, "final_codes_holdout.npz"), allow_pickle=False)
+    ex = np.load(os.path.join(gd, "exact_codes_cfg2_holdout.npz"), allow_pickle=False)
+    sp = json.load(open(os.path.join(gd, "ref_spread_cfg2_holdout.json")))["seeds"]
+    m, n = wl["m"], wl["n"]
+    per, vs_ref, vs_ex, over = {}, [], [], {}
+    for s in HOLDOUT:
+        tag = f"cfg2s{s}"
+        if f"{tag}_rowhash" not in fx.files or f"s{s}_rowhash" not in ex.files:
+            continue
+        d = decs[s]
+        c = compare(tag, d["Q_idxs"], m, n, fx=fx)
+        e = compare(f"s{s}", d["Q_idxs"], m, n, fx=ex)
+        sk = _sketch(d["Q"], d["L"], d["R"], n)
+        ref = fx[f"{tag}_sketch_QLR"].astype(np.float64)
+        rel = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
+        spr = sp.get(str(s), {})
+        per[f"seed{s}"] = {"rel_frob_QLR": rel, "ref_spread": spr.get("rel_frob_QLR_ref4_vs_ref8"),
+                           "codes_vs_ref": c, "codes_vs_exact_lr_bit_exact": e["sha_equal"]}
+        vs_ref.append(c)
+        vs_ex.append(e)
+        if rel > 1e-4:
+            over[f"seed{s}"] = {"ours": rel, "reference_spread": spr.get("rel_frob_QLR_ref4_vs_ref8")}
+    k = len(vs_ref)
+    return {"matrices": k,
+            "bit_exact_vs_reference": sum(c["sha_equal"] for c in vs_ref),
+            "bit_exact_vs_exact_lr": sum(c["sha_equal"] for c in vs_ex),
+            "reference_reproduces_itself": sum(1 for s in HOLDOUT if sp.get(str(s), {}).get(
+                "final_code_flips_ref4_vs_ref8", 1) == 0),
+            "rows_unexplained_vs_reference": sum(c["rows_unexplained"] for c in vs_ref),
+            "flips_at_near_ties_vs_reference": sum(c["flips"] for c in vs_ref),
+            "seeds_over_1e-4": over, "per_seed": per}
 
 
 def cpu_baseline(name, wl, dec0):
@@ -686,6 +732,9 @@ def main():
     ap.add_argument("--solver-refine-steps", type=str, default=None,
                     help="per LR update, '+'-separated filter degrees of extra outer iterations after "
                          "convergence, updates separated by ',' (e.g. '6' or '6+4,4')")
+    ap.add_argument("--deg-cold", type=str, default=None,
+                    help="comma-separated Chebyshev degrees of a cold solve's outer iterations (the last repeats; "
+                         "default solver.RankRSolver's)")
     ap.add_argument("--no-l-split", action="store_true", help="sparse Gram without the l-split ELL (A/B)")
     ap.add_argument("--no-transposed-output", action="store_true",
                     help="solver products without the C^T epilogue output (transpose passes instead; A/B)")
@@ -738,7 +787,8 @@ def main():
     # device generator only, and each rank's host threads are capped at its share of the cores
     if world > 1:
         torch.set_num_threads(max(1, torch.get_num_threads() // world))
-    Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev, host=PINNED if rank == 0 else 0)
+    pinned = (HOLDOUT[-1] + 1 if args.workload == "cfg2" else PINNED) if rank == 0 else 0
+    Wb = synth_batch(wl, B, wl.get("seed0", 0) + 1000 * rank, dev, host=pinned)
     h = make_h(wl)
     h = None if h is None else h.to(dev)
     parts = max(1, args.streams or default_parts(B))
@@ -746,13 +796,15 @@ def main():
     refine_steps = (tuple(tuple(int(d) for d in x.split("+") if d) for x in args.solver_refine_steps.split(","))
                     if args.solver_refine_steps else None)
 
+    skw = {"deg_cold": tuple(int(x) for x in args.deg_cold.split(","))} if args.deg_cold else None
+
     def step(nparts=None):
         nparts = parts if nparts is None else nparts
         # the hot path: caldera() (alg.py:24-112) on B matrices resident in HBM, results
         # (packed Q codes + scale, L, R, dequantised Q, error history) left in HBM.  The
         # drop-in API layer adds only output placement (alg.py:81 copies W to the host); it is
         # timed separately below ("api_path").
-        engines = [CalderaEngine(ep) for _ in range(nparts)]
+        engines = [CalderaEngine(ep, solver_kwargs=skw) for _ in range(nparts)]
         for e in engines:
             e.solver_tol_steps = tol_steps
             if refine_steps is not None:
@@ -982,7 +1034,8 @@ def main():
                             "gather_ms_per_step": gather_stats["ms"] / max(1, gather_stats["calls"]),
                             "included_in_value": True}
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
-    result["solver"] = {"parts": parts, "matvecs_per_part": st.get("matvecs", 0),
+    result["solver"] = {"parts": parts, "deg_cold": list(eng.solver.deg_cold) if eng.solver is not None else None,
+                        "matvecs_per_part": st.get("matvecs", 0),
                         "outer_iters": st.get("outer", 0), "stalled_matrices": st.get("stalls", 0),
                         "jacobi_unconverged": st.get("jacobi_unconverged", 0),
                         "block_jacobi_readbacks": st.get("bj_readbacks", 0),

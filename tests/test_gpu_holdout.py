@@ -1,0 +1,79 @@
+"""Out-of-sample parity (round 6): config 2 on 32 HELD-OUT matrices (seeds 16-47) that no solver
+schedule, tolerance or degree of this engine was ever tuned on, against the reference's own runs
+of them (tests/golden/final_codes_holdout.npz, ref_spread_cfg2_holdout.json: 8- and 4-thread
+runs of the unmodified reference, tests/golden/gen_golden_codes.py cfg2holdout) and against an
+exact rank-r step (tests/golden/exact_codes_cfg2_holdout.npz, gen_exact_codes.py holdout).
+The seeds sit at scattered positions of a B = 64 batch among 32 other random matrices.
+
+Bars (the same as the tuning-set test test_cfg2_seeds_inside_full_batch): Q + L R within
+max(1e-4, the reference's own 4- vs 8-thread spread) plus what the final codes' near-tie flips
+account for; final codes bit-exact, or within the reference's own spread of flips; and the
+rates measured on this set (bit-exact vs the reference, vs exact LR) as floors."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from final_codes import assert_codes_within_reference_spread, compare
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SEEDS = range(16, 48)
+# measured on this set (bench.py parity_timed_step.holdout): floors of the rates
+MIN_EXACT_VS_REFERENCE = 0
+MIN_EXACT_VS_EXACT_LR = 0
+
+
+def _omega(n, k=16, seed=1234):
+    return np.random.default_rng(seed).standard_normal((n, k))
+
+
+def test_cfg2_holdout_seeds_in_batch():
+    fx = np.load(os.path.join(GOLDEN, "final_codes_holdout.npz"), allow_pickle=False)
+    ex = np.load(os.path.join(GOLDEN, "exact_codes_cfg2_holdout.npz"), allow_pickle=False)
+    spread = json.load(open(os.path.join(GOLDEN, "ref_spread_cfg2_holdout.json")))["seeds"]
+    from ee274_convexcaldera_llm_quantization_amd.engine import CalderaEngine, EngineParams
+    from src.caldera.utils.dataclasses import CalderaParams
+    qp = CalderaParams(Q_bits=2, L_bits=16, R_bits=16, rank=128, iters=5, update_order=["Q", "LR"], sigma_reg=1e-8)
+    B = 64
+    pos = {s: (s * 37) % B for s in SEEDS}
+    assert len(set(pos.values())) == len(pos)
+    g = torch.Generator(device=DEV).manual_seed(456)
+    Wb = (torch.randn(B, 4096, 4096, device=DEV, generator=g) * 0.02).half()
+    import hashlib
+    for s, i in pos.items():
+        torch.manual_seed(s)
+        W = (torch.randn(4096, 4096) * 0.02).to(torch.float16)
+        assert hashlib.sha256(W.numpy().tobytes()).hexdigest() == str(fx[f"cfg2s{s}_W_sha256"])
+        Wb[i].copy_(W.to(DEV))
+    out = CalderaEngine(EngineParams.from_caldera_params(qp)).run(Wb)
+    om = torch.from_numpy(_omega(4096)).to(DEV)
+    n_ref = n_ex = 0
+    rows = []
+    for s, i in pos.items():
+        tag = f"cfg2s{s}"
+        d = out[i]
+        sk = (d["Q"].double() @ om + d["L"].double() @ (d["R"].double() @ om)).cpu().numpy()
+        ref = fx[f"{tag}_sketch_QLR"].astype(np.float64)
+        rel = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
+        qlr = float(torch.linalg.norm(d["Q"].double() + d["L"].double() @ d["R"].double()))
+        c = compare(tag, d["Q_idxs"], 4096, 4096, fx=fx)
+        e = compare(f"s{s}", d["Q_idxs"], 4096, 4096, fx=ex)
+        sp = spread[str(s)]
+        bar = max(1e-4, sp["rel_frob_QLR_ref4_vs_ref8"]) + 2.0 * float(fx[f"{tag}_Q_scale"]) * c["flips"] / qlr
+        rows.append((s, rel, bar, c, e["sha_equal"], sp))
+        n_ref += c["sha_equal"]
+        n_ex += e["sha_equal"]
+        assert abs(d["errors"]["Q"][0] - fx[f"{tag}_errors_Q"][0]) < 1e-6
+        assert abs(d["errors"]["LR"][0] - fx[f"{tag}_errors_LR"][0]) < 1e-5
+    for s, rel, bar, c, exact, sp in rows:
+        print(f"seed {s}: rel {rel:.2e} (bar {bar:.2e}, reference spread {sp['rel_frob_QLR_ref4_vs_ref8']:.1e}, "
+              f"its flips {sp['final_code_flips_ref4_vs_ref8']}); codes vs reference {c}; exact-LR codes {exact}")
+    print(f"held-out: bit-exact vs reference {n_ref}/{len(rows)}, vs exact LR {n_ex}/{len(rows)}")
+    for s, rel, bar, c, exact, sp in rows:
+        assert rel <= bar, (s, rel, bar, sp)
+        assert_codes_within_reference_spread(c, sp, f"seed {s}")
+    assert n_ref >= MIN_EXACT_VS_REFERENCE and n_ex >= MIN_EXACT_VS_EXACT_LR, (n_ref, n_ex)
