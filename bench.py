@@ -183,13 +183,13 @@ def holdout_parity(decs, wl):
     reference's runs and against an exact rank-r step, Q + L R against the reference's sketch, with
     the reference's own 4- vs 8-thread spread.  No solver schedule or tolerance was chosen on these
     matrices (tests/golden/gen_golden_codes.py cfg2holdout, gen_exact_codes.py holdout)."""
-    from final_codes import compare
+    from final_codes import classify, compare
     gd = os.path.join(ROOT, "tests", "golden")
     fx = np.load(os.path.join(gd, "final_codes_holdout.npz"), allow_pickle=False)
     ex = np.load(os.path.join(gd, "exact_codes_cfg2_holdout.npz"), allow_pickle=False)
     sp = json.load(open(os.path.join(gd, "ref_spread_cfg2_holdout.json")))["seeds"]
     m, n = wl["m"], wl["n"]
-    per, vs_ref, vs_ex, over = {}, [], [], {}
+    per, vs_ref, vs_ex, over, classes = {}, [], [], {}, {}
     for s in HOLDOUT:
         tag = f"cfg2s{s}"
         if f"{tag}_rowhash" not in fx.files or f"s{s}_rowhash" not in ex.files:
@@ -201,8 +201,10 @@ def holdout_parity(decs, wl):
         ref = fx[f"{tag}_sketch_QLR"].astype(np.float64)
         rel = float(np.linalg.norm(sk - ref) / np.linalg.norm(ref))
         spr = sp.get(str(s), {})
+        cls = classify(c, e["sha_equal"], spr)
+        classes.setdefault(cls, []).append(s)
         per[f"seed{s}"] = {"rel_frob_QLR": rel, "ref_spread": spr.get("rel_frob_QLR_ref4_vs_ref8"),
-                           "codes_vs_ref": c, "codes_vs_exact_lr_bit_exact": e["sha_equal"]}
+                           "codes_vs_ref": c, "codes_vs_exact_lr_bit_exact": e["sha_equal"], "class": cls}
         vs_ref.append(c)
         vs_ex.append(e)
         if rel > 1e-4:
@@ -215,6 +217,10 @@ def holdout_parity(decs, wl):
                 "final_code_flips_ref4_vs_ref8", 1) == 0),
             "rows_unexplained_vs_reference": sum(c["rows_unexplained"] for c in vs_ref),
             "flips_at_near_ties_vs_reference": sum(c["flips"] for c in vs_ref),
+            "classes": {k: classes.get(k, []) for k in ("reference", "ref_spread", "exact_lr", "miss")},
+            "classes_note": "final_codes.classify: the reference's codes / within its own 4- vs 8-thread spread / "
+                            "bit-exact with an exact rank-r step where the reference's fp32 LAPACK lands elsewhere / "
+                            "none of these",
             "seeds_over_1e-4": over, "per_seed": per}
 
 

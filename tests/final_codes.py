@@ -98,6 +98,32 @@ def assert_codes_within_reference_spread(c, sp, what=""):
         assert c["flips"] <= ref_flips, (what, c, sp)
 
 
+def within_reference_spread(c, sp):
+    """assert_codes_within_reference_spread as a predicate."""
+    try:
+        assert_codes_within_reference_spread(c, sp)
+        return True
+    except AssertionError:
+        return False
+
+
+def classify(c_ref, exact_lr_equal, sp):
+    """Where a config-2 matrix's final codes land:
+    'reference'     bit-exact with the reference's final codes;
+    'ref_spread'    within the reference's own 4- vs 8-thread spread (near-tie flips only);
+    'exact_lr'      bit-exact with an EXACT rank-r step's codes (fp64 LR, the reference's fp32 Q
+                    step) where the reference's fp32 LAPACK lands elsewhere -- the codes an
+                    infinitely accurate solver of alg.py's algorithm produces;
+    'miss'          none of these: a trajectory the solver's own error moved."""
+    if c_ref["sha_equal"]:
+        return "reference"
+    if within_reference_spread(c_ref, sp):
+        return "ref_spread"
+    if exact_lr_equal:
+        return "exact_lr"
+    return "miss"
+
+
 def frob_bar(tag, c, qlr_norm, ref_spread=0.0):
     """Bar on the relative Frobenius distance of Q + L R to the reference's run: max(1e-4, the
     reference's own run-to-run spread on this matrix) plus what the final codes' near-tie
