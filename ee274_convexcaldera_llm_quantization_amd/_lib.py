@@ -116,6 +116,7 @@ _SIGS = {
     "cq_jacobi_staged_workspace": (c_size, [c_i64, c_i64]),
     "cq_jacobi_eigh_staged": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_double, c_int, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_size, c_vp]),
+    "cq_extreme_eigs": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "cq_ritz_workspace": (c_size, [c_i64, c_i64, c_i64]),
     "cq_ritz_residual": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_size,
                                  c_vp]),
@@ -550,6 +551,17 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
     _check(lib.cq_jacobi_eigh(_p(A), p, B, max_sweeps, tol, _p(ev), _p(V32), _p(V64), _p(sw), _p(ws),
                               ws.numel(), _stream(A.device)), "cq_jacobi_eigh")
     return ev, V32, V64, sw
+
+
+def extreme_eigs(T: torch.Tensor, steps: int = 40) -> torch.Tensor:
+    """T (B, p, p) fp64 symmetric, p <= 192 (not overwritten) -> (B, 2) fp64 [largest,
+    smallest eigenvalue] by Lanczos + bisection (cq_extreme_eigs): the filter bounds of the
+    solver's cheap outer iterations without a values-only eigensolve."""
+    _require_hip(T)
+    B, p, _ = T.shape
+    ends = torch.empty((B, 2), dtype=torch.float64, device=T.device)
+    _check(load().cq_extreme_eigs(_p(T), p, B, int(steps), _p(ends), _stream(T.device)), "cq_extreme_eigs")
+    return ends
 
 
 class BlockJacobi:

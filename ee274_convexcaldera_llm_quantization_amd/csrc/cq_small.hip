@@ -723,6 +723,153 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
         }
 }
 
+// ------------------------------------------------------------------ extreme Ritz values
+// The cheap outer iterations of the rank-r solver only need the two ends of the Ritz spectrum
+// (the filter's bounds theta_0 and its cut theta_{p-1}); a full Jacobi eigensolve for them
+// (values only, off-norm 1e-2) costs several sweeps of a chain of rotations.  Here: `steps`
+// Lanczos iterations on S = (T + T^T) / 2 held in LDS as fp32 (fp32 products over a quarter of
+// the rows per wave, fp64 recurrences in wave 0: no barrier inside a reduction), then the
+// extreme eigenvalues of the Lanczos tridiagonal by 64-point multisection on Sturm counts (fp64,
+// to the last bit of the bracket).  They approach S's extremes from inside, to ~1e-6 relative
+// after a few dozen steps even on flat spectra; a lost orthogonality only duplicates converged
+// values.  One workgroup per matrix, deterministic (fixed start vector, fixed sum orders).
+constexpr int kLzThreads = 256, kLzMaxP = 192, kLzMaxSteps = 64;
+
+__device__ __forceinline__ int lz_sturm(const double* al, const double* b2, int m, double x) {
+    int cnt = 0;
+    double d = 1.0;
+    for (int k = 0; k < m; ++k) {
+        d = (al[k] - x) - (k > 0 ? b2[k] / d : 0.0);
+        if (d == 0.0) d = -1e-300;
+        cnt += d < 0.0;
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* __restrict__ T_all, int p, int steps,
+                                                                 double* __restrict__ ends) {
+    extern __shared__ __attribute__((aligned(16))) float lz_t[];   // S, p x p fp32 (row j at j p)
+    __shared__ float vf[kLzMaxP];                                  // current Lanczos vector (fp32 copy)
+    __shared__ float part[kLzThreads / 64][kLzMaxP];               // per-wave partial products
+    __shared__ double al[kLzMaxSteps], b2[kLzMaxSteps];            // alpha_k, beta_k^2
+    __shared__ int m_s;
+    const int64_t b = blockIdx.x;
+    const double* T = T_all + b * (int64_t)p * p;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int e = tid; e < p * p; e += kLzThreads) {
+        const int j = e / p, i = e % p;
+        lz_t[e] = (float)(0.5 * (T[(int64_t)j * p + i] + T[(int64_t)i * p + j]));
+    }
+    // wave 0 owns the vectors: lane l holds entries l, l + 64, l + 128 (fp64)
+    double v[3] = {0.0, 0.0, 0.0}, vp[3] = {0.0, 0.0, 0.0};
+    if (wid == 0) {
+        double ss = 0.0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int i = lane + 64 * q;
+            if (i < p) {
+                uint32_t h = (uint32_t)i * 2654435761u ^ 0x9E3779B9u;
+                h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15;
+                v[q] = ((double)(h & 0xffffu) / 65536.0 + 0.5) * ((h & 0x10000u) ? 1.0 : -1.0);
+                ss += v[q] * v[q];
+            }
+        }
+        const double inv = 1.0 / sqrt(wave_sum(ss));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            v[q] *= inv;
+            if (lane + 64 * q < p) vf[lane + 64 * q] = (float)v[q];
+        }
+        if (lane == 0) m_s = steps;
+    }
+    __syncthreads();
+    const int jc = (p + 3) / 4, j0 = wid * jc, j1 = min(p, j0 + jc);
+    double beta = 0.0;
+    for (int k = 0; k < steps; ++k) {
+        // partial products of S v over this wave's rows j (S symmetric: column reads coalesce)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int i = lane + 64 * q;
+            if (i < p) {
+                float acc = 0.f;
+                for (int j = j0; j < j1; ++j) acc = __builtin_fmaf(lz_t[j * p + i], vf[j], acc);
+                part[wid][i] = acc;
+            }
+        }
+        __syncthreads();
+        int stop = 0;
+        if (wid == 0) {
+            double w[3], a = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = lane + 64 * q;
+                w[q] = 0.0;
+                if (i < p) {
+                    w[q] = ((double)part[0][i] + (double)part[1][i]) + ((double)part[2][i] + (double)part[3][i]);
+                    w[q] -= beta * vp[q];
+                    a += w[q] * v[q];
+                }
+            }
+            a = wave_sum(a);
+            double ss = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                w[q] -= a * v[q];
+                ss += w[q] * w[q];
+            }
+            ss = wave_sum(ss);
+            if (lane == 0) {
+                al[k] = a;
+                b2[k + 1 < kLzMaxSteps ? k + 1 : 0] = ss;
+            }
+            beta = sqrt(ss);
+            // breakdown (an invariant subspace: its values are exact) or the last step
+            stop = !(beta > 1e-30 * fabs(a)) || k + 1 == steps;
+            if (stop && lane == 0) m_s = k + 1;
+            const double inv = stop ? 0.0 : 1.0 / beta;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                vp[q] = v[q];
+                v[q] = w[q] * inv;
+                if (lane + 64 * q < p) vf[lane + 64 * q] = (float)v[q];
+            }
+        }
+        __syncthreads();
+        if (m_s != steps || k + 1 == steps) break;
+    }
+    // extreme eigenvalues of the m x m tridiagonal: wave 0 the largest, wave 1 the smallest
+    const int m = m_s;
+    if (wid < 2) {
+        double lo = INFINITY, hi = -INFINITY;
+        for (int k = 0; k < m; ++k) {
+            const double r = (k > 0 ? sqrt(b2[k]) : 0.0) + (k + 1 < m ? sqrt(b2[k + 1]) : 0.0);
+            lo = fmin(lo, al[k] - r);
+            hi = fmax(hi, al[k] + r);
+        }
+        const double pad = 1e-12 * fmax(fabs(lo), fabs(hi)) + 1e-300;
+        double a = lo - pad, c = hi + pad;   // count(a) = 0, count(c) = m
+        bool bad = !(a == a) || !(c == c);
+        for (int it = 0; it < 9 && !bad; ++it) {   // 65^-9 of the Gershgorin width: fp64 resolution
+            const double x = a + (c - a) * (double)(lane + 1) / 65.0;
+            const int cnt = lz_sturm(al, b2, m, x);
+            if (wid == 0) {   // largest: the first x with every eigenvalue below it
+                const uint64_t msk = __ballot(cnt == m);
+                const int jf = msk ? __builtin_ctzll(msk) : 64;
+                const double nc = jf < 64 ? a + (c - a) * (double)(jf + 1) / 65.0 : c;
+                const double na = jf > 0 ? a + (c - a) * (double)jf / 65.0 : a;
+                a = na; c = nc;
+            } else {          // smallest: the last x with no eigenvalue below it
+                const uint64_t msk = __ballot(cnt == 0);
+                const int jl = __builtin_popcountll(msk);   // counts are monotone in x: a prefix
+                const double na = jl > 0 ? a + (c - a) * (double)jl / 65.0 : a;
+                const double nc = jl < 64 ? a + (c - a) * (double)(jl + 1) / 65.0 : c;
+                a = na; c = nc;
+            }
+        }
+        if (lane == 0) ends[2 * b + wid] = bad ? NAN : 0.5 * (a + c);
+    }
+}
+
 // ------------------------------------------------------------------ Ritz residuals
 __global__ __launch_bounds__(256) void ritz_partial_kernel(const float* __restrict__ X,
                                                             const float* __restrict__ Z,
@@ -896,6 +1043,15 @@ int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int ns
         return set_error(CQ_EWORKSPACE, "cq_jacobi_eigh_staged: workspace too small");
     return cq::bj_stage(A, p, batch, phase, nsweeps, tol, want_vectors != 0, evals, V32, V64, sweeps_out, pending_out,
                         ws, ws_bytes, as_stream(stream));
+}
+
+int cq_extreme_eigs(const double* T, int64_t p, int64_t batch, int steps, double* ends, void* stream) {
+    CQ_REQUIRE(T && ends && p >= 2 && batch > 0 && batch <= 2147483647, "cq_extreme_eigs: bad args");
+    CQ_REQUIRE(p <= kLzMaxP, "cq_extreme_eigs: p > %d (the fp32 copy of T must fit the LDS)", kLzMaxP);
+    CQ_REQUIRE(steps >= 1 && steps < kLzMaxSteps, "cq_extreme_eigs: steps must be in [1, %d)", kLzMaxSteps);
+    const size_t lds = (size_t)p * p * sizeof(float);
+    extreme_eigs_kernel<<<(unsigned)batch, kLzThreads, lds, as_stream(stream)>>>(T, (int)p, steps, ends);
+    return check_launch("cq_extreme_eigs");
 }
 
 size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch) {

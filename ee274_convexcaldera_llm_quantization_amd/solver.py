@@ -178,6 +178,7 @@ JACOBI_MAX_SWEEPS = 30
 BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
 BJ_SMALL_SUBPROBLEMS = 256  # batches with at most this many 64 x 64 block-Jacobi subproblems take it at every p
 STALL_RATIO = 0.98
+VALUES_LANCZOS = 40  # Lanczos steps for the cheap iterations' filter bounds (0: values-only Jacobi)
 
 
 class SolverStats:
@@ -208,7 +209,7 @@ class RankRSolver:
                  seed: int = 0x5EED, jacobi_tol: float = 1e-7, filter_precision: str = "f16x3",
                  cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool = False,
                  jacobi_tol_values: float = 1e-2, criterion: str = "product",
-                 jacobi_values_sweeps: int = 30):
+                 jacobi_values_sweeps: int = 30, values_lanczos: int | None = None):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -239,6 +240,10 @@ class RankRSolver:
         # sweep cap of the values-only eigensolves (cheap iterations: the Ritz values only set
         # the next filter's bounds)
         self.jacobi_values_sweeps = int(jacobi_values_sweeps)
+        # the cheap iterations' filter bounds (the two ends of the Ritz spectrum) from this many
+        # Lanczos steps on T (cq_extreme_eigs, one launch, no read-back) instead of a values-only
+        # eigensolve; 0: the eigensolve (p > 192 always: T's fp32 copy must fit one CU's LDS)
+        self.values_lanczos = int(VALUES_LANCZOS if values_lanczos is None else values_lanczos)
         self.refine = ()   # extra full outer iterations after convergence (per call; engine.py)
         self.X = None      # warm-start Ritz block (B, k, p)
         self.theta = None  # its Ritz values (B, p) fp64: filter bounds for the next call
@@ -383,6 +388,14 @@ class RankRSolver:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
+        if values_only and self.values_lanczos > 0 and self.p <= 192:
+            # only theta_0 and theta_{p-1} are read (filter bounds): Lanczos ends, the rest NaN
+            ends = K.extreme_eigs(T, self.values_lanczos)
+            theta = torch.full((self.B, self.p), math.nan, dtype=torch.float64, device=T.device)
+            theta[:, 0] = ends[:, 0]
+            theta[:, self.p - 1] = ends[:, 1]
+            self._last_sw = torch.zeros(self.B, dtype=torch.int32, device=T.device)
+            return theta, X, None
         if values_only:
             # eigenvalue errors are O(off-norm^2): a loose off-norm tolerance still gives the
             # filter bounds to ~1e-8 relative, in fewer sweeps

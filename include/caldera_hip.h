@@ -244,6 +244,14 @@ int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int ns
                           double* evals, float* V32, double* V64, int* sweeps_out, int* pending_out, void* ws,
                           size_t ws_bytes, void* stream);
 
+/* The two ends of the spectrum of each symmetric T (p x p fp64, (T + T^T) / 2 used, not
+ * overwritten): ends[2 b] = largest, ends[2 b + 1] = smallest eigenvalue, from `steps`
+ * (1 <= steps < 64) Lanczos iterations and bisection on the Lanczos tridiagonal (approach the
+ * true ends from inside; exact when the iteration breaks down on an invariant subspace).
+ * p <= 192.  The rank-r solver's cheap outer iterations take their Chebyshev filter bounds
+ * from it instead of a values-only eigensolve (the SVD replacement of alg.py:217). */
+int cq_extreme_eigs(const double* T, int64_t p, int64_t batch, int steps, double* ends, void* stream);
+
 /* Ritz residuals: out[b] = max_{i<r} ||Z[:,i] - theta_i X[:,i]||_2 / |theta_0|
  * (X, Z: k x p row-major with ld p).  theta fp64 [b*p..]. */
 size_t cq_ritz_workspace(int64_t k, int64_t r, int64_t batch);

@@ -384,6 +384,36 @@ def test_jacobi_register_path_accuracy(K, p):
     assert torch.equal(V32.cpu().double(), V)
 
 
+@pytest.mark.parametrize("p", [8, 64, 128, 192])
+def test_extreme_eigs_lanczos(K, p):
+    """cq_extreme_eigs, the filter bounds of the solver's cheap outer iterations: both ends of
+    the spectrum approached from inside — to 1e-6 of the spread on Wishart spectra, inside a flat
+    top cluster (a Ritz-like spectrum, 1 + 1e-3 u) to its width; exact when p <= steps (the
+    Lanczos iteration breaks down on the whole space); T untouched; a NaN gives NaN ends."""
+    torch.manual_seed(5 + p)
+    X = torch.randn(4, 1024, p, dtype=torch.float64)
+    S = X.transpose(1, 2) @ X
+    Q, _ = torch.linalg.qr(torch.randn(p, p, dtype=torch.float64))
+    lam = torch.cat([1 + 1e-3 * torch.rand(p - p // 3, dtype=torch.float64), 0.5 * torch.rand(p // 3, dtype=torch.float64)])
+    S[2] = Q @ torch.diag(lam) @ Q.T
+    S[3, 1, 2] = math.nan
+    Sd = S.to(DEV)
+    before = Sd.clone()
+    ends = K.extreme_eigs(Sd, 40).cpu()
+    assert torch.equal(Sd.view(torch.int64), before.view(torch.int64))   # (bitwise: matrix 3 holds a NaN)
+    assert torch.isnan(ends[3]).all()
+    ref = torch.linalg.eigvalsh(0.5 * (S[:3] + S[:3].transpose(1, 2)))
+    spread = ref[:, -1] - ref[:, 0]
+    hi_err = (ref[:, -1] - ends[:3, 0]) / spread
+    lo_err = (ends[:3, 1] - ref[:, 0]) / spread
+    assert (hi_err > -1e-9).all() and (lo_err > -1e-9).all(), (hi_err, lo_err)   # from inside
+    exact = p <= 40
+    for b in range(3):
+        tol_hi = 1e-10 if exact else (2e-3 if b == 2 else 1e-6)
+        tol_lo = 1e-10 if exact else (1e-5 if b == 2 else 1e-6)
+        assert hi_err[b] < tol_hi and lo_err[b] < tol_lo, (b, hi_err[b].item(), lo_err[b].item())
+
+
 @pytest.mark.parametrize("p", [256, 384])  # panel 32 / panel 16
 def test_whiten_blocked(K, p):
     torch.manual_seed(10)
