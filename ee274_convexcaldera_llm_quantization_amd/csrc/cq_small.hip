@@ -553,20 +553,30 @@ static size_t jacobi_reg_bytes(int p) {
 // Symmetric Gaussian elimination S = L D L^T (rank-revealing: a pivot below rcond2 times the
 // largest is dropped), E = L^{-1}; Wt = E^T D^{-1/2}.  One workgroup per matrix.
 // LDL^T block form, nb = 32 pivots per panel J:
-//   1. one wave factors the 32 x 32 diagonal block in registers (lane l = row l of the
-//      symmetric block and of its L^{-1}; the pivot row is broadcast by shuffles): pivots
-//      (rank-revealing drop rule unchanged), L11^{-1};
+//   1. the 32 x 32 diagonal block in LDS, one barrier per pivot: pivots (rank-revealing drop
+//      rule), L11^{-1};
 //   2. panel rows of S right of the block, U12 = L11^{-1} S12, and the panel rows of
 //      E = L^{-1} (columns < J + 32), Ep = L11^{-1} E_panel — v_mfma_f64_16x16x4f64 tiles of
-//      32 rows x 16 columns (one wave per column block: in place without a race);
-//   3. trailing S (upper tiles) -= G^T U12 with G = diag(1/d) U12, trailing E rows -= G^T Ep.
-// Three workgroup barriers per panel instead of two per pivot; operands come from L2 (S, E
-// are fp64 p x p per matrix), so the LDS footprint is small and p is unbounded.  Products and
-// sums in fp64, as the scalar loops; the row operations are the same, in block order.
+//      32 rows x 16 columns (one wave per column block), written to the LDS panel (32 x p: Ep
+//      in columns < J + 32, U12 right of them) and Ep also to E (U12 is read by this panel
+//      only: S's panel rows are not written back);
+//   3. trailing S (upper tiles) -= G^T U12 with G = diag(1/d) U12, trailing E rows -= G^T Ep,
+//      both operands from the LDS panel; each wave takes its tiles two at a time with the
+//      destination tiles' loads issued before the MFMAs.
+// Three workgroup barriers per panel; S and E (fp64 p x p per matrix) stay in global memory
+// (L2) and only the current panel's 32 rows live in LDS (256 p bytes: p <= ~560; larger p
+// read the panel in place from L2, <false>).  Round 6: the trailing updates read their
+// operands from the LDS panel instead of L2, two tiles per wave at a time (the same fp64
+// values, MFMAs and sums in the same order: the same bits; p = 192 0.23 -> 0.18 ms at B = 1,
+// 0.33 -> 0.24 ms at B = 256, tools/bench_whiten.py).
 constexpr int kWmThreads = 512;
+// LDS panel pitch in doubles, = 16 mod 32: of a 16 x 4 fragment read, rows k and k + 1 (one
+// 32-lane half) fall on disjoint halves of the banks
+__host__ __device__ inline int wm_pitch(int p) { return p + (48 - p % 32) % 32; }
 constexpr int kWmWaves = kWmThreads / 64;
 
 
+template <bool LP>   // LP: the panel rows in LDS (p <= 512); else read in place from L2 (any p)
 __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __restrict__ S_all, int p, double rc2,
                                                                      double* __restrict__ E_all,
                                                                      float* __restrict__ W32, int* __restrict__ info) {
@@ -575,6 +585,8 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
     double* Li = piv + p;           // 32 x 33: L11^{-1} of the current panel (row-major, padded)
     double* rp = Li + 32 * 33;      // 32: 1 / pivot (0 for dropped) of the current panel
     double* Bk = rp + 32;           // 32 x 33: the diagonal block being factored
+    const int pp = wm_pitch(p);     // LDS panel pitch
+    double* PP = Bk + 32 * 33;      // 32 x pp: Ep (columns < J + 32) | U12 (columns >= J + 32)
     __shared__ int bad;
     __shared__ double dmax_s;
     __shared__ double red[16];
@@ -644,8 +656,8 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
             if (tid == 0) bad += nbad;
         }
         __syncthreads();
-        // ---- 2. U12 = L11^{-1} S12 (columns >= t0) and Ep = L11^{-1} E_panel (columns < t0),
-        // in place; one wave per 16-column block, both 16-row halves
+        // ---- 2. U12 = L11^{-1} S12 (columns >= t0) and Ep = L11^{-1} E_panel (columns < t0)
+        // into the LDS panel (Ep also to E); one wave per 16-column block, both 16-row halves
         const int ncs = (p - t0 + 15) / 16, nce = (t0 + 15) / 16;
         for (int cb = wid; cb < ncs + nce; cb += kWmWaves) {
             const bool isS = cb < ncs;
@@ -666,7 +678,11 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * h + lk + 4 * r;
-                    if (k < nb && col < clim) M[(int64_t)(J + k) * p + col] = acc[h][r];
+                    if (col < clim) {
+                        const double v = k < nb ? acc[h][r] : 0.0;
+                        if (LP) PP[k * pp + col] = v;
+                        if ((!isS || !LP) && k < nb) M[(int64_t)(J + k) * p + col] = v;
+                    }
                 }
         }
         __syncthreads();
@@ -675,39 +691,56 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
         //   E[i][c] -= sum_k G^T[i][k] Ep[k][c]   (rows i >= t0, columns c < t0)
         const int nt = (p - t0 + 15) / 16;
         const int nst = nt * (nt + 1) / 2, net = nt * nce;
-        for (int t = wid; t < nst + net; t += kWmWaves) {
-            int ti, c0;
-            double* M;
+        auto tile_of = [&](int t, int& i0, int& c0, double*& M) {
             if (t < nst) {  // upper tile (ti, tj), tj >= ti
                 int tj = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
                 if (tj * (tj + 1) / 2 > t) --tj;
                 if ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
-                ti = t - tj * (tj + 1) / 2;
+                i0 = t0 + 16 * (t - tj * (tj + 1) / 2);
                 c0 = t0 + 16 * tj;
                 M = S;
             } else {
-                ti = (t - nst) / nce;
+                i0 = t0 + 16 * ((t - nst) / nce);
                 c0 = 16 * ((t - nst) % nce);
                 M = E;
             }
-            const int i0 = t0 + 16 * ti;
-            const int clim = (M == S) ? p : t0;
-            const int col = c0 + l16, arow = i0 + l16;
-            f64x4v acc = f64x4v{0.0, 0.0, 0.0, 0.0};
+        };
+        for (int t = wid; t < nst + net; t += 2 * kWmWaves) {
+            const int tb = t + kWmWaves;
+            const bool two = tb < nst + net;
+            int i0[2] = {0, 0}, c0[2] = {0, 0};
+            double* M[2] = {S, S};
+            tile_of(t, i0[0], c0[0], M[0]);
+            if (two) tile_of(tb, i0[1], c0[1], M[1]);
+            double dv[2][4];
 #pragma unroll
-            for (int k0 = 0; k0 < 32; k0 += 4) {
-                const int k = k0 + lk;
-                const bool kv = k < nb;
-                const double av = (kv && arow < p) ? S[(int64_t)(J + k) * p + arow] * rp[k] : 0.0;
-                const double bv = (kv && col < clim) ? M[(int64_t)(J + k) * p + col] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            for (int u = 0; u < 2; ++u) {   // the destination tiles first: their loads fly under the MFMAs
+                const int clim = (M[u] == S) ? p : t0;
+                const int col = c0[u] + l16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = i0[u] + lk + 4 * r;
+                    dv[u][r] = (u == 0 || two) && i < p && col < clim ? M[u][(int64_t)i * p + col] : 0.0;
+                }
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = i0 + lk + 4 * r;
-                if (i < p && col < clim) {
-                    double* dst = M + (int64_t)i * p + col;
-                    *dst = *dst - acc[r];
+            for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !two) break;
+                const int clim = (M[u] == S) ? p : t0;
+                const int col = c0[u] + l16, arow = i0[u] + l16;
+                f64x4v acc = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k0 = 0; k0 < 32; k0 += 4) {
+                    const int k = k0 + lk;
+                    const bool kv = k < nb;
+                    const double av = (kv && arow < p) ? (LP ? PP[k * pp + arow] : S[(int64_t)(J + k) * p + arow]) * rp[k] : 0.0;
+                    const double bv = (kv && col < clim) ? (LP ? PP[k * pp + col] : M[u][(int64_t)(J + k) * p + col]) : 0.0;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = i0[u] + lk + 4 * r;
+                    if (i < p && col < clim) M[u][(int64_t)i * p + col] = dv[u][r] - acc[r];
                 }
             }
         }
@@ -756,9 +789,15 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
     const int64_t b = blockIdx.x;
     const double* T = T_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int e = tid; e < p * p; e += kLzThreads) {
+    for (int e = tid; e < p * p; e += kLzThreads) lz_t[e] = (float)T[e];   // coalesced
+    __syncthreads();
+    for (int e = tid; e < p * p; e += kLzThreads) {   // S = (T + T^T) / 2, each pair once
         const int j = e / p, i = e % p;
-        lz_t[e] = (float)(0.5 * (T[(int64_t)j * p + i] + T[(int64_t)i * p + j]));
+        if (i < j) {
+            const float v = 0.5f * (lz_t[e] + lz_t[i * p + j]);
+            lz_t[e] = v;
+            lz_t[i * p + j] = v;
+        }
     }
     // wave 0 owns the vectors: lane l holds entries l, l + 64, l + 128 (fp64)
     double v[3] = {0.0, 0.0, 0.0}, vp[3] = {0.0, 0.0, 0.0};
@@ -787,14 +826,37 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
     double beta = 0.0;
     for (int k = 0; k < steps; ++k) {
         // partial products of S v over this wave's rows j (S symmetric: column reads coalesce)
+        {
+            // three independent chains per lane (rows i = lane + 64 q; beyond p: row 0, unused),
+            // four rows j per step so the LDS reads of several j are in flight
+            const int i0 = lane, i1 = lane + 64 < p ? lane + 64 : 0, i2 = lane + 128 < p ? lane + 128 : 0;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+            int j = j0;
+            for (; j + 4 <= j1; j += 4) {
+                float t0[4], t1[4], t2[4], vj[4];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int i = lane + 64 * q;
-            if (i < p) {
-                float acc = 0.f;
-                for (int j = j0; j < j1; ++j) acc = __builtin_fmaf(lz_t[j * p + i], vf[j], acc);
-                part[wid][i] = acc;
+                for (int u = 0; u < 4; ++u) {
+                    vj[u] = vf[j + u];
+                    t0[u] = lz_t[(j + u) * p + i0];
+                    t1[u] = lz_t[(j + u) * p + i1];
+                    t2[u] = lz_t[(j + u) * p + i2];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a0 = __builtin_fmaf(t0[u], vj[u], a0);
+                    a1 = __builtin_fmaf(t1[u], vj[u], a1);
+                    a2 = __builtin_fmaf(t2[u], vj[u], a2);
+                }
             }
+            for (; j < j1; ++j) {
+                const float vj = vf[j];
+                a0 = __builtin_fmaf(lz_t[j * p + i0], vj, a0);
+                a1 = __builtin_fmaf(lz_t[j * p + i1], vj, a1);
+                a2 = __builtin_fmaf(lz_t[j * p + i2], vj, a2);
+            }
+            if (i0 < p) part[wid][i0] = a0;
+            if (lane + 64 < p) part[wid][lane + 64] = a1;
+            if (lane + 128 < p) part[wid][lane + 128] = a2;
         }
         __syncthreads();
         int stop = 0;
@@ -997,9 +1059,13 @@ int cq_spd_whiten_rcond(double* S, int64_t p, int64_t batch, double rcond2, floa
     hipStream_t s = as_stream(stream);
     // E is built in Wt64 (scratch); the final fp64 Wt is left in S (ABI 4: no device copy to
     // Wt64 -- the copy was 0.46 ms per B = 256, p = 192 call, ~18 ms per config-2 step)
-    const size_t wlm = (size_t)(p + 2 * 32 * 33 + 32) * sizeof(double);
-    CQ_REQUIRE(wlm <= 64 * 1024, "cq_spd_whiten: p too large");
-    spd_whiten_mfma_kernel<<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    const size_t wsm = (size_t)(p + 2 * 32 * 33 + 32) * sizeof(double);
+    const size_t wlm = wsm + (size_t)32 * wm_pitch((int)p) * sizeof(double);
+    CQ_REQUIRE(wsm <= 64 * 1024, "cq_spd_whiten: p too large");
+    if (wlm <= 150 * 1024)
+        spd_whiten_mfma_kernel<true><<<(unsigned)batch, kWmThreads, wlm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
+    else
+        spd_whiten_mfma_kernel<false><<<(unsigned)batch, kWmThreads, wsm, s>>>(S, (int)p, rcond2, Wt64, Wt32, info);
     return check_launch("cq_spd_whiten");
 }
 

@@ -387,9 +387,10 @@ def test_jacobi_register_path_accuracy(K, p):
 @pytest.mark.parametrize("p", [8, 64, 128, 192])
 def test_extreme_eigs_lanczos(K, p):
     """cq_extreme_eigs, the filter bounds of the solver's cheap outer iterations: both ends of
-    the spectrum approached from inside — to 1e-6 of the spread on Wishart spectra, inside a flat
-    top cluster (a Ritz-like spectrum, 1 + 1e-3 u) to its width; exact when p <= steps (the
-    Lanczos iteration breaks down on the whole space); T untouched; a NaN gives NaN ends."""
+    the spectrum approached from inside — to 5e-6 of the spread on Wishart spectra, inside a flat
+    top cluster (a Ritz-like spectrum, 1 + 1e-3 u) to its width; exact up to the fp32 copy of T
+    when p <= steps (the Lanczos iteration breaks down on the whole space); T untouched; a NaN
+    gives NaN ends."""
     torch.manual_seed(5 + p)
     X = torch.randn(4, 1024, p, dtype=torch.float64)
     S = X.transpose(1, 2) @ X
@@ -406,11 +407,12 @@ def test_extreme_eigs_lanczos(K, p):
     spread = ref[:, -1] - ref[:, 0]
     hi_err = (ref[:, -1] - ends[:3, 0]) / spread
     lo_err = (ends[:3, 1] - ref[:, 0]) / spread
-    assert (hi_err > -1e-9).all() and (lo_err > -1e-9).all(), (hi_err, lo_err)   # from inside
+    # from inside, up to the fp32 rounding of the LDS copy of T (~6e-8 of its norm)
+    assert (hi_err > -5e-7).all() and (lo_err > -5e-7).all(), (hi_err, lo_err)
     exact = p <= 40
     for b in range(3):
-        tol_hi = 1e-10 if exact else (2e-3 if b == 2 else 1e-6)
-        tol_lo = 1e-10 if exact else (1e-5 if b == 2 else 1e-6)
+        tol_hi = 5e-7 if exact else (2e-3 if b == 2 else 5e-6)
+        tol_lo = 5e-7 if exact else (1e-5 if b == 2 else 5e-6)
         assert hi_err[b] < tol_hi and lo_err[b] < tol_lo, (b, hi_err[b].item(), lo_err[b].item())
 
 
