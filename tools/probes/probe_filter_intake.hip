@@ -14,7 +14,18 @@
 //   mode 7  X^T's fragments loaded by each wave straight into registers (global_load, L2/L1-
 //           served): row block i's fragments of step t + 1 are loaded into the registers of
 //           step t's right after its MFMAs; only G through the LDS-DMA ring
-// Results are numerically meaningless for modes 1-6 (stale LDS / reused fragments).
+//   mode 8  loads and barriers only (no fragment reads, no MFMAs): the 2-stage ring's intake floor
+//   mode 9  a 3-stage ring (round 6): 192 x 192 x 32 tiles (48 KB stages, 3 fit
+//           the 144 KB), 12 waves of 48 x 64, stage t + 2 issued at step t (counted vmcnt: two
+//           stages in flight instead of one) -- the same MFMAs per output, 1.33x the intake per
+//           flop (X^T re-read by twice as many tiles)
+//   mode 10 mode 9's loads and barriers only (its intake floor)
+//   mode 11 the 192 x 384 tile and 2-slot ring, but G's stage t + 2 issued inside step t: every
+//           wave reads its G fragments of step t first (they are already front-loaded), a second
+//           barrier, then the G loads of t + 2 into the slot just read (two steps to land instead
+//           of one: 2/3 of the intake); X^T's stage t + 1 at the top of step t as before
+//   mode 12 mode 11's loads and barriers only
+// Results are numerically meaningless for modes 1-6, 8, 10 (stale LDS / reused fragments).
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -o probe_filter_intake probe_filter_intake.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -105,6 +116,7 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
                   (MODE != 1 || ((t + 1) & 1) == 0) && MODE != 6, MODE != 5 && MODE != 7);
         const _Float16* sA = smem + (t & 1) * STAGE;
         const _Float16* sB = sA + 2 * APART;
+        if (MODE == 8) continue;
         if (MODE != 3) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -159,6 +171,171 @@ __global__ __launch_bounds__(THREADS, 1) void probe_kernel(const _Float16* Ah, c
         }
 }
 
+
+// mode 9 / 10: 192 x 192 tiles, 3-stage ring, two stages in flight
+constexpr int BN3 = 192, BPART3 = BN3 * BK, STAGE3 = 2 * APART + 2 * BPART3;
+constexpr size_t LDS3 = (size_t)3 * STAGE3 * 2;   // 144 KB
+constexpr int PER_WAVE3 = 4;                      // 48 wave-instructions per stage / 12 waves
+
+template <int MODE>
+__global__ __launch_bounds__(THREADS, 1) void probe3_kernel(const _Float16* Ah, const _Float16* Al, const _Float16* Bh,
+                                                            const _Float16* Bl, int64_t M, int64_t N, int64_t K,
+                                                            int64_t tiles_n, float* C) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    const int64_t b = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    const int64_t n0 = tn * BN3;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid & 3, wn = wid >> 2, l16 = lane & 15, lq = lane >> 4;   // 4 x 48 rows, 3 x 64 columns
+    uint32_t off[PER_WAVE3];
+    const _Float16* src[PER_WAVE3];
+    int dsto[PER_WAVE3];
+#pragma unroll
+    for (int u = 0; u < PER_WAVE3; ++u) {
+        const int I = wid * PER_WAVE3 + u;   // 0..47: Ah 0-11, Al 12-23, Bh 24-35, Bl 36-47
+        const bool isA = I < 24;
+        const int part = isA ? (I >= 12) : (I >= 36);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 12 * part);
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ swz(row);
+        int64_t gr = (isA ? 0 : n0) + row;
+        const int64_t lim = isA ? M : N;
+        gr = gr < lim ? gr : lim - 1;
+        off[u] = (uint32_t)(gr * 32 + c * 8);
+        src[u] = isA ? (part ? Al : Ah) + b * M * K : (part ? Bl : Bh) + b * N * K;
+        dsto[u] = (isA ? part * APART : 2 * APART + part * BPART3) + (16 * sub) * BK;
+    }
+    auto issue = [&](int64_t k0, _Float16* st) {
+#pragma unroll
+        for (int u = 0; u < PER_WAVE3; ++u) {
+            const int64_t lda = (wid * PER_WAVE3 + u) < 24 ? M : N;   // A: instructions 0-23 (waves 0-5)
+            __builtin_amdgcn_global_load_lds((const void*)(src[u] + (k0 >> 5) * (lda * 32) + off[u]),
+                                             (__attribute__((address_space(3))) void*)(st + dsto[u]), 16, 0, 0);
+        }
+    };
+    f32x4v acc[3][4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int64_t nt = K / BK;
+    issue(0, smem);
+    if (nt > 1) issue(BK, smem + STAGE3);
+    for (int64_t t = 0; t < nt; ++t) {
+        if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // stage t + 1 may still fly
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // stage t landed everywhere; slot of t - 1 fully read
+        if (t + 2 < nt) issue((t + 2) * BK, smem + ((t + 2) % 3) * STAGE3);
+        if (MODE == 10) continue;
+        const _Float16* sA = smem + (t % 3) * STAGE3;
+        const _Float16* sB = sA + 2 * APART;
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bh[j] = frag(sB, 64 * wn + 16 * j + l16, lq);
+            bl[j] = frag(sB + BPART3, 64 * wn + 16 * j + l16, lq);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const f16x8 ah = frag(sA, 48 * wm + 16 * i + l16, lq);
+            const f16x8 al = frag(sA + APART, 48 * wm + 16 * i + l16, lq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = 48 * wm + 16 * i + l16, col = n0 + 64 * wn + 16 * j + 4 * lq;
+            if (col < N)
+                *reinterpret_cast<float4*>(C + (b * M + row) * N + col) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+}
+
+// mode 11 / 12: G two steps ahead in the 2-slot ring (a second barrier per step)
+template <int MODE>
+__global__ __launch_bounds__(THREADS, 1) void probe11_kernel(const _Float16* Ah, const _Float16* Al, const _Float16* Bh,
+                                                             const _Float16* Bl, int64_t M, int64_t N, int64_t K,
+                                                             int64_t tiles_n, float* C) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    const int64_t b = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    const int64_t n0 = tn * BN;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid & 1, wn = wid >> 1, l16 = lane & 15, lq = lane >> 4;
+    const bool aw = wid < 4;   // waves 0-3 load X^T (instructions 0-23), waves 4-11 load G
+    uint32_t off[PER_WAVE];
+#pragma unroll
+    for (int u = 0; u < PER_WAVE; ++u) {
+        const int I = wid * PER_WAVE + u;
+        const bool isA = I < 24;
+        const int part = isA ? (I >= 12) : (I >= 48);
+        const int sub = isA ? (I - 12 * part) : (I - 24 - 24 * part);
+        const int row = 16 * sub + (lane >> 2);
+        const int c = (lane & 3) ^ swz(row);
+        int64_t gr = (isA ? 0 : n0) + row;
+        const int64_t lim = isA ? M : N;
+        gr = gr < lim ? gr : lim - 1;
+        off[u] = (uint32_t)(gr * 32 + c * 8);
+    }
+    f32x4v acc[6][4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int64_t nt = K / BK;
+    issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, 0, smem, true);
+    if (nt > 1) issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, BK, smem + STAGE, true, false);   // G of step 1
+    for (int64_t t = 0; t < nt; ++t) {
+        if (!aw && t + 1 < nt) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // G of t + 1 may fly
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // stage t landed; X^T slot of t - 1 fully read
+        if (t + 1 < nt) issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE, false);
+        const _Float16* sA = smem + (t & 1) * STAGE;
+        const _Float16* sB = sA + 2 * APART;
+        f16x8 bh[4], bl[4];
+        if (MODE == 11) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[j] = frag(sB, 64 * wn + 16 * j + l16, lq);
+                bl[j] = frag(sB + BPART, 64 * wn + 16 * j + l16, lq);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // every wave holds its G fragments of step t: the G slot is free
+        if (t + 2 < nt) issue(Ah, Al, Bh, Bl, b, M, N, K, wid, off, (t + 2) * BK, smem + (t & 1) * STAGE, true, false);
+        if (MODE == 12) continue;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const f16x8 ah = frag(sA, 96 * wm + 16 * i + l16, lq);
+            const f16x8 al = frag(sA + APART, 96 * wm + 16 * i + l16, lq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = 96 * wm + 16 * i + l16, col = n0 + 64 * wn + 16 * j + 4 * lq;
+            if (col < N)
+                *reinterpret_cast<float4*>(C + (b * M + row) * N + col) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+}
+
 __global__ void fill_kernel(_Float16* p, int64_t n, uint32_t seed) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint32_t x = (uint32_t)i * 2654435761u ^ seed;
@@ -183,13 +360,23 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const unsigned grid = (unsigned)(B * tiles_n);
-    const char* names[8] = {"full split product", "G loads skipped on odd K steps (intake -1/3)",
+    const int64_t tiles3 = (N + BN3 - 1) / BN3;
+    const char* names[13] = {"full split product", "G loads skipped on odd K steps (intake -1/3)",
                             "no loads after the first stage", "fragments read once (no per-step LDS reads)",
                             "one MFMA per block and step (loads + reads as full)",
                             "X^T loads skipped after the first stage (G every step)",
                             "G loads skipped after the first stage (X^T every step)",
-                            "X^T fragments into registers one step ahead, G by LDS-DMA"};
-    for (int mode = 0; mode < 8; ++mode) {
+                            "X^T fragments into registers one step ahead, G by LDS-DMA",
+                            "loads and barriers only (2-stage ring intake floor)",
+                            "192 x 192 tile, 3-stage ring, two stages in flight",
+                            "192 x 192 tile, 3-stage ring: loads and barriers only",
+                            "G two steps ahead (second barrier per step), X^T one step",
+                            "G two steps ahead: loads and barriers only"};
+    CK(hipFuncSetAttribute((const void*)probe3_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS3));
+    CK(hipFuncSetAttribute((const void*)probe3_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS3));
+    CK(hipFuncSetAttribute((const void*)probe_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES));
+    const int first = argc > 2 ? atoi(argv[2]) : 0;
+    for (int mode = first; mode < 13; ++mode) {
         auto launch = [&]() {
             switch (mode) {
                 case 0: probe_kernel<0><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
@@ -200,6 +387,11 @@ int main(int argc, char** argv) {
                 case 6: probe_kernel<6><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 case 7: probe_kernel<7><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 case 4: probe_kernel<4><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 8: probe_kernel<8><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 9: probe3_kernel<9><<<(unsigned)(B * tiles3), THREADS, LDS3>>>(Ah, Al, Bh, Bl, M, N, K, tiles3, C); break;
+                case 10: probe3_kernel<10><<<(unsigned)(B * tiles3), THREADS, LDS3>>>(Ah, Al, Bh, Bl, M, N, K, tiles3, C); break;
+                case 11: probe11_kernel<11><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
+                case 12: probe11_kernel<12><<<grid, THREADS, LDS_BYTES>>>(Ah, Al, Bh, Bl, M, N, K, tiles_n, C); break;
                 default: break;
             }
         };
