@@ -554,7 +554,7 @@ def jacobi_eigh(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-13, want6
 
 
 def extreme_eigs(T: torch.Tensor, steps: int = 40) -> torch.Tensor:
-    """T (B, p, p) fp64 symmetric, p <= 192 (not overwritten) -> (B, 2) fp64 [largest,
+    """T (B, p, p) fp64 symmetric, p <= 512 (not overwritten) -> (B, 2) fp64 [largest,
     smallest eigenvalue] by Lanczos + bisection (cq_extreme_eigs): the filter bounds of the
     solver's cheap outer iterations without a values-only eigensolve."""
     _require_hip(T)

@@ -48,12 +48,30 @@ __device__ __forceinline__ int gidx(int a, int c, int u, int p) {
     return g < p ? g : -1;
 }
 
+// 1 / x and 1 / sqrt(x) from the hardware seeds (v_rcp_f64, v_rsq_f64) and two Newton steps
+// each: ~1 ulp, without the correctly rounded division / square-root sequences (round 6:
+// the 32 rotations of a subproblem round are a serial step between two barriers)
+__device__ __forceinline__ double nr_rcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+    return __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+}
+__device__ __forceinline__ double nr_rsq(double x) {   // x >= 1 here
+    double y = __builtin_amdgcn_rsq(x);
+    y = __builtin_fma(0.5 * y, __builtin_fma(-x * y, y, 1.0), y);
+    return __builtin_fma(0.5 * y, __builtin_fma(-x * y, y, 1.0), y);
+}
+
+// the rotation that annihilates a_ij: th = (a_jj - a_ii) / (2 a_ij), t = sgn(th) / (|th| +
+// sqrt(1 + th^2)), c = 1 / sqrt(1 + t^2), s = t c (c^2 + s^2 = 1 to a few ulp: the rotation
+// stays orthogonal; the annihilation itself need not be exact)
 __device__ __forceinline__ void rot_params(double aii, double ajj, double aij, double thr, double& c, double& s) {
     c = 1.0; s = 0.0;
     if (fabs(aij) > 1e-300 && aij * aij > (thr * thr) * fabs(aii * ajj)) {
-        const double th = (ajj - aii) / (2.0 * aij);
-        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
-        c = 1.0 / sqrt(1.0 + t * t);
+        const double th = (ajj - aii) * nr_rcp(2.0 * aij);
+        const double q = 1.0 + th * th;   // (|th| > 1e100: t = 1 / (2 th), th^2 would overflow)
+        const double t = fabs(th) > 1e100 ? 0.5 * nr_rcp(th) : (th >= 0 ? 1.0 : -1.0) * nr_rcp(fabs(th) + q * nr_rsq(q));
+        c = nr_rsq(1.0 + t * t);
         s = t * c;
     }
 }

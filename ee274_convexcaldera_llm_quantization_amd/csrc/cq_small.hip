@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kWmThreads) void spd_whiten_mfma_kernel(double* __r
 // to the last bit of the bracket).  They approach S's extremes from inside, to ~1e-6 relative
 // after a few dozen steps even on flat spectra; a lost orthogonality only duplicates converged
 // values.  One workgroup per matrix, deterministic (fixed start vector, fixed sum orders).
-constexpr int kLzThreads = 256, kLzMaxP = 192, kLzMaxSteps = 64;
+constexpr int kLzThreads = 256, kLzMaxP = 192, kLzMaxPG = 512, kLzMaxSteps = 64;
 
 __device__ __forceinline__ int lz_sturm(const double* al, const double* b2, int m, double x) {
     int cnt = 0;
@@ -779,32 +779,40 @@ __device__ __forceinline__ int lz_sturm(const double* al, const double* b2, int 
     return cnt;
 }
 
+// Q: 64-row groups per lane (p <= 64 Q).  GT: p > 192, T is read in place (fp64, L2-resident
+// after the first step; S v from T's columns, the Rayleigh-Ritz matrix being symmetric to its
+// rounding) instead of an fp32 copy of S in LDS
+template <int Q, bool GT>
 __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* __restrict__ T_all, int p, int steps,
                                                                  double* __restrict__ ends) {
-    extern __shared__ __attribute__((aligned(16))) float lz_t[];   // S, p x p fp32 (row j at j p)
-    __shared__ float vf[kLzMaxP];                                  // current Lanczos vector (fp32 copy)
-    __shared__ float part[kLzThreads / 64][kLzMaxP];               // per-wave partial products
+    extern __shared__ __attribute__((aligned(16))) float lz_t[];   // S, p x p fp32 (row j at j p), !GT
+    __shared__ float vf[64 * Q];                                   // current Lanczos vector (fp32 copy)
+    __shared__ float part[kLzThreads / 64][64 * Q];                // per-wave partial products
     __shared__ double al[kLzMaxSteps], b2[kLzMaxSteps];            // alpha_k, beta_k^2
     __shared__ int m_s;
     const int64_t b = blockIdx.x;
     const double* T = T_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int e = tid; e < p * p; e += kLzThreads) lz_t[e] = (float)T[e];   // coalesced
-    __syncthreads();
-    for (int e = tid; e < p * p; e += kLzThreads) {   // S = (T + T^T) / 2, each pair once
-        const int j = e / p, i = e % p;
-        if (i < j) {
-            const float v = 0.5f * (lz_t[e] + lz_t[i * p + j]);
-            lz_t[e] = v;
-            lz_t[i * p + j] = v;
+    if constexpr (!GT) {
+        for (int e = tid; e < p * p; e += kLzThreads) lz_t[e] = (float)T[e];   // coalesced
+        __syncthreads();
+        for (int e = tid; e < p * p; e += kLzThreads) {   // S = (T + T^T) / 2, each pair once
+            const int j = e / p, i = e % p;
+            if (i < j) {
+                const float v = 0.5f * (lz_t[e] + lz_t[i * p + j]);
+                lz_t[e] = v;
+                lz_t[i * p + j] = v;
+            }
         }
     }
-    // wave 0 owns the vectors: lane l holds entries l, l + 64, l + 128 (fp64)
-    double v[3] = {0.0, 0.0, 0.0}, vp[3] = {0.0, 0.0, 0.0};
+    // wave 0 owns the vectors: lane l holds entries l + 64 q (fp64)
+    double v[Q], vp[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = vp[q] = 0.0;
     if (wid == 0) {
         double ss = 0.0;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < Q; ++q) {
             const int i = lane + 64 * q;
             if (i < p) {
                 uint32_t h = (uint32_t)i * 2654435761u ^ 0x9E3779B9u;
@@ -815,7 +823,7 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
         }
         const double inv = 1.0 / sqrt(wave_sum(ss));
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < Q; ++q) {
             v[q] *= inv;
             if (lane + 64 * q < p) vf[lane + 64 * q] = (float)v[q];
         }
@@ -825,45 +833,47 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
     const int jc = (p + 3) / 4, j0 = wid * jc, j1 = min(p, j0 + jc);
     double beta = 0.0;
     for (int k = 0; k < steps; ++k) {
-        // partial products of S v over this wave's rows j (S symmetric: column reads coalesce)
+        // partial products of S v over this wave's rows j (S symmetric: column reads coalesce);
+        // Q independent chains per lane (rows i = lane + 64 q; beyond p: row 0, unused), four
+        // rows j per step so the reads of several j are in flight
         {
-            // three independent chains per lane (rows i = lane + 64 q; beyond p: row 0, unused),
-            // four rows j per step so the LDS reads of several j are in flight
-            const int i0 = lane, i1 = lane + 64 < p ? lane + 64 : 0, i2 = lane + 128 < p ? lane + 128 : 0;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+            int ii[Q];
+            float a[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                ii[q] = lane + 64 * q < p ? lane + 64 * q : 0;
+                a[q] = 0.f;
+            }
             int j = j0;
             for (; j + 4 <= j1; j += 4) {
-                float t0[4], t1[4], t2[4], vj[4];
+                float t[4][Q], vj[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     vj[u] = vf[j + u];
-                    t0[u] = lz_t[(j + u) * p + i0];
-                    t1[u] = lz_t[(j + u) * p + i1];
-                    t2[u] = lz_t[(j + u) * p + i2];
+#pragma unroll
+                    for (int q = 0; q < Q; ++q)
+                        t[u][q] = GT ? (float)T[(int64_t)(j + u) * p + ii[q]] : lz_t[(j + u) * p + ii[q]];
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    a0 = __builtin_fmaf(t0[u], vj[u], a0);
-                    a1 = __builtin_fmaf(t1[u], vj[u], a1);
-                    a2 = __builtin_fmaf(t2[u], vj[u], a2);
-                }
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) a[q] = __builtin_fmaf(t[u][q], vj[u], a[q]);
             }
             for (; j < j1; ++j) {
                 const float vj = vf[j];
-                a0 = __builtin_fmaf(lz_t[j * p + i0], vj, a0);
-                a1 = __builtin_fmaf(lz_t[j * p + i1], vj, a1);
-                a2 = __builtin_fmaf(lz_t[j * p + i2], vj, a2);
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+                    a[q] = __builtin_fmaf(GT ? (float)T[(int64_t)j * p + ii[q]] : lz_t[j * p + ii[q]], vj, a[q]);
             }
-            if (i0 < p) part[wid][i0] = a0;
-            if (lane + 64 < p) part[wid][lane + 64] = a1;
-            if (lane + 128 < p) part[wid][lane + 128] = a2;
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                if (lane + 64 * q < p) part[wid][lane + 64 * q] = a[q];
         }
         __syncthreads();
-        int stop = 0;
         if (wid == 0) {
-            double w[3], a = 0.0;
+            double w[Q], a = 0.0;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < Q; ++q) {
                 const int i = lane + 64 * q;
                 w[q] = 0.0;
                 if (i < p) {
@@ -875,7 +885,7 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
             a = wave_sum(a);
             double ss = 0.0;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < Q; ++q) {
                 w[q] -= a * v[q];
                 ss += w[q] * w[q];
             }
@@ -886,11 +896,11 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
             }
             beta = sqrt(ss);
             // breakdown (an invariant subspace: its values are exact) or the last step
-            stop = !(beta > 1e-30 * fabs(a)) || k + 1 == steps;
+            const int stop = !(beta > 1e-30 * fabs(a)) || k + 1 == steps;
             if (stop && lane == 0) m_s = k + 1;
             const double inv = stop ? 0.0 : 1.0 / beta;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < Q; ++q) {
                 vp[q] = v[q];
                 v[q] = w[q] * inv;
                 if (lane + 64 * q < p) vf[lane + 64 * q] = (float)v[q];
@@ -1113,10 +1123,13 @@ int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int ns
 
 int cq_extreme_eigs(const double* T, int64_t p, int64_t batch, int steps, double* ends, void* stream) {
     CQ_REQUIRE(T && ends && p >= 2 && batch > 0 && batch <= 2147483647, "cq_extreme_eigs: bad args");
-    CQ_REQUIRE(p <= kLzMaxP, "cq_extreme_eigs: p > %d (the fp32 copy of T must fit the LDS)", kLzMaxP);
+    CQ_REQUIRE(p <= kLzMaxPG, "cq_extreme_eigs: p > %d", kLzMaxPG);
     CQ_REQUIRE(steps >= 1 && steps < kLzMaxSteps, "cq_extreme_eigs: steps must be in [1, %d)", kLzMaxSteps);
-    const size_t lds = (size_t)p * p * sizeof(float);
-    extreme_eigs_kernel<<<(unsigned)batch, kLzThreads, lds, as_stream(stream)>>>(T, (int)p, steps, ends);
+    hipStream_t s = as_stream(stream);
+    if (p <= kLzMaxP)   // S's fp32 copy in LDS
+        extreme_eigs_kernel<3, false><<<(unsigned)batch, kLzThreads, (size_t)p * p * sizeof(float), s>>>(T, (int)p, steps, ends);
+    else
+        extreme_eigs_kernel<8, true><<<(unsigned)batch, kLzThreads, 0, s>>>(T, (int)p, steps, ends);
     return check_launch("cq_extreme_eigs");
 }
 

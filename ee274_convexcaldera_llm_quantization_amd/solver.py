@@ -178,6 +178,7 @@ JACOBI_MAX_SWEEPS = 30
 BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
 BJ_SMALL_SUBPROBLEMS = 256  # batches with at most this many 64 x 64 block-Jacobi subproblems take it at every p
 STALL_RATIO = 0.98
+LATENCY_BATCH = 8  # batches up to this size (one caldera() call) take the latency-first variants
 VALUES_LANCZOS = 40  # Lanczos steps for the cheap iterations' filter bounds (0: values-only Jacobi)
 
 
@@ -207,9 +208,9 @@ class RankRSolver:
     def __init__(self, B: int, m: int, n: int, r: int, device, *, p: int | None = None,
                  tol: float = 1e-5, deg_cold=(6, 12, 12, 12, 12, 12, 12), deg_warm=(10, 7, 6, 6, 6, 6),
                  seed: int = 0x5EED, jacobi_tol: float = 1e-7, filter_precision: str = "f16x3",
-                 cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool = False,
+                 cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool | None = None,
                  jacobi_tol_values: float = 1e-2, criterion: str = "product",
-                 jacobi_values_sweeps: int = 30, values_lanczos: int | None = None):
+                 jacobi_values_sweeps: int = 30, values_lanczos: int | None = None, ns_second: bool | None = None):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -242,7 +243,7 @@ class RankRSolver:
         self.jacobi_values_sweeps = int(jacobi_values_sweeps)
         # the cheap iterations' filter bounds (the two ends of the Ritz spectrum) from this many
         # Lanczos steps on T (cq_extreme_eigs, one launch, no read-back) instead of a values-only
-        # eigensolve; 0: the eigensolve (p > 192 always: T's fp32 copy must fit one CU's LDS)
+        # eigensolve; 0: the eigensolve (p > 512 always)
         self.values_lanczos = int(VALUES_LANCZOS if values_lanczos is None else values_lanczos)
         self.refine = ()   # extra full outer iterations after convergence (per call; engine.py)
         self.X = None      # warm-start Ritz block (B, k, p)
@@ -284,7 +285,17 @@ class RankRSolver:
         # basis, so the G X product, Jacobi and rotations of that step are dropped.  Off by
         # default: measured at config 2 (B = 256) the stale bounds cost later warm calls a third
         # outer iteration (131 vs 121 G products per step, 243.6 vs 244.1 matrices/s)
-        self.skip_warm_cheap_rr = bool(skip_warm_cheap_rr)
+        # (None: on for latency batches, below)
+        self.latency = B <= LATENCY_BATCH
+        self.skip_warm_cheap_rr = self.latency if skip_warm_cheap_rr is None else bool(skip_warm_cheap_rr)
+        # CholQR2's second pass (and the final re-orthonormalisation) as Newton-Schulz steps
+        # X <- X (3 I - X^T X) / 2 (fp64 Gram, one fp32 product each) instead of a whitening: the
+        # block after one CholQR pass is orthonormal to ~eps32 cond(X) <= ~1e-2, two steps take that
+        # to the fp32 floor (error^2 per step) -- the same subspace without the whitening's chain of
+        # 32-pivot panels on one CU (0.2 ms at p = 192): for latency batches, where that chain is
+        # the critical path (one caldera() call), not for large ones (there the whitening costs
+        # less than the two Grams and products that replace it)
+        self.ns_second = self.latency if ns_second is None else bool(ns_second)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
@@ -367,6 +378,26 @@ class RankRSolver:
             K.gemm(X, Wt32, C=out, b_triu=True)  # Wt upper triangular (zeros stored)
         return out, info
 
+    def _ns(self, X, *keep, steps=2):
+        """Newton-Schulz re-orthonormalisation of a nearly orthonormal block (see ns_second)."""
+        self._halves_of = None
+        eye = None
+        for _ in range(steps):
+            out = self._free(X, *keep)
+            M = K.gram_f64(X, X)
+            if eye is None:
+                eye = torch.eye(self.p, dtype=torch.float64, device=X.device)
+            N = (1.5 * eye - 0.5 * M).float()
+            K.gemm(X, N, C=out)
+            X = out
+        return X, None
+
+    def _orth2(self, X, *keep, halves=False):
+        """CholQR2's second pass: CholQR, or Newton-Schulz steps for latency batches."""
+        if self.ns_second:
+            return self._ns(X, *keep)
+        return self._cholqr(X, *keep, halves=halves)
+
     def _rr(self, X, *keep, single=False, values_only=False):
         """Rayleigh-Ritz on the block X (generator: yields before the block Jacobi's read-backs).  single: Z = G X with one fp16 product (cheap outer
         iterations: the Ritz values only set the next filter's bounds, and the residuals it
@@ -388,7 +419,7 @@ class RankRSolver:
             K.gemm(G, X, ta=True, C=Z)  # Z = G X  (G symmetric: G^T's layout stages faster)
         self.stats.matvecs += 1
         T = K.gram_f64(X, Z)
-        if values_only and self.values_lanczos > 0 and self.p <= 192:
+        if values_only and self.values_lanczos > 0 and self.p <= 512:
             # only theta_0 and theta_{p-1} are read (filter bounds): Lanczos ends, the rest NaN
             ends = K.extreme_eigs(T, self.values_lanczos)
             theta = torch.full((self.B, self.p), math.nan, dtype=torch.float64, device=T.device)
@@ -637,7 +668,7 @@ class RankRSolver:
             if self.valid_k < k:  # zero-padded columns of W (engine.py): keep the block out of them
                 X[:, self.valid_k:, :] = 0.0
             X, _ = self._cholqr(X)
-            X, _ = self._cholqr(X, halves=True)
+            X, _ = self._orth2(X, halves=True)
             theta, X, Z = yield from self._rr(X, single=self.cheap_cold > 0, values_only=self.cheap_cold > 0)
             ends = torch.stack([theta[:, 0], theta[:, p - 1]], 1)
             yield
@@ -676,7 +707,7 @@ class RankRSolver:
                 coef = self._cheb_coeffs(ends, d, dev)
                 Xf = self._filter(X, coef, single=True)
                 Xa, _ = self._cholqr(Xf, X)
-                Xb, _ = self._cholqr(Xa, X)
+                Xb, _ = self._orth2(Xa, X)
                 ok = True
                 if self.x3:  # an fp16 overflow of a single-product iterate: redo this outer
                     ovf = self._ovf.max()  # iteration on the regular path below (fp32 fallback)
@@ -691,7 +722,7 @@ class RankRSolver:
                 coef = self._cheb_coeffs(ends, d, dev)
                 Xf = self._filter(X, coef, single=cheap)
                 Xa, _ = self._cholqr(Xf, X)
-                Xb, _ = self._cholqr(Xa, X, halves=True)
+                Xb, _ = self._orth2(Xa, X, halves=True)
                 theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
                 # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
                 # stopping test: estimated relative error of the rank-r projection of Y (a
@@ -787,8 +818,9 @@ class RankRSolver:
             theta, X, Z = yield from self._rr(X)
         self.stats.history.append((cold, used, list(self.stats.resid_hist)))
         # Ritz rotations are accumulated in fp32 by the Jacobi kernel (orthogonal to ~1e-6):
-        # one CholQR pass restores orthonormality without moving the converged subspace
-        X, _ = self._cholqr(X)
+        # one CholQR pass restores orthonormality without moving the converged subspace (latency
+        # batches: one Newton-Schulz step, error 1e-6 -> the fp32 floor)
+        X, _ = self._ns(X, steps=1) if self.ns_second else self._cholqr(X)
         # the final block becomes the warm start by a swap with the pool (no copy): X's pool
         # slot takes the previous warm-start buffer (a fresh one on the first call)
         i = next(j for j, t in enumerate(self._bufs) if t is X)

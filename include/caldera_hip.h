@@ -248,7 +248,8 @@ int cq_jacobi_eigh_staged(double* A, int64_t p, int64_t batch, int phase, int ns
  * overwritten): ends[2 b] = largest, ends[2 b + 1] = smallest eigenvalue, from `steps`
  * (1 <= steps < 64) Lanczos iterations and bisection on the Lanczos tridiagonal (approach the
  * true ends from inside; exact when the iteration breaks down on an invariant subspace).
- * p <= 192.  The rank-r solver's cheap outer iterations take their Chebyshev filter bounds
+ * p <= 512 (p > 192: T read in place, its upper and lower triangle taken as equal).  The
+ * rank-r solver's cheap outer iterations take their Chebyshev filter bounds
  * from it instead of a values-only eigensolve (the SVD replacement of alg.py:217). */
 int cq_extreme_eigs(const double* T, int64_t p, int64_t batch, int steps, double* ends, void* stream);
 

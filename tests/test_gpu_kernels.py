@@ -384,11 +384,12 @@ def test_jacobi_register_path_accuracy(K, p):
     assert torch.equal(V32.cpu().double(), V)
 
 
-@pytest.mark.parametrize("p", [8, 64, 128, 192])
+@pytest.mark.parametrize("p", [8, 64, 128, 192, 288, 384])   # > 192: T read in place from L2
 def test_extreme_eigs_lanczos(K, p):
     """cq_extreme_eigs, the filter bounds of the solver's cheap outer iterations: both ends of
     the spectrum approached from inside — to 5e-6 of the spread on Wishart spectra, inside a flat
-    top cluster (a Ritz-like spectrum, 1 + 1e-3 u) to its width; exact up to the fp32 copy of T
+    top cluster (a Ritz-like spectrum, 1 + 1e-3 u) to its width (its spread-out bottom to 1e-4);
+    exact up to the fp32 copy of T
     when p <= steps (the Lanczos iteration breaks down on the whole space); T untouched; a NaN
     gives NaN ends."""
     torch.manual_seed(5 + p)
@@ -412,7 +413,9 @@ def test_extreme_eigs_lanczos(K, p):
     exact = p <= 40
     for b in range(3):
         tol_hi = 5e-7 if exact else (2e-3 if b == 2 else 5e-6)
-        tol_lo = 5e-7 if exact else (1e-5 if b == 2 else 5e-6)
+        # (the Wishart bottom edge at p / N = 288 / 1024, 384 / 1024 is a slower Lanczos end:
+        # 40 steps reach 4e-5 / 5e-4 of the spread there -- ample for a filter cut)
+        tol_lo = 5e-7 if exact else (1e-4 if b == 2 else (5e-6 if p <= 192 else 2e-3))
         assert hi_err[b] < tol_hi and lo_err[b] < tol_lo, (b, hi_err[b].item(), lo_err[b].item())
 
 
