@@ -490,6 +490,7 @@ def run_model(args):
     for _ in range(args.steps):
         out = None
         out = step()
+    finish_gather()   # the last step's transfer is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -821,25 +822,40 @@ def main():
         # next step drops them, or the caching allocator grows and stalls on hipMalloc
         if world > 1:
             # N > 1: the one collective north_star names -- every rank's packed results
-            # (2-bit codes, L, R, scales, errors) gathered to rank 0 over RCCL (HBM -> HBM)
+            # (2-bit codes, L, R, scales, errors) gathered to rank 0 over RCCL (HBM -> HBM).
+            # Issued asynchronously: step i's transfer runs on the collective's stream under step
+            # i + 1's compute and is waited for before step i + 1 issues its own (the last one
+            # at the end of the timed region, inside it)
             from ee274_convexcaldera_llm_quantization_amd import sharding as S
             res = [S.MatrixResult(f"rank{rank}.m{j}", wl["m"], wl["n"], wl["rank"], wl["Q_bits"], d["codes"],
                                   d["Q_scale"], d["L"], d["R"], d["global_scale"], d["errors"])
                    for j, d in enumerate(pd for e in engines for pd in e.last_packed)]
-            torch.cuda.synchronize()
-            tg = time.perf_counter()
-            pl = S.gather_to_rank0(S.pack_results(res, device=dev), device=dev)
-            torch.cuda.synchronize()
-            gather_stats["ms"] += 1000.0 * (time.perf_counter() - tg)
+            payload = S.pack_results(res, device=dev)
+            finish_gather()
+            gather_stats["pending"] = S.gather_to_rank0_async(payload, device=dev,
+                                                              sizes=[payload.numel()] * world)
             gather_stats["calls"] += 1
-            gather_stats["bytes"] = 0 if pl is None else int(sum(x.numel() for x in pl))
-            gather_stats["ranks"] = 0 if pl is None else len(pl)
         return [d for o in outs for d in o], engines[0]
 
-    gather_stats = {"ms": 0.0, "calls": 0, "bytes": 0, "ranks": 0}
+    gather_stats = {"ms": 0.0, "calls": 0, "bytes": 0, "ranks": 0, "pending": None}
+
+    def finish_gather():
+        """Wait for the previous step's gather (the time the host blocks on it is its exposed
+        part: gather_ms_per_step)."""
+        pg = gather_stats["pending"]
+        if pg is None:
+            return
+        tg = time.perf_counter()
+        pl = pg.wait()
+        torch.cuda.synchronize()
+        gather_stats["ms"] += 1000.0 * (time.perf_counter() - tg)
+        gather_stats["bytes"] = 0 if pl is None else int(sum(x.numel() for x in pl))
+        gather_stats["ranks"] = 0 if pl is None else len(pl)
+        gather_stats["pending"] = None
 
     for _ in range(args.warmup):
         step()
+    finish_gather()
     torch.cuda.synchronize()
     if os.environ.get("CQ_BENCH_VERBOSE"):
         print(f"warmup done; reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
@@ -1038,6 +1054,9 @@ def main():
         result["gather"] = {"collective": "torch.distributed.gather (RCCL) of packed (codes, L, R) to rank 0",
                             "gathered_bytes_per_step": gather_stats["bytes"], "ranks": gather_stats["ranks"],
                             "gather_ms_per_step": gather_stats["ms"] / max(1, gather_stats["calls"]),
+                            "overlap": "step i's gather issued async on the collective's stream, waited for "
+                                       "before step i + 1 issues its own; gather_ms_per_step = the host's "
+                                       "wait on it (the exposed part); the last step's wait is timed",
                             "included_in_value": True}
     st = eng.solver.stats.as_dict() if eng.solver is not None else {}
     result["solver"] = {"parts": parts, "deg_cold": list(eng.solver.deg_cold) if eng.solver is not None else None,

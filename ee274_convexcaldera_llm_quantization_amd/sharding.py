@@ -169,6 +169,44 @@ def gather_to_rank0(payload: torch.Tensor, group=None, device=None, to_host: boo
     return [o.cpu() for o in out] if to_host else out
 
 
+class PendingGather:
+    """An issued gather_to_rank0_async: wait() -> rank 0's per-rank payloads (None elsewhere)."""
+
+    def __init__(self, work, gl, sizes, buf):
+        self.work, self.gl, self.sizes, self.buf = work, gl, sizes, buf
+
+    def wait(self):
+        self.work.wait()
+        self.buf = None
+        if self.gl is None:
+            return None
+        return [g[:n] for g, n in zip(self.gl, self.sizes)]
+
+
+def gather_to_rank0_async(payload: torch.Tensor, group=None, device=None, sizes=None) -> PendingGather:
+    """gather_to_rank0 issued asynchronously (the transfer runs on the collective's own stream
+    while the caller's stream computes on; the payload is copied into a send buffer first, so
+    the caller may free or reuse it).  sizes: every rank's payload size when the caller knows
+    them (same-size batches), which skips the blocking size exchange."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = device if device is not None else payload.device
+    if sizes is None:
+        n = torch.tensor([payload.numel()], dtype=torch.int64, device=dev)
+        st = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(st, n, group=group)
+        sizes = [int(x.item()) for x in st]
+    sizes = [int(x) for x in sizes]
+    assert len(sizes) == world and sizes[rank] == payload.numel(), "gather_to_rank0_async: sizes"
+    mx = max(sizes)
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    buf[: payload.numel()] = payload.to(dev)
+    gl = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+    work = dist.gather(buf, gather_list=gl, dst=0, group=group, async_op=True)
+    return PendingGather(work, gl, sizes, buf)
+
+
 def _plan(items, world: int, rank: int, max_batch: int, h_key=None, skip=()):
     """The batches rank `rank` decomposes: its round-robin shard grouped by shape (and h_key),
     in batches of <= max_batch.  Deterministic, so every rank can compute every rank's plan."""

@@ -240,3 +240,43 @@ def test_payload_magic_and_version_are_checked():
         S.unpack_results(torch.frombuffer(future, dtype=torch.uint8))
     with pytest.raises(ValueError):
         S.unpack_results(torch.zeros(3, dtype=torch.uint8))
+
+
+def _worker_async(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # two steps' payloads in flight at once (bench.py: step i's gather under step i + 1),
+        # one with the sizes given (no size exchange), one with ragged sizes exchanged
+        p1 = torch.arange(64, dtype=torch.int64).to(torch.uint8) + rank
+        p2 = torch.full((10 + 7 * rank,), 100 + rank, dtype=torch.uint8)
+        g1 = S.gather_to_rank0_async(p1, sizes=[64] * world)
+        g2 = S.gather_to_rank0_async(p2)
+        p1.zero_()   # the send buffers are copies: the caller may reuse its payload at once
+        o1, o2 = g1.wait(), g2.wait()
+        q.put((rank, None if o1 is None else [t.numpy().copy() for t in o1],
+               None if o2 is None else [t.numpy().copy() for t in o2]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gather_async_world2_gloo():
+    """gather_to_rank0_async (bench.py's N > 1 step gather, overlapped with the next step):
+    rank 0 receives every rank's payload in rank order, trimmed to its size; others get None."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_async, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = sorted([q.get(timeout=90) for _ in range(2)], key=lambda o: o[0])
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    (_, o1, o2), (_, n1, n2) = outs
+    assert n1 is None and n2 is None
+    for r in range(2):
+        assert o1[r].tolist() == [(i + r) % 256 for i in range(64)]
+        assert o2[r].tolist() == [100 + r] * (10 + 7 * r)
