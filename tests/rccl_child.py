@@ -1,7 +1,8 @@
 """Child process of tests/test_gpu_rccl.py: a world-1 "nccl" (RCCL) process group initialised
 before any other GPU call, then the sharded decomposition of two real matrices on the HIP
 engine, the packed payload gathered to rank 0 over RCCL (HBM -> HBM), and the gathered
-results compared byte for byte with the direct ones.  Prints one JSON line; exit code 0 = equal."""
+results compared byte for byte with the direct ones, and the same payload once more through the
+asynchronous gather bench.py's N > 1 steps use.  Prints one JSON line; exit code 0 = equal."""
 import json
 import os
 import sys
@@ -37,6 +38,16 @@ def main():
             for x, y in ((a.codes, b.codes), (a.L, b.L), (a.R, b.R)):
                 ok &= torch.equal(x.contiguous().view(-1).view(torch.uint8), y.contiguous().view(-1).view(torch.uint8))
             ok &= a.Q_scale == b.Q_scale and a.global_scale == b.global_scale and a.errors == b.errors
+        # the asynchronous form bench.py's N > 1 steps use (round 6): issued, the payload reused
+        # at once, compute queued behind it on the default stream, then retired stream-ordered
+        pk = S.pack_results(direct, device=dev)
+        ref = pk.clone()
+        pend = S.gather_to_rank0_async(pk, device=dev, sizes=[pk.numel()])
+        pk.zero_()
+        x = torch.randn(2048, 2048, device=dev)
+        y = x @ x   # noqa: F841  (compute beside the transfer)
+        got2 = pend.wait()
+        ok &= got2 is not None and len(got2) == 1 and torch.equal(got2[0], ref)
         torch.cuda.synchronize()
         print(json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "equal": bool(ok),
                           "payload_bytes": int(payloads[0].numel()), "matrices": len(got)}), flush=True)
