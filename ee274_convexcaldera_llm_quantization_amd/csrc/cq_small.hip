@@ -782,21 +782,21 @@ __device__ __forceinline__ int lz_sturm(const double* al, const double* b2, int 
 // Q: 64-row groups per lane (p <= 64 Q).  GT: p > 192, T is read in place (fp64, L2-resident
 // after the first step; S v from T's columns, the Rayleigh-Ritz matrix being symmetric to its
 // rounding) instead of an fp32 copy of S in LDS
-template <int Q, bool GT>
-__global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* __restrict__ T_all, int p, int steps,
-                                                                 double* __restrict__ ends) {
+template <int Q, bool GT, int NT>
+__global__ __launch_bounds__(NT) void extreme_eigs_kernel(const double* __restrict__ T_all, int p, int steps,
+                                                         double* __restrict__ ends) {
     extern __shared__ __attribute__((aligned(16))) float lz_t[];   // S, p x p fp32 (row j at j p), !GT
     __shared__ float vf[64 * Q];                                   // current Lanczos vector (fp32 copy)
-    __shared__ float part[kLzThreads / 64][64 * Q];                // per-wave partial products
+    __shared__ float part[NT / 64][64 * Q];                        // per-wave partial products
     __shared__ double al[kLzMaxSteps], b2[kLzMaxSteps];            // alpha_k, beta_k^2
     __shared__ int m_s;
     const int64_t b = blockIdx.x;
     const double* T = T_all + b * (int64_t)p * p;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if constexpr (!GT) {
-        for (int e = tid; e < p * p; e += kLzThreads) lz_t[e] = (float)T[e];   // coalesced
+        for (int e = tid; e < p * p; e += NT) lz_t[e] = (float)T[e];   // coalesced
         __syncthreads();
-        for (int e = tid; e < p * p; e += kLzThreads) {   // S = (T + T^T) / 2, each pair once
+        for (int e = tid; e < p * p; e += NT) {   // S = (T + T^T) / 2, each pair once
             const int j = e / p, i = e % p;
             if (i < j) {
                 const float v = 0.5f * (lz_t[e] + lz_t[i * p + j]);
@@ -830,7 +830,8 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
         if (lane == 0) m_s = steps;
     }
     __syncthreads();
-    const int jc = (p + 3) / 4, j0 = wid * jc, j1 = min(p, j0 + jc);
+    constexpr int NWV = NT / 64;
+    const int jc = (p + NWV - 1) / NWV, j0 = wid * jc, j1 = min(p, j0 + jc);
     double beta = 0.0;
     for (int k = 0; k < steps; ++k) {
         // partial products of S v over this wave's rows j (S symmetric: column reads coalesce);
@@ -877,7 +878,10 @@ __global__ __launch_bounds__(kLzThreads) void extreme_eigs_kernel(const double* 
                 const int i = lane + 64 * q;
                 w[q] = 0.0;
                 if (i < p) {
-                    w[q] = ((double)part[0][i] + (double)part[1][i]) + ((double)part[2][i] + (double)part[3][i]);
+                    double acc = 0.0;
+#pragma unroll
+                    for (int wv = 0; wv < NWV; ++wv) acc += (double)part[wv][i];
+                    w[q] = acc;
                     w[q] -= beta * vp[q];
                     a += w[q] * v[q];
                 }
@@ -1126,10 +1130,18 @@ int cq_extreme_eigs(const double* T, int64_t p, int64_t batch, int steps, double
     CQ_REQUIRE(p <= kLzMaxPG, "cq_extreme_eigs: p > %d", kLzMaxPG);
     CQ_REQUIRE(steps >= 1 && steps < kLzMaxSteps, "cq_extreme_eigs: steps must be in [1, %d)", kLzMaxSteps);
     hipStream_t s = as_stream(stream);
-    if (p <= kLzMaxP)   // S's fp32 copy in LDS
-        extreme_eigs_kernel<3, false><<<(unsigned)batch, kLzThreads, (size_t)p * p * sizeof(float), s>>>(T, (int)p, steps, ends);
+    // p <= 192: S's fp32 copy in LDS, four waves; above: T read in place by sixteen waves (a
+    // quarter of the rows each would leave each step's matvec latency-bound on L2), Q = the
+    // 64-row groups p needs
+    if (p <= kLzMaxP)
+        extreme_eigs_kernel<3, false, kLzThreads><<<(unsigned)batch, kLzThreads, (size_t)p * p * sizeof(float), s>>>(
+            T, (int)p, steps, ends);
+    else if (p <= 320)
+        extreme_eigs_kernel<5, true, 1024><<<(unsigned)batch, 1024, 0, s>>>(T, (int)p, steps, ends);
+    else if (p <= 384)
+        extreme_eigs_kernel<6, true, 1024><<<(unsigned)batch, 1024, 0, s>>>(T, (int)p, steps, ends);
     else
-        extreme_eigs_kernel<8, true><<<(unsigned)batch, kLzThreads, 0, s>>>(T, (int)p, steps, ends);
+        extreme_eigs_kernel<8, true, 1024><<<(unsigned)batch, 1024, 0, s>>>(T, (int)p, steps, ends);
     return check_launch("cq_extreme_eigs");
 }
 
