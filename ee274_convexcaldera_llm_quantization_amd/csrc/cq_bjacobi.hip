@@ -76,14 +76,17 @@ __device__ __forceinline__ void rot_params(double aii, double ajj, double aij, d
     }
 }
 
-__global__ __launch_bounds__(BT) void bj_init_kernel(double* __restrict__ A_all, int p, double* __restrict__ Vt_all,
+// NT threads per matrix: 256, or 1024 for small batches (one caldera() call: these one-matrix
+// passes over p^2 elements are memory-latency chains on one CU)
+template <int NT>
+__global__ __launch_bounds__(NT) void bj_init_kernel(double* __restrict__ A_all, int p, double* __restrict__ Vt_all,
                                                      int* __restrict__ done, int* __restrict__ sweeps,
                                                      double tol) {
     const int64_t b = blockIdx.x;
     double* A = A_all + b * (int64_t)p * p;
     __shared__ double red[16];
     double off = 0.0, dg = 0.0;
-    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += BT) {
+    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += NT) {
         const int i = (int)(t / p), c = (int)(t % p);
         if (Vt_all) Vt_all[b * (int64_t)p * p + t] = (i == c) ? 1.0 : 0.0;
         if (i < c) {  // symmetrise (Rayleigh-Ritz matrices carry rounding asymmetry)
@@ -371,19 +374,23 @@ __global__ void bj_check_kernel(const double* __restrict__ part_off, const doubl
 }
 
 // Descending eigenvalues by rank counting (ties by index); column rank(i) of V = Vt row i.
-__global__ __launch_bounds__(BT) void bj_finish_kernel(const double* __restrict__ A_all, int p,
+template <int NT>
+__global__ __launch_bounds__(NT) void bj_finish_kernel(const double* __restrict__ A_all, int p,
                                                        const double* __restrict__ Vt_all, double* __restrict__ evals,
                                                        float* __restrict__ V32, double* __restrict__ V64,
                                                        const int* __restrict__ sweeps, int* __restrict__ sweeps_out,
                                                        int* __restrict__ rank_ws) {
+    extern __shared__ double fdg[];   // the diagonal (p values): the ranks read it p times
     const int64_t b = blockIdx.x;
     const double* A = A_all + b * (int64_t)p * p;
     int* rk = rank_ws + b * (int64_t)p;
-    for (int i = threadIdx.x; i < p; i += BT) {
-        const double di = A[(int64_t)i * p + i];
+    for (int i = threadIdx.x; i < p; i += NT) fdg[i] = A[(int64_t)i * p + i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < p; i += NT) {
+        const double di = fdg[i];
         int r = 0;
         for (int j = 0; j < p; ++j) {
-            const double dj = A[(int64_t)j * p + j];
+            const double dj = fdg[j];
             r += (dj > di) || (dj == di && j < i);
         }
         evals[b * p + r] = di;
@@ -393,7 +400,7 @@ __global__ __launch_bounds__(BT) void bj_finish_kernel(const double* __restrict_
     if (!Vt_all) return;
     __syncthreads();
     const double* Vt = Vt_all + b * (int64_t)p * p;
-    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += BT) {
+    for (int64_t t = threadIdx.x; t < (int64_t)p * p; t += NT) {
         const int i = (int)(t / p), x = (int)(t % p);
         const double v = Vt[t];
         if (V32) V32[b * (int64_t)p * p + (int64_t)x * p + rk[i]] = (float)v;
@@ -450,7 +457,12 @@ int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double
     int* ranks = reinterpret_cast<int*>(take((size_t)batch * p * sizeof(int)));
     const double thr = fmax(1e-17, 0.5 * tol / sqrt((double)p));
     if (phase & BJ_BEGIN)
-        bj_init_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
+    {
+        if (batch < kCUs)
+            bj_init_kernel<1024><<<(unsigned)batch, 1024, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
+        else
+            bj_init_kernel<BT><<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, done, sweeps, tol);
+    }
     if (phase & BJ_SWEEPS) {
         for (int sw = 0; sw < nsweeps; ++sw) {
             for (int st = 0; st < nblk - 1; ++st) {
@@ -470,8 +482,15 @@ int bj_stage(double* A, int64_t p, int64_t batch, int phase, int nsweeps, double
         if (pending_out) bj_pending_kernel<<<1, 64, 0, s>>>(done, batch, pending_out);
     }
     if (phase & BJ_END)
-        bj_finish_kernel<<<(unsigned)batch, BT, 0, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64, sweeps,
-                                                         sweeps_out, ranks);
+    {
+        const size_t fl = (size_t)p * sizeof(double);
+        if (batch < kCUs)
+            bj_finish_kernel<1024><<<(unsigned)batch, 1024, fl, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64,
+                                                                     sweeps, sweeps_out, ranks);
+        else
+            bj_finish_kernel<BT><<<(unsigned)batch, BT, fl, s>>>(A, (int)p, want_v ? Vt : nullptr, evals, V32, V64,
+                                                                 sweeps, sweeps_out, ranks);
+    }
     return check_launch("cq_jacobi_eigh (block Jacobi)");
 }
 

@@ -179,6 +179,7 @@ BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
 BJ_SMALL_SUBPROBLEMS = 256  # batches with at most this many 64 x 64 block-Jacobi subproblems take it at every p
 STALL_RATIO = 0.98
 LATENCY_BATCH = 8  # batches up to this size (one caldera() call) take the latency-first variants
+SEGMENTS_MAX = 4  # filter segments per outer iteration at most (segment_capped; tools/tune_main.py: 1 -> 113, 3 -> 198, 4 -> 200, 6 -> 145, 16 -> 104 matrices/s on main.py's layer set)
 VALUES_LANCZOS = 40  # Lanczos steps for the cheap iterations' filter bounds (0: values-only Jacobi)
 
 
@@ -191,6 +192,7 @@ class SolverStats:
         self.bj_readbacks = 0        # block-Jacobi stage read-backs (one int each)
         self.stalls = 0              # matrices whose solve ended at the products' precision floor
         self.refines = 0             # refinement outer iterations run after convergence
+        self.segments = 0            # extra filter segments run (segment_capped), over the batch
         self.calls = 0
         self.max_resid = 0.0
         self.resid_hist = []
@@ -199,7 +201,8 @@ class SolverStats:
     def as_dict(self):
         return dict(outer=self.outer, matvecs=self.matvecs, calls=self.calls,
                     jacobi_unconverged=self.jacobi_unconverged, bj_readbacks=self.bj_readbacks, stalls=self.stalls,
-                    max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks, refines=self.refines)
+                    max_resid=self.max_resid, x3_fallbacks=self.x3_fallbacks, refines=self.refines,
+                    segments=self.segments)
 
 
 class RankRSolver:
@@ -210,7 +213,8 @@ class RankRSolver:
                  seed: int = 0x5EED, jacobi_tol: float = 1e-7, filter_precision: str = "f16x3",
                  cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool | None = None,
                  jacobi_tol_values: float = 1e-2, criterion: str = "product",
-                 jacobi_values_sweeps: int = 30, values_lanczos: int | None = None, ns_second: bool | None = None):
+                 jacobi_values_sweeps: int = 30, values_lanczos: int | None = None, ns_second: bool | None = None,
+                 segment_capped: bool = True):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -296,6 +300,10 @@ class RankRSolver:
         # the critical path (one caldera() call), not for large ones (there the whitening costs
         # less than the two Grams and products that replace it)
         self.ns_second = self.latency if ns_second is None else bool(ns_second)
+        # a requested filter degree the amplification cap cuts runs as several segments with a
+        # CholQR pass between them, inside one outer iteration (round 6; False: the cut degree
+        # and more outer iterations, as through round 5)
+        self.segment_capped = bool(segment_capped)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
@@ -470,17 +478,26 @@ class RankRSolver:
         check).  Returns a (deg, 3, B) fp32 device tensor: step i computes
         X_{i+1} = a_i G X_i + b_i X_{i-1} + c_i X_i."""
         ref = ends[:, 0]
-        c = np.maximum(ends[:, 1], 0.0)
-        ok = (c > 0) & (ref > c * (1 + 1e-6))
-        e = np.where(ok, c / 2.0, 1.0)
-        ctr = np.where(ok, c / 2.0, 0.0)
-        t0 = np.where(ok, (ref - ctr) / e, 2.0)
+        live = np.isfinite(ref) & (ref > 0)
+        # G is positive semi-definite: a Ritz value below 0 (or a few ulps of theta_0 above it) is
+        # the rounding of the products on a spectrum whose bottom is ~0 relative to its top -- a
+        # widely spread one -- so the damped interval ends just above 0 (the degree cap then holds
+        # the amplification); a flat block (theta_{p-1} ~ theta_0) damps [0, theta_0 / 2].  Either
+        # way the recurrence stays scaled to 1 at theta_0: unscaled, G's top (1e7 on an
+        # activation-weighted Y) overflows the iterates within a few steps.
+        c = np.where(live, np.maximum(ends[:, 1], ref * 1e-6), 0.0)
+        ok = live & (ref > c * (1 + 1e-6))
+        c = np.where(live & ~ok, ref / 2.0, c)
+        e = np.where(live, c / 2.0, 1.0)
+        ctr = np.where(live, c / 2.0, 0.0)
+        t0 = np.where(live, (ref - ctr) / e, 2.0)
         # per-matrix degree cap: the filter amplifies the top of the wanted band by up to
         # T_d(t0) against its bottom (~1); beyond ~1/eps of the products the wanted directions
         # near theta_r drown in the top ones and the block degenerates.  Widely spread spectra
         # (activation-weighted Y, theta_0/theta_r ~ 20 at config 3) thus get low degrees and more
         # outer iterations; near-flat ones (config 2, t0 ~ 1.6) keep the full schedule.
         cap = np.maximum(1, np.floor(np.arccosh(FILTER_MAX_AMP) / np.arccosh(np.maximum(t0, 1.0 + 1e-12))))
+        self._eff_deg = np.minimum(cap, deg).astype(np.int64)   # per matrix (segment_capped)
         deg = int(min(deg, cap.max()))
         s = 1.0 / t0
         rows = [(s / e, np.zeros_like(s), -s * ctr / e)]
@@ -493,17 +510,44 @@ class RankRSolver:
         tab = torch.from_numpy(np.asarray(rows, dtype=np.float64).astype(np.float32))
         return tab.to(dev)
 
-    def _filter(self, X, coef, single=False):
+    def _more_segments(self, Xf, X, d, coef, single):
+        """The segments after the first of an outer iteration's filter (segment_capped): matrix
+        b runs ceil(d / its capped degree) segments of its capped degree, each after a CholQR
+        pass; a matrix whose segments are done sits out the rest (its block is restored from
+        before the segment, and it passes through the filter), so its result does not depend on
+        its batch-mates' spectra.  Returns the filtered block."""
+        if not self.segment_capped:
+            return Xf
+        eff = np.maximum(self._eff_deg, 1)
+        segs = np.minimum(SEGMENTS_MAX, -(-d // eff))
+        dev = X.device
+        for j in range(1, int(segs.max())):
+            cont = segs > j
+            self.stats.segments += 1
+            Xs, _ = self._cholqr(Xf, X)
+            saved = None
+            if not cont.all():
+                saved = self._active.clone()
+                self._active.mul_(torch.from_numpy(cont.astype(np.int32)).to(dev))
+            Xn = self._filter(Xs, coef, single=single, keep=(X, Xf))
+            if saved is not None:
+                self._active.copy_(saved)
+                idx = torch.from_numpy(np.nonzero(~cont)[0]).to(dev)
+                Xn.index_copy_(0, idx, Xf.index_select(0, idx))
+            Xf = Xn
+        return Xf
+
+    def _filter(self, X, coef, single=False, keep=()):
         """X <- p_d(G) X, p_d = Chebyshev polynomial of degree d = len(coef) damping [0, c],
         c = theta_p, scaled to 1 at theta_0 (scaled 3-term recurrence).  Returns a buffer
         other than X's (X is left intact)."""
         if self.x3 and self._x3f:
-            return self._filter_x3(X, coef, single)
+            return self._filter_x3(X, coef, single, keep)
         G = self._G
         deg = coef.shape[0]
-        X0 = self._free(X)  # the recurrence overwrites its buffers: keep the input intact
+        X0 = self._free(X, *keep)  # the recurrence overwrites its buffers: keep the input intact
         X0.copy_(X)
-        Y1 = self._free(X, X0)
+        Y1 = self._free(X, X0, *keep)
         fl = 2.0 * self.k * self.k * self.p * self.B
         nb = float(self.B) * (4.0 * self.k * self.k + 16.0 * self.p * self.k)
         kn = "gemm_f32_kernel (fp32 G X, Chebyshev filter)"
@@ -521,7 +565,7 @@ class RankRSolver:
             prev, cur = cur, prev
         return cur
 
-    def _filter_x3(self, X, coef, single=False):
+    def _filter_x3(self, X, coef, single=False, keep=()):
         """Same recurrence on X^T with split-fp16 products (cq_gemm_x3; single: one fp16
         product per step); X is left intact."""
         deg = coef.shape[0]
@@ -541,7 +585,7 @@ class RankRSolver:
             kn = "gemm_x3v_kernel<1> (single fp16 product G X, Chebyshev filter)"
         probe = EVENT_PROBE.start
         # the last step also writes its result in X's own k x p layout (Ct): no transpose pass
-        out = self._free(X)
+        out = self._free(X, *keep)
         ct = out if TRANSPOSED_OUT else None
         last = deg == 1
         ev = probe(fl, nb, kn)
@@ -720,7 +764,15 @@ class RankRSolver:
                     continue
             while True:
                 coef = self._cheb_coeffs(ends, d, dev)
+                # a widely spread spectrum caps the degree (FILTER_MAX_AMP): in the full
+                # iterations the rest of the requested degree runs as further segments, each after
+                # a CholQR pass that re-conditions the block (the same subspace), instead of as
+                # further outer iterations with a Rayleigh-Ritz eigensolve and a read-back each.
+                # (Not in the cheap ones: their bounds are a cold block's or the previous call's,
+                # and a cold block's loose ends cap flat spectra too -- config 2's first iterations)
                 Xf = self._filter(X, coef, single=cheap)
+                if not cheap:
+                    Xf = self._more_segments(Xf, X, d, coef, cheap)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._orth2(Xa, X, halves=True)
                 theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
