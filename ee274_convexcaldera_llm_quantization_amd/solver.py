@@ -179,6 +179,13 @@ BJ_FIRST, BJ_MIN_FIRST, BJ_STEP = 6, 2, 2
 BJ_SMALL_SUBPROBLEMS = 256  # batches with at most this many 64 x 64 block-Jacobi subproblems take it at every p
 STALL_RATIO = 0.98
 LATENCY_BATCH = 8  # batches up to this size (one caldera() call) take the latency-first variants
+# B <= this (an outer iteration latency-bound: its eigensolve and read-back cost more than filter
+# products): a warm solve's cheap iteration is segmented too (its bounds are the previous call's
+# converged ones), and every segment runs the whole capped degree (above: the last one only the
+# rest of the requested degree).  tools/tune_main.py: main.py's layer set (batches of 7-14) 174 ->
+# 203 matrices/s with both, 189 with remainder segments; config 5 (B = 256) 93.5 whole, 95.1
+# remainder, 96.3 unsegmented; config 3 (B = 192) 219 with its warm cheap iteration segmented, 243 without
+SEGMENTS_SMALL_BATCH = 32
 SEGMENTS_MAX = 4  # filter segments per outer iteration at most (segment_capped; tools/tune_main.py: 1 -> 113, 3 -> 198, 4 -> 200, 6 -> 145, 16 -> 104 matrices/s on main.py's layer set)
 VALUES_LANCZOS = 40  # Lanczos steps for the cheap iterations' filter bounds (0: values-only Jacobi)
 
@@ -472,11 +479,13 @@ class RankRSolver:
         self.stats.bj_readbacks += 1 + (bj.swept - first + BJ_STEP - 1) // BJ_STEP
         return bj.finish()
 
-    def _cheb_coeffs(self, ends, deg, dev):
+    def _cheb_coeffs(self, ends, deg, dev, limit=None):
         """Coefficients of the scaled 3-term recurrence, from the host copy of the Ritz values
         ends = [(theta_0, theta_{p-1}) per matrix] (fp64, as read back at the convergence
         check).  Returns a (deg, 3, B) fp32 device tensor: step i computes
-        X_{i+1} = a_i G X_i + b_i X_{i-1} + c_i X_i."""
+        X_{i+1} = a_i G X_i + b_i X_{i-1} + c_i X_i.  limit: optional per-matrix degree bound
+        below the cap (a segment's remainder, _more_segments); the table then only sets
+        self._eff_deg when limit is None."""
         ref = ends[:, 0]
         live = np.isfinite(ref) & (ref > 0)
         # G is positive semi-definite: a Ritz value below 0 (or a few ulps of theta_0 above it) is
@@ -497,7 +506,10 @@ class RankRSolver:
         # (activation-weighted Y, theta_0/theta_r ~ 20 at config 3) thus get low degrees and more
         # outer iterations; near-flat ones (config 2, t0 ~ 1.6) keep the full schedule.
         cap = np.maximum(1, np.floor(np.arccosh(FILTER_MAX_AMP) / np.arccosh(np.maximum(t0, 1.0 + 1e-12))))
-        self._eff_deg = np.minimum(cap, deg).astype(np.int64)   # per matrix (segment_capped)
+        if limit is None:
+            self._eff_deg = np.minimum(cap, deg).astype(np.int64)   # per matrix (segment_capped)
+        else:
+            cap = np.minimum(cap, np.maximum(limit, 1))
         deg = int(min(deg, cap.max()))
         s = 1.0 / t0
         rows = [(s / e, np.zeros_like(s), -s * ctr / e)]
@@ -510,12 +522,12 @@ class RankRSolver:
         tab = torch.from_numpy(np.asarray(rows, dtype=np.float64).astype(np.float32))
         return tab.to(dev)
 
-    def _more_segments(self, Xf, X, d, coef, single):
+    def _more_segments(self, Xf, X, d, coef, single, ends):
         """The segments after the first of an outer iteration's filter (segment_capped): matrix
-        b runs ceil(d / its capped degree) segments of its capped degree, each after a CholQR
-        pass; a matrix whose segments are done sits out the rest (its block is restored from
-        before the segment, and it passes through the filter), so its result does not depend on
-        its batch-mates' spectra.  Returns the filtered block."""
+        b runs ceil(d / its capped degree) segments of its capped degree (the last one the
+        remainder of d), each after a CholQR pass; a matrix whose segments are done sits out the
+        rest (its block is restored from before the segment, and it passes through the filter),
+        so its result does not depend on its batch-mates' spectra.  Returns the filtered block."""
         if not self.segment_capped:
             return Xf
         eff = np.maximum(self._eff_deg, 1)
@@ -524,12 +536,17 @@ class RankRSolver:
         for j in range(1, int(segs.max())):
             cont = segs > j
             self.stats.segments += 1
+            # large batches: the last segment runs only the remainder of the requested degree
+            # (config 5: d = 12 capped at 7-11 -- a whole capped-degree segment there costs more
+            # than it gains); small ones keep whole segments (SEGMENTS_SMALL_BATCH)
+            rem = eff if self.B <= SEGMENTS_SMALL_BATCH else np.where(cont, np.minimum(d - j * eff, eff), eff)
+            cj = coef if (rem >= eff).all() else self._cheb_coeffs(ends, d, dev, limit=rem)
             Xs, _ = self._cholqr(Xf, X)
             saved = None
             if not cont.all():
                 saved = self._active.clone()
                 self._active.mul_(torch.from_numpy(cont.astype(np.int32)).to(dev))
-            Xn = self._filter(Xs, coef, single=single, keep=(X, Xf))
+            Xn = self._filter(Xs, cj, single=single, keep=(X, Xf))
             if saved is not None:
                 self._active.copy_(saved)
                 idx = torch.from_numpy(np.nonzero(~cont)[0]).to(dev)
@@ -750,6 +767,8 @@ class RankRSolver:
             if cheap and not cold and self.skip_warm_cheap_rr:
                 coef = self._cheb_coeffs(ends, d, dev)
                 Xf = self._filter(X, coef, single=True)
+                if B <= SEGMENTS_SMALL_BATCH:
+                    Xf = self._more_segments(Xf, X, d, coef, True, ends)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._orth2(Xa, X)
                 ok = True
@@ -771,8 +790,9 @@ class RankRSolver:
                 # (Not in the cheap ones: their bounds are a cold block's or the previous call's,
                 # and a cold block's loose ends cap flat spectra too -- config 2's first iterations)
                 Xf = self._filter(X, coef, single=cheap)
-                if not cheap:
-                    Xf = self._more_segments(Xf, X, d, coef, cheap)
+                # (a warm solve's cheap iteration too in small batches, SEGMENTS_SMALL_BATCH)
+                if not cheap or (not cold and B <= SEGMENTS_SMALL_BATCH):
+                    Xf = self._more_segments(Xf, X, d, coef, cheap, ends)
                 Xa, _ = self._cholqr(Xf, X)
                 Xb, _ = self._orth2(Xa, X, halves=True)
                 theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
