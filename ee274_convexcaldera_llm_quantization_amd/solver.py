@@ -221,7 +221,7 @@ class RankRSolver:
                  cheap_cold: int = 3, cheap_warm: int = 1, skip_warm_cheap_rr: bool | None = None,
                  jacobi_tol_values: float = 1e-2, criterion: str = "product",
                  jacobi_values_sweeps: int = 30, values_lanczos: int | None = None, ns_second: bool | None = None,
-                 segment_capped: bool = True):
+                 segment_capped: bool = True, cheap_one_pass: bool = False):
         self.B, self.m, self.n = B, m, n
         self.k = min(m, n)
         self.left = m <= n  # G = Y Y^T -> eigenvectors are left singular vectors
@@ -311,6 +311,9 @@ class RankRSolver:
         # CholQR pass between them, inside one outer iteration (round 6; False: the cut degree
         # and more outer iterations, as through round 5)
         self.segment_capped = bool(segment_capped)
+        # cheap (values-only) outer iterations: one CholQR pass instead of two -- the block only
+        # feeds the next filter and the two ends of a Lanczos spectrum (experiment, off)
+        self.cheap_one_pass = bool(cheap_one_pass)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, dev):
@@ -794,7 +797,7 @@ class RankRSolver:
                 if not cheap or (not cold and B <= SEGMENTS_SMALL_BATCH):
                     Xf = self._more_segments(Xf, X, d, coef, cheap, ends)
                 Xa, _ = self._cholqr(Xf, X)
-                Xb, _ = self._orth2(Xa, X, halves=True)
+                Xb = Xa if (cheap and self.cheap_one_pass) else self._orth2(Xa, X, halves=True)[0]
                 theta_n, Xn, Zn = yield from self._rr(Xb, X, single=cheap, values_only=cheap)
                 # (B,) per-matrix max residual; a cheap iteration cannot converge (see _rr)
                 # stopping test: estimated relative error of the rank-r projection of Y (a

@@ -5,7 +5,7 @@ import glob
 import sys
 
 d = sys.argv[1]
-f = glob.glob(f"{d}/t/**/run_kernel_trace.csv", recursive=True)[0]
+f = (glob.glob(f"{d}/t/**/run_kernel_trace.csv", recursive=True) or glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True))[0]
 rows = list(csv.DictReader(open(f)))
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:
