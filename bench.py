@@ -490,7 +490,7 @@ def run_model(args):
     for _ in range(args.steps):
         out = None
         out = step()
-    finish_gather(tail=True)   # the last step's transfer is inside the timed region
+    # (decompose_sharded gathers inside step(): its last batch's transfer is inside the region)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -312,7 +312,13 @@ class RankRSolver:
         # and more outer iterations, as through round 5)
         self.segment_capped = bool(segment_capped)
         # cheap (values-only) outer iterations: one CholQR pass instead of two -- the block only
-        # feeds the next filter and the two ends of a Lanczos spectrum (experiment, off)
+        # feeds the next filter and the two ends of a Lanczos spectrum, for which orthonormality
+        # to eps32 * cond(filtered block) is plenty (fp64 Gram).  Config 2: +1.7-2.0 % (320.9 ->
+        # 326.4, 323.3 -> 329.8 matrices/s), pinned / exact-LR / held-out parity at B = 256
+        # unchanged at 11/16, 15/16, 27/32 (tools/ab_solver_kw.py, profiles/r06ba_*, r06bb_*);
+        # NOT the default: at B = 64 (test_gpu_holdout.py) it moved the held-out classes from
+        # 27 / 29 / 1 miss to 28 / 28 / 2 misses (vs reference / vs exact LR / in no class,
+        # profiles/r06bc_gpu_suite.log) -- parity first
         self.cheap_one_pass = bool(cheap_one_pass)
 
     # ------------------------------------------------------------------ buffers

@@ -21,7 +21,7 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
-ROUND5 = dict(values_lanczos=0, ns_second=False, skip_warm_cheap_rr=False, segment_capped=False)
+ROUND5 = dict(values_lanczos=0, ns_second=False, skip_warm_cheap_rr=False, segment_capped=False, cheap_one_pass=False)
 
 
 def _run(W, h, **kw):
@@ -36,7 +36,7 @@ def test_solver_variants_match_round5_path(B, weighted):
     g = torch.Generator().manual_seed(61 + B + weighted)
     W = (torch.randn(B, 1024, 2048, generator=g) * 0.02).half().to(DEV)
     h = (torch.rand(2048, generator=g) + 0.05).to(DEV) if weighted else None
-    new, eng = _run(W, h, segment_capped=False)
+    new, eng = _run(W, h, segment_capped=False, cheap_one_pass=False)
     old, eng5 = _run(W, h, **ROUND5)
     sv = eng.solver
     assert sv.values_lanczos > 0 and sv.latency == (B <= 8)
