@@ -2,7 +2,7 @@
 # the filter launch average the bench line's HIP-event probe must agree with), one-part stats.
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/r06z
+O=${1:-gpurun_out/r06z}
 mkdir -p $O/kt $O/kt1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py > $O/bench_default_ktrace.log 2>&1
